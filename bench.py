@@ -1,0 +1,290 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: DDP toy training throughput (whole-node samples/s).
+
+Metric / config (BASELINE.json): "samples/sec (whole node) + DDP scaling eff.,
+toy MLP at 1/2/4/8 MI355X" on ``ddp_gpus_torchrun.py``'s job -- ``Linear(20, 1)``,
+``F.cross_entropy`` on float targets, ``SGD(lr=1e-2)``, per-device batch 32,
+2048-sample synthetic dataset, DistributedSampler sharding, DDP gradient
+all-reduce every step (reference ddp_gpus_torchrun.py:16-88). Weak scaling:
+per-GPU batch fixed, global batch 32*N.
+
+Contract: ``python bench.py --gpus N --steps K --warmup W`` (N>1 under
+``torch.distributed.run``); W untimed warmup steps (rounded up to whole
+epochs), then EXACTLY K timed steps bracketed by barrier + synchronize, the
+MAX elapsed over ranks, one JSON line from rank 0.
+
+Every timed step does the full work: batch gather by sampler index, forward,
+loss, backward, RCCL all-reduce of the gradient bucket across all ranks, SGD
+update; the sampler permutation of every epoch is generated on device inside
+the timed region. Engines:
+  fused     (default) fused step kernel + RCCL all-reduce, epochs captured into
+            hipGraphs (ops/fused_step.py)
+  autograd  native DDP reducer + native Linear/CE/SGD kernels, eager
+  reference stock PyTorch-ROCm loop (torch DDP, DataLoader + DistributedSampler,
+            nn.Linear, F.cross_entropy, torch.optim.SGD) -- the comparator
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import torch
+
+# BASELINE.md survey probe (unmodified reference loop, CPU/gloo, whole-node samples/s).
+# The reference publishes no GPU DDP number; see BASELINE.md.
+BASELINE_SAMPLES_PER_S = {1: 99_000.0, 2: 110_000.0, 4: 102_000.0}
+METRIC = "samples/sec (whole node) + DDP scaling eff., toy MLP at 1/2/4/8 MI355X"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--batch_size", type=int, default=32, help="per-device batch (reference default 32)")
+    ap.add_argument("--dataset_size", type=int, default=2048)
+    ap.add_argument("--lr", type=float, default=1e-2)
+    ap.add_argument("--model", default="linear", choices=["linear", "mlp"],
+                    help="linear = reference Linear(20,1)+soft CE; mlp = Linear(20,64)-ReLU-Linear(64,10)+CE")
+    ap.add_argument("--engine", default="fused", choices=["fused", "autograd", "reference"])
+    ap.add_argument("--graph_steps", type=int, default=128, help="target steps per captured hipGraph")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--out", default=None, help="also append the JSON line to this file")
+    return ap.parse_args(argv)
+
+
+def _setup(args):
+    from pytorch_distributed_training_tutorials_amd.parallel import env
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    env.init_process_group("nccl")
+    return env.rank(), env.world_size(), env.local_rank()
+
+
+def _build_model(args, dev):
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP, ddp_toy_model
+
+    torch.manual_seed(args.seed)
+    if args.model == "linear":
+        return ddp_toy_model(20, 1).to(dev), "ce_soft"
+    return ToyMLP(20, 64, 10).to(dev), "ce_index"
+
+
+def _dataset(args, dev, loss):
+    from pytorch_distributed_training_tutorials_amd.data import DeviceTensorDataset
+
+    if loss == "ce_soft":
+        return DeviceTensorDataset.synthetic_regression(args.dataset_size, 20, 1, device=dev, seed=args.seed)
+    return DeviceTensorDataset.synthetic_classification(args.dataset_size, 20, 10, device=dev, seed=args.seed)
+
+
+# --------------------------------------------------------------------------- fused
+def run_fused(args, rank, world, dev, comm):
+    from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+
+    model, loss = _build_model(args, dev)
+    ds = _dataset(args, dev, loss)
+    X, Y = ds.tensors
+    eng = FusedMLPStep(model, loss=loss, lr=args.lr, comm=comm)
+    if world > 1:
+        comm.broadcast(eng.P, 0)  # DDP init: rank 0's parameters everywhere
+    sampler = DeviceDistributedSampler(len(ds), world, rank, seed=args.seed, device=dev)
+    B = args.batch_size
+    ns = sampler.num_samples
+    S = math.ceil(ns / B)
+    batches = [(s * B, min(B, ns - s * B)) for s in range(S)]
+    idx = torch.zeros(ns, dtype=torch.int32, device=dev)
+    losses = torch.zeros(S, device=dev)
+
+    def epochs_fn(n_steps):
+        """n_steps from an epoch boundary: sampler at each epoch start, steps, final flush."""
+        def fn():
+            for g in range(n_steps):
+                j = g % S
+                if j == 0:
+                    sampler.generate(idx)
+                st, b = batches[j]
+                eng.step(X, Y, idx[st:st + b], b, losses[j:j + 1])
+            eng.flush()
+        return fn
+
+    m = max(1, round(args.graph_steps / S))
+    full = m * S
+    warm_steps = math.ceil(max(args.warmup, 1) / S) * S
+    graphs = {}
+
+    def get_graph(n):
+        if n not in graphs:
+            graphs[n] = eng.graph(epochs_fn(n), extra_state=(sampler._epoch, losses))
+        return graphs[n]
+
+    def schedule(n):
+        out = [full] * (n // full)
+        if n % full:
+            out.append(n % full)
+        return out
+
+    warm = schedule(warm_steps)
+    timed = schedule(args.steps)
+    for n in set(warm + timed):
+        get_graph(n)
+    sampler.set_epoch(0)
+    for n in warm:
+        get_graph(n).replay()
+    # timed region starts on an epoch boundary (warm_steps is a whole number of epochs)
+    t = _timed(comm, dev, lambda: [get_graph(n).replay() for n in timed])
+    extra = {"steps_per_epoch": S, "steps_per_graph": full, "warmup_steps_run": warm_steps,
+             "final_loss": float(losses[(args.steps - 1) % S].item()),
+             "kernels": "fused_mlp_step+rccl_allreduce per step, hipGraph"}
+    return t, extra
+
+
+# --------------------------------------------------------------------------- autograd
+def run_autograd(args, rank, world, dev, comm):
+    from pytorch_distributed_training_tutorials_amd.data import DeviceDataLoader, DistributedSampler
+    from pytorch_distributed_training_tutorials_amd.ops.loss import cross_entropy
+    from pytorch_distributed_training_tutorials_amd.ops.optim import FusedSGD
+    from pytorch_distributed_training_tutorials_amd.parallel.ddp import DistributedDataParallel
+
+    model, loss = _build_model(args, dev)
+    ds = _dataset(args, dev, loss)
+    loader = DeviceDataLoader(ds, batch_size=args.batch_size,
+                              sampler=DistributedSampler(ds, world, rank, seed=args.seed))
+    ddp = DistributedDataParallel(model, device_ids=[dev.index], comm=comm)
+    opt = FusedSGD(model.parameters(), lr=args.lr)
+    state = {"epoch": 0, "it": None}
+
+    def steps(n):
+        for _ in range(n):
+            batch = next(state["it"], None) if state["it"] is not None else None
+            if batch is None:
+                loader.set_epoch(state["epoch"])
+                state["epoch"] += 1
+                state["it"] = iter(loader)
+                batch = next(state["it"])
+            xs, ys = batch
+            ddp.zero_grad()
+            out = ddp(xs)
+            l = cross_entropy(out, ys)
+            l.backward()
+            opt.step()
+        return l
+
+    steps(max(args.warmup, 1))
+    t = _timed(comm, dev, lambda: steps(args.steps))
+    return t, {"kernels": "native DDP reducer + native linear/CE/SGD, eager"}
+
+
+# --------------------------------------------------------------------------- reference
+def run_reference(args, rank, world, dev, comm):
+    """Stock PyTorch-ROCm loop with the reference's structure (comparator)."""
+    import torch.nn.functional as F
+    from torch.nn.parallel import DistributedDataParallel as TorchDDP
+    from torch.utils.data import DataLoader, TensorDataset
+    from torch.utils.data.distributed import DistributedSampler as TorchSampler
+
+    torch.manual_seed(args.seed)
+    g = torch.Generator().manual_seed(args.seed)
+    if args.model == "linear":
+        ds = TensorDataset(torch.rand(args.dataset_size, 20, generator=g), torch.rand(args.dataset_size, 1, generator=g))
+        model = torch.nn.Linear(20, 1).to(dev)
+    else:
+        ds = TensorDataset(torch.randn(args.dataset_size, 20, generator=g),
+                           torch.randint(0, 10, (args.dataset_size,), generator=g))
+        model = torch.nn.Sequential(torch.nn.Linear(20, 64), torch.nn.ReLU(), torch.nn.Linear(64, 10)).to(dev)
+    sampler = TorchSampler(ds, num_replicas=world, rank=rank)
+    loader = DataLoader(ds, batch_size=args.batch_size, pin_memory=True, shuffle=False, sampler=sampler)
+    ddp = TorchDDP(model, device_ids=[dev.index])
+    opt = torch.optim.SGD(model.parameters(), lr=args.lr)
+    state = {"epoch": 0, "it": None}
+
+    def steps(n):
+        for _ in range(n):
+            batch = next(state["it"], None) if state["it"] is not None else None
+            if batch is None:
+                sampler.set_epoch(state["epoch"])
+                state["epoch"] += 1
+                state["it"] = iter(loader)
+                batch = next(state["it"])
+            xs, ys = batch
+            xs, ys = xs.to(dev), ys.to(dev)
+            opt.zero_grad()
+            l = F.cross_entropy(ddp(xs), ys)
+            l.backward()
+            opt.step()
+
+    steps(max(args.warmup, 1))
+    t = _timed(comm, dev, lambda: steps(args.steps))
+    return t, {"kernels": "stock torch: DataLoader+DistributedSampler, nn.Linear, F.cross_entropy, torch DDP, SGD"}
+
+
+# --------------------------------------------------------------------------- timing
+def _timed(comm, dev, fn):
+    comm.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize(dev)
+    comm.barrier()
+    t1 = time.perf_counter()
+    el = torch.tensor([t1 - t0], device=dev, dtype=torch.float64)
+    if comm.world > 1:
+        comm.all_reduce(el, "max")
+    return float(el.item())
+
+
+def main(argv=None):
+    args = parse(argv)
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU (MI355X)")
+    rank, world, local = _setup(args)
+    dev = torch.device("cuda", local)
+    from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+
+    comm = comm_mod.get_default(dev)
+    runner = {"fused": run_fused, "autograd": run_autograd, "reference": run_reference}[args.engine]
+    elapsed, extra = runner(args, rank, world, dev, comm)
+    gb = args.batch_size * world
+    samples = args.steps * gb
+    value = samples / elapsed
+    base = BASELINE_SAMPLES_PER_S.get(world)
+    rec = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / base, 3) if base else None,
+        "dtype": "fp32",
+        "data": "synthetic (uniform [0,1) features/targets generated on device, 2048 samples), random-init weights",
+        "config": {"model": "ddp_gpus_torchrun toy: Linear(20,1) + F.cross_entropy(soft targets) + SGD(lr=1e-2)"
+                   if args.model == "linear" else "toy MLP Linear(20,64)-ReLU-Linear(64,10) + CE + SGD",
+                   "global_batch": gb, "per_device_batch": args.batch_size, "seq_len": None,
+                   "dataset_size": args.dataset_size, "parallelism": f"dp{world}", "engine": args.engine},
+        "baseline_note": "vs_baseline divides by BASELINE.md's survey probe of the unmodified reference loop "
+                         "(CPU/gloo, same N); the reference publishes no GPU DDP number",
+        **extra,
+    }
+    if rank == 0:
+        line = json.dumps(rec)
+        print(line, flush=True)
+        if args.out:
+            with open(args.out, "a") as f:
+                f.write(line + "\n")
+    destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

@@ -1,0 +1,624 @@
+// Python bindings of the native layer: gfx950 kernels (csrc/kernels), the RCCL
+// communicator (csrc/comm) and the DDP reducer (csrc/reducer).
+//
+// Every kernel wrapper validates device/dtype/contiguity/shape on the host
+// before launching (a bad launch on MI355X can reset the whole node) and
+// launches on the caller's current HIP stream, so all of them are capturable
+// into hipGraphs via torch.cuda.graph.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "comm/rccl_comm.h"
+#include "kernels/kernels.h"
+#include "reducer/reducer.h"
+
+namespace py = pybind11;
+using at::Tensor;
+
+namespace ptdt {
+namespace {
+
+hipStream_t cur_stream(const Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+void hip_check(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, what, " failed: ", hipGetErrorString(e));
+}
+
+int dt_of(const Tensor& t) {
+  if (t.scalar_type() == at::kFloat) return kF32;
+  if (t.scalar_type() == at::kBFloat16) return kBF16;
+  TORCH_CHECK(false, "ptdt kernels support float32 and bfloat16, got ", t.scalar_type());
+  return -1;
+}
+
+void check_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+template <typename T>
+T* ptr_or_null(const c10::optional<Tensor>& t) {
+  return (t.has_value() && t->defined()) ? static_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+// ------------------------------------------------------------- fused step
+void fused_mlp_step_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<Tensor> Yi,
+                    c10::optional<Tensor> idx, Tensor P, Tensor G, c10::optional<Tensor> mom,
+                    c10::optional<Tensor> opt_step, Tensor loss_out, int64_t B, int64_t Din, int64_t H,
+                    int64_t Dout, int64_t loss_kind, int64_t ignore_index, bool has_bias,
+                    double grad_scale, bool accumulate, double pre_lr, double pre_momentum,
+                    double pre_dampening, double pre_weight_decay, bool pre_nesterov) {
+  check_gpu(X, "X");
+  check_gpu(P, "P");
+  check_gpu(G, "G");
+  TORCH_CHECK(X.scalar_type() == at::kFloat && P.scalar_type() == at::kFloat && G.scalar_type() == at::kFloat,
+              "fused_mlp_step: fp32 dataset/params/grads");
+  TORCH_CHECK(X.dim() == 2 && X.size(1) == Din, "fused_mlp_step: X must be [N, Din]");
+  const int64_t Dh = H > 0 ? H : Din;
+  const int64_t np = (H > 0 ? H * Din + (has_bias ? H : 0) : 0) + Dout * Dh + (has_bias ? Dout : 0);
+  TORCH_CHECK(P.numel() == np && G.numel() == np, "fused_mlp_step: flat param/grad size mismatch (want ",
+              np, ")");
+  TORCH_CHECK(loss_out.is_cuda() && loss_out.scalar_type() == at::kFloat && loss_out.numel() >= 1);
+  const int64_t N = X.size(0);
+  if (idx.has_value() && idx->defined()) {
+    check_gpu(*idx, "idx");
+    TORCH_CHECK(idx->scalar_type() == at::kInt && idx->numel() >= B, "idx must be int32 with >= B entries");
+  } else {
+    TORCH_CHECK(B <= N, "fused_mlp_step: B > N without indices");
+  }
+  if (loss_kind == kLossCEIndex) {
+    TORCH_CHECK(Yi.has_value() && Yi->defined() && Yi->scalar_type() == at::kLong && Yi->numel() == N,
+                "CE-index needs int64 labels [N]");
+    check_gpu(*Yi, "Yi");
+  } else {
+    TORCH_CHECK(Yf.has_value() && Yf->defined() && Yf->scalar_type() == at::kFloat && Yf->numel() == N * Dout,
+                "soft-CE/MSE need float targets [N, Dout]");
+    check_gpu(*Yf, "Yf");
+  }
+  if (mom.has_value() && mom->defined()) TORCH_CHECK(mom->numel() == np && mom->is_cuda());
+  TORCH_CHECK(fused_mlp_lds_bytes((int)B, (int)Din, (int)H, (int)Dout) <= 160 * 1024,
+              "fused_mlp_step: model/batch too large for one workgroup's LDS; use the layered path");
+  c10::hip::HIPGuard guard(X.device().index());
+  FusedMlpArgs a{};
+  a.X = X.data_ptr<float>();
+  a.Yf = ptr_or_null<const float>(Yf);
+  a.Yi = ptr_or_null<const int64_t>(Yi);
+  a.idx = ptr_or_null<const int32_t>(idx);
+  a.P = P.data_ptr<float>();
+  a.G = G.data_ptr<float>();
+  a.mom = ptr_or_null<float>(mom);
+  a.opt_step = ptr_or_null<int32_t>(opt_step);
+  a.loss_out = loss_out.data_ptr<float>();
+  a.B = (int)B; a.Din = (int)Din; a.H = (int)H; a.Dout = (int)Dout;
+  a.loss_kind = (int)loss_kind;
+  a.ignore_index = (int)ignore_index;
+  a.has_bias = has_bias ? 1 : 0;
+  a.grad_scale = (float)grad_scale;
+  a.accumulate = accumulate ? 1 : 0;
+  a.pre_lr = (float)pre_lr;
+  a.pre_momentum = (float)pre_momentum;
+  a.pre_dampening = (float)pre_dampening;
+  a.pre_weight_decay = (float)pre_weight_decay;
+  a.pre_nesterov = pre_nesterov ? 1 : 0;
+  hip_check(ptdt::fused_mlp_step(a, cur_stream(X)), "fused_mlp_step");
+}
+
+// ------------------------------------------------------------- optimizers
+void sgd_flat_(Tensor p, Tensor g, c10::optional<Tensor> mom, c10::optional<Tensor> step, double lr,
+               double momentum, double dampening, double wd, bool nesterov, double grad_scale) {
+  check_gpu(p, "param");
+  check_gpu(g, "grad");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat && p.numel() == g.numel());
+  c10::hip::HIPGuard guard(p.device().index());
+  hip_check(sgd_flat(p.data_ptr<float>(), g.data_ptr<float>(), ptr_or_null<float>(mom),
+                     ptr_or_null<int32_t>(step), p.numel(), (float)lr, (float)momentum, (float)dampening,
+                     (float)wd, nesterov, (float)grad_scale, cur_stream(p)),
+            "sgd_flat");
+}
+
+void adam_flat_(Tensor p, Tensor g, Tensor m, Tensor v, Tensor step, double lr, double b1, double b2,
+                double eps, double wd, bool decoupled, double grad_scale) {
+  check_gpu(p, "param");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && g.numel() == p.numel() && m.numel() == p.numel() &&
+              v.numel() == p.numel() && step.scalar_type() == at::kInt);
+  c10::hip::HIPGuard guard(p.device().index());
+  hip_check(adam_flat(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                      step.data_ptr<int32_t>(), p.numel(), (float)lr, (float)b1, (float)b2, (float)eps,
+                      (float)wd, decoupled, (float)grad_scale, cur_stream(p)),
+            "adam_flat");
+}
+
+template <typename F>
+void for_tensor_chunks(size_t n, F&& f) {
+  for (size_t s = 0; s < n; s += kMaxTensorsPerLaunch) f(s, std::min(n, s + (size_t)kMaxTensorsPerLaunch));
+}
+
+void sgd_multi_(std::vector<Tensor> ps, std::vector<Tensor> gs, std::vector<Tensor> moms,
+                c10::optional<Tensor> step, double lr, double momentum, double dampening, double wd,
+                bool nesterov, double grad_scale) {
+  if (ps.empty()) return;
+  TORCH_CHECK(ps.size() == gs.size() && (moms.empty() || moms.size() == ps.size()));
+  const int dt = dt_of(ps[0]);
+  c10::hip::HIPGuard guard(ps[0].device().index());
+  for_tensor_chunks(ps.size(), [&](size_t a, size_t b) {
+    TensorList tl{};
+    tl.n = (int)(b - a);
+    for (size_t i = a; i < b; ++i) {
+      check_gpu(ps[i], "param");
+      check_gpu(gs[i], "grad");
+      TORCH_CHECK(dt_of(ps[i]) == dt && gs[i].scalar_type() == ps[i].scalar_type() && gs[i].numel() == ps[i].numel());
+      tl.numel[i - a] = ps[i].numel();
+      tl.p[i - a] = ps[i].data_ptr();
+      tl.g[i - a] = gs[i].data_ptr();
+      tl.s1[i - a] = moms.empty() ? nullptr : moms[i].data_ptr<float>();
+      tl.s2[i - a] = nullptr;
+    }
+    hip_check(sgd_multi(tl, dt, ptr_or_null<int32_t>(step), (float)lr, (float)momentum, (float)dampening,
+                        (float)wd, nesterov, (float)grad_scale, cur_stream(ps[0])),
+              "sgd_multi");
+  });
+}
+
+void adam_multi_(std::vector<Tensor> ps, std::vector<Tensor> gs, std::vector<Tensor> ms,
+                 std::vector<Tensor> vs, Tensor step, double lr, double b1, double b2, double eps,
+                 double wd, bool decoupled, double grad_scale) {
+  if (ps.empty()) return;
+  TORCH_CHECK(ps.size() == gs.size() && ms.size() == ps.size() && vs.size() == ps.size());
+  const int dt = dt_of(ps[0]);
+  c10::hip::HIPGuard guard(ps[0].device().index());
+  for_tensor_chunks(ps.size(), [&](size_t a, size_t b) {
+    TensorList tl{};
+    tl.n = (int)(b - a);
+    for (size_t i = a; i < b; ++i) {
+      check_gpu(ps[i], "param");
+      check_gpu(gs[i], "grad");
+      TORCH_CHECK(dt_of(ps[i]) == dt && gs[i].numel() == ps[i].numel());
+      TORCH_CHECK(ms[i].scalar_type() == at::kFloat && vs[i].scalar_type() == at::kFloat);
+      tl.numel[i - a] = ps[i].numel();
+      tl.p[i - a] = ps[i].data_ptr();
+      tl.g[i - a] = gs[i].data_ptr();
+      tl.s1[i - a] = ms[i].data_ptr<float>();
+      tl.s2[i - a] = vs[i].data_ptr<float>();
+    }
+    hip_check(adam_multi(tl, dt, step.data_ptr<int32_t>(), (float)lr, (float)b1, (float)b2, (float)eps,
+                         (float)wd, decoupled, (float)grad_scale, cur_stream(ps[0])),
+              "adam_multi");
+  });
+}
+
+void bucket_copy(std::vector<Tensor> ts, Tensor flat, double scale, bool unpack) {
+  if (ts.empty()) return;
+  check_gpu(flat, "flat");
+  const int dt = dt_of(flat);
+  c10::hip::HIPGuard guard(flat.device().index());
+  int64_t off = 0;
+  for_tensor_chunks(ts.size(), [&](size_t a, size_t b) {
+    CopyList cl{};
+    cl.n = (int)(b - a);
+    for (size_t i = a; i < b; ++i) {
+      check_gpu(ts[i], "tensor");
+      TORCH_CHECK(ts[i].scalar_type() == flat.scalar_type());
+      cl.numel[i - a] = ts[i].numel();
+      cl.offset[i - a] = off;
+      cl.t[i - a] = ts[i].data_ptr();
+      off += ts[i].numel();
+    }
+    TORCH_CHECK(off <= flat.numel(), "bucket_copy: flat buffer too small");
+    hip_check(unpack ? bucket_unpack(cl, flat.data_ptr(), dt, (float)scale, cur_stream(flat))
+                     : bucket_pack(cl, flat.data_ptr(), dt, (float)scale, cur_stream(flat)),
+              "bucket_copy");
+  });
+}
+
+void scale_(Tensor x, double s) {
+  check_gpu(x, "x");
+  c10::hip::HIPGuard guard(x.device().index());
+  hip_check(scale_inplace(x.data_ptr(), x.numel(), dt_of(x), (float)s, cur_stream(x)), "scale_inplace");
+}
+
+// ------------------------------------------------------------- losses
+// returns (loss[1], lse_ws[3B], valid[1])
+std::vector<Tensor> ce_fwd(Tensor logits, c10::optional<Tensor> soft, c10::optional<Tensor> index,
+                           int64_t ignore_index, double label_smoothing) {
+  check_gpu(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2, "cross_entropy: logits must be [B, C]");
+  const int64_t B = logits.size(0), C = logits.size(1);
+  if (soft.has_value() && soft->defined()) {
+    check_gpu(*soft, "soft target");
+    TORCH_CHECK(soft->scalar_type() == at::kFloat && soft->numel() == B * C, "soft targets: float [B, C]");
+  } else {
+    TORCH_CHECK(index.has_value() && index->defined(), "cross_entropy: need soft or index targets");
+    check_gpu(*index, "index target");
+    TORCH_CHECK(index->scalar_type() == at::kLong && index->numel() == B, "index targets: int64 [B]");
+  }
+  c10::hip::HIPGuard guard(logits.device().index());
+  auto fopt = logits.options().dtype(at::kFloat);
+  Tensor loss = at::empty({}, fopt), lse = at::empty({3 * B}, fopt), valid = at::empty({1}, fopt);
+  hip_check(ce_forward(logits.data_ptr(), dt_of(logits), ptr_or_null<const float>(soft),
+                       ptr_or_null<const int64_t>(index), (int)B, (int)C, (int)ignore_index,
+                       (float)label_smoothing, loss.data_ptr<float>(), lse.data_ptr<float>(),
+                       valid.data_ptr<float>(), cur_stream(logits)),
+            "ce_forward");
+  return {loss, lse, valid};
+}
+
+Tensor ce_bwd(Tensor logits, c10::optional<Tensor> soft, c10::optional<Tensor> index, Tensor lse,
+              Tensor valid, c10::optional<Tensor> grad_out, int64_t ignore_index, double label_smoothing) {
+  check_gpu(logits, "logits");
+  const int64_t B = logits.size(0), C = logits.size(1);
+  c10::hip::HIPGuard guard(logits.device().index());
+  Tensor d = at::empty_like(logits);
+  hip_check(ce_backward(logits.data_ptr(), dt_of(logits), ptr_or_null<const float>(soft),
+                        ptr_or_null<const int64_t>(index), lse.data_ptr<float>(), valid.data_ptr<float>(),
+                        ptr_or_null<const float>(grad_out), (int)B, (int)C, (int)ignore_index,
+                        (float)label_smoothing, d.data_ptr(), cur_stream(logits)),
+            "ce_backward");
+  return d;
+}
+
+Tensor mse_fwd(Tensor x, Tensor y) {
+  check_gpu(x, "input");
+  check_gpu(y, "target");
+  TORCH_CHECK(x.numel() == y.numel() && x.scalar_type() == y.scalar_type(), "mse: shape/dtype mismatch");
+  c10::hip::HIPGuard guard(x.device().index());
+  Tensor ws = at::empty({1 + 1024}, x.options().dtype(at::kFloat));
+  hip_check(mse_forward(x.data_ptr(), y.data_ptr(), dt_of(x), x.numel(), ws.data_ptr<float>(), cur_stream(x)),
+            "mse_forward");
+  return ws.narrow(0, 0, 1).view({});
+}
+
+std::vector<Tensor> mse_bwd(Tensor x, Tensor y, c10::optional<Tensor> grad_out, bool need_dx, bool need_dy) {
+  check_gpu(x, "input");
+  check_gpu(y, "target");
+  c10::hip::HIPGuard guard(x.device().index());
+  Tensor dx = need_dx ? at::empty_like(x) : Tensor();
+  Tensor dy = need_dy ? at::empty_like(y) : Tensor();
+  hip_check(mse_backward(x.data_ptr(), y.data_ptr(), dt_of(x), x.numel(), ptr_or_null<const float>(grad_out),
+                         need_dx ? dx.data_ptr() : nullptr, need_dy ? dy.data_ptr() : nullptr, cur_stream(x)),
+            "mse_backward");
+  return {dx, dy};
+}
+
+// ------------------------------------------------------------- GEMM / Linear
+// C = alpha*A.B (+beta C) (+bias) (relu); A/B/C/mask are 2-D (possibly transposed views).
+void gemm_(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> bias, c10::optional<Tensor> amask, bool relu,
+           double alpha, double beta, c10::optional<Tensor> colsum, int64_t split_k) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm: GPU tensors");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm: 2-D operands");
+  TORCH_CHECK(A.size(1) == B.size(0) && C.size(0) == A.size(0) && C.size(1) == B.size(1), "gemm: shape mismatch ",
+              A.sizes(), " x ", B.sizes(), " -> ", C.sizes());
+  TORCH_CHECK(A.scalar_type() == B.scalar_type(), "gemm: A/B dtype mismatch");
+  GemmArgs g{};
+  g.M = (int)A.size(0);
+  g.N = (int)B.size(1);
+  g.K = (int)A.size(1);
+  g.A = A.data_ptr(); g.sam = A.stride(0); g.sak = A.stride(1);
+  g.B = B.data_ptr(); g.sbk = B.stride(0); g.sbn = B.stride(1);
+  g.C = C.data_ptr(); g.scm = C.stride(0); g.scn = C.stride(1);
+  g.in_dtype = dt_of(A);
+  g.out_dtype = dt_of(C);
+  if (bias.has_value() && bias->defined()) {
+    check_gpu(*bias, "bias");
+    TORCH_CHECK(bias->numel() == g.N, "gemm: bias must have N entries");
+    g.bias = bias->data_ptr();
+    g.bias_dtype = dt_of(*bias);
+  }
+  if (amask.has_value() && amask->defined()) {
+    TORCH_CHECK(amask->sizes() == A.sizes() && amask->scalar_type() == A.scalar_type(), "gemm: mask like A");
+    g.amask = amask->data_ptr(); g.smm = amask->stride(0); g.smk = amask->stride(1);
+  }
+  if (colsum.has_value() && colsum->defined()) {
+    check_gpu(*colsum, "colsum");
+    TORCH_CHECK(colsum->scalar_type() == at::kFloat && colsum->numel() == g.M, "gemm: colsum f32 [M]");
+    g.colsum_out = colsum->data_ptr<float>();
+  }
+  g.relu = relu ? 1 : 0;
+  g.alpha = (float)alpha;
+  g.beta = (float)beta;
+  g.split_k = (int)split_k;
+  c10::hip::HIPGuard guard(A.device().index());
+  hip_check(gemm(g, cur_stream(A)), "gemm");
+}
+
+Tensor relu_bwd(Tensor dy, Tensor y) {
+  check_gpu(dy, "dy");
+  check_gpu(y, "y");
+  c10::hip::HIPGuard guard(dy.device().index());
+  Tensor dx = at::empty_like(dy);
+  hip_check(relu_backward(dy.data_ptr(), y.data_ptr(), dx.data_ptr(), dt_of(dy), dy.numel(), cur_stream(dy)),
+            "relu_backward");
+  return dx;
+}
+
+void col_sum_(Tensor x, Tensor out, bool accumulate) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && out.scalar_type() == at::kFloat && out.numel() == x.size(1));
+  c10::hip::HIPGuard guard(x.device().index());
+  hip_check(col_sum(x.data_ptr(), dt_of(x), x.size(0), x.size(1), out.data_ptr<float>(), accumulate, cur_stream(x)),
+            "col_sum");
+}
+
+// ------------------------------------------------------------- data
+void philox_(Tensor out, int64_t seed, int64_t offset, int64_t dist) {
+  check_gpu(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kFloat);
+  c10::hip::HIPGuard guard(out.device().index());
+  hip_check(philox_fill(out.data_ptr<float>(), out.numel(), (uint64_t)seed, (uint64_t)offset, (int)dist,
+                        cur_stream(out)),
+            "philox_fill");
+}
+
+Tensor one_hot_(Tensor idx, int64_t C) {
+  check_gpu(idx, "idx");
+  TORCH_CHECK(idx.scalar_type() == at::kLong && idx.dim() == 1);
+  c10::hip::HIPGuard guard(idx.device().index());
+  Tensor out = at::empty({idx.size(0), C}, idx.options().dtype(at::kFloat));
+  hip_check(one_hot(idx.data_ptr<int64_t>(), out.data_ptr<float>(), (int)idx.size(0), (int)C, cur_stream(idx)),
+            "one_hot");
+  return out;
+}
+
+void gather_rows_(Tensor src, Tensor idx, Tensor out) {
+  check_gpu(src, "src");
+  check_gpu(idx, "idx");
+  check_gpu(out, "out");
+  TORCH_CHECK(idx.scalar_type() == at::kInt && out.scalar_type() == src.scalar_type());
+  TORCH_CHECK(src.dim() >= 1 && out.size(0) == idx.numel(), "gather_rows: out rows == idx count");
+  const int64_t cols = src.numel() / std::max<int64_t>(src.size(0), 1);
+  TORCH_CHECK(out.numel() == idx.numel() * cols);
+  c10::hip::HIPGuard guard(src.device().index());
+  hip_check(gather_rows(src.data_ptr(), idx.data_ptr<int32_t>(), out.data_ptr(), idx.numel(), cols,
+                        (int)src.element_size(), cur_stream(src)),
+            "gather_rows");
+}
+
+void device_sampler_(Tensor out, int64_t N, int64_t W, int64_t rank, int64_t num_samples, int64_t seed,
+                     Tensor epoch, bool shuffle) {
+  check_gpu(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kInt && out.numel() >= num_samples, "sampler out: int32 [num_samples]");
+  TORCH_CHECK(epoch.is_cuda() && epoch.scalar_type() == at::kInt && epoch.numel() == 1, "epoch: int32 [1] on GPU");
+  TORCH_CHECK(N > 0 && W > 0 && rank >= 0 && rank < W, "device_sampler: bad N/W/rank");
+  c10::hip::HIPGuard guard(out.device().index());
+  hip_check(device_sampler(out.data_ptr<int32_t>(), N, (int)W, (int)rank, num_samples, (uint64_t)seed,
+                           epoch.data_ptr<int32_t>(), shuffle ? 1 : 0, cur_stream(out)),
+            "device_sampler");
+}
+
+// ------------------------------------------------------------- int8
+std::vector<Tensor> quantize_int8(Tensor w) {
+  check_gpu(w, "weight");
+  TORCH_CHECK(w.dim() == 2);
+  c10::hip::HIPGuard guard(w.device().index());
+  Tensor q = at::empty(w.sizes(), w.options().dtype(at::kChar));
+  Tensor s = at::empty({w.size(0)}, w.options().dtype(at::kFloat));
+  hip_check(quantize_rowwise_int8(w.data_ptr(), dt_of(w), w.size(0), w.size(1), q.data_ptr<int8_t>(),
+                                  s.data_ptr<float>(), cur_stream(w)),
+            "quantize_int8");
+  return {q, s};
+}
+
+Tensor int8_linear(Tensor x, Tensor q, Tensor scale, c10::optional<Tensor> bias) {
+  check_gpu(x, "x");
+  check_gpu(q, "q");
+  TORCH_CHECK(x.dim() == 2 && q.dim() == 2 && x.size(1) == q.size(1) && q.scalar_type() == at::kChar);
+  TORCH_CHECK(scale.numel() == q.size(0));
+  if (bias.has_value() && bias->defined())
+    TORCH_CHECK(bias->numel() == q.size(0) && bias->scalar_type() == x.scalar_type());
+  c10::hip::HIPGuard guard(x.device().index());
+  Tensor y = at::empty({x.size(0), q.size(0)}, x.options());
+  hip_check(int8_weight_gemm(x.data_ptr(), dt_of(x), q.data_ptr<int8_t>(), scale.data_ptr<float>(),
+                             bias.has_value() && bias->defined() ? bias->data_ptr() : nullptr, (int)x.size(0),
+                             (int)q.size(0), (int)x.size(1), y.data_ptr(), dt_of(y), cur_stream(x)),
+            "int8_weight_gemm");
+  return y;
+}
+
+Tensor bn_relu(Tensor x, Tensor scale, Tensor shift, bool relu) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() >= 2);
+  const int64_t N = x.size(0), C = x.size(1);
+  const int64_t HW = x.numel() / std::max<int64_t>(N * C, 1);
+  TORCH_CHECK(scale.numel() == C && shift.numel() == C && scale.scalar_type() == at::kFloat);
+  c10::hip::HIPGuard guard(x.device().index());
+  Tensor y = at::empty_like(x);
+  hip_check(bn_relu_apply(x.data_ptr(), dt_of(x), scale.data_ptr<float>(), shift.data_ptr<float>(), N, C, HW,
+                          relu, y.data_ptr(), cur_stream(x)),
+            "bn_relu_apply");
+  return y;
+}
+
+// ------------------------------------------------------------- comm
+ncclDataType_t nccl_dt(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return ncclFloat32;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kHalf: return ncclFloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    case at::kChar: return ncclInt8;
+    case at::kByte: return ncclUint8;
+    default: TORCH_CHECK(false, "RcclComm: unsupported dtype ", t.scalar_type());
+  }
+  return ncclFloat32;
+}
+
+hipStream_t stream_arg(const Tensor& t, int64_t s) {
+  return s != 0 ? reinterpret_cast<hipStream_t>(s) : cur_stream(t);
+}
+
+}  // namespace
+}  // namespace ptdt
+
+PYBIND11_MODULE(_C, m) {
+  using namespace ptdt;
+  m.doc() = "MI355X-native kernels, RCCL communicator and DDP reducer";
+  m.attr("ARCH") = "gfx950";
+
+  m.def("fused_mlp_step", &fused_mlp_step_py, py::arg("X"), py::arg("Yf"), py::arg("Yi"), py::arg("idx"),
+        py::arg("P"), py::arg("G"), py::arg("mom"), py::arg("opt_step"), py::arg("loss_out"), py::arg("B"),
+        py::arg("Din"), py::arg("H"), py::arg("Dout"), py::arg("loss_kind"), py::arg("ignore_index"),
+        py::arg("has_bias"), py::arg("grad_scale"), py::arg("accumulate"), py::arg("pre_lr"),
+        py::arg("pre_momentum"), py::arg("pre_dampening"), py::arg("pre_weight_decay"), py::arg("pre_nesterov"));
+  m.def("fused_mlp_lds_bytes", [](int B, int Din, int H, int Dout) { return fused_mlp_lds_bytes(B, Din, H, Dout); });
+  m.def("sgd_flat_", &sgd_flat_);
+  m.def("adam_flat_", &adam_flat_);
+  m.def("sgd_multi_", &sgd_multi_);
+  m.def("adam_multi_", &adam_multi_);
+  m.def("bucket_copy", &bucket_copy);
+  m.def("scale_", &scale_);
+  m.def("ce_fwd", &ce_fwd);
+  m.def("ce_bwd", &ce_bwd);
+  m.def("mse_fwd", &mse_fwd);
+  m.def("mse_bwd", &mse_bwd);
+  m.def("gemm_", &gemm_, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias") = py::none(),
+        py::arg("amask") = py::none(), py::arg("relu") = false, py::arg("alpha") = 1.0, py::arg("beta") = 0.0,
+        py::arg("colsum") = py::none(), py::arg("split_k") = 1);
+  m.def("relu_bwd", &relu_bwd);
+  m.def("col_sum_", &col_sum_);
+  m.def("philox_", &philox_);
+  m.def("one_hot", &one_hot_);
+  m.def("gather_rows_", &gather_rows_);
+  m.def("device_sampler_", &device_sampler_);
+  m.def("quantize_int8", &quantize_int8);
+  m.def("int8_linear", &int8_linear);
+  m.def("bn_relu", &bn_relu);
+
+  m.def("plan_buckets", &plan_buckets);
+
+  py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")
+      .def_static("new_unique_id",
+                  []() {
+                    auto v = RcclComm::new_unique_id();
+                    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+                  })
+      .def(py::init([](int rank, int world, py::bytes uid, int device, double timeout_s, bool fingerprint) {
+             std::string s = uid;
+             std::vector<uint8_t> v(s.begin(), s.end());
+             py::gil_scoped_release nogil;
+             return std::make_shared<RcclComm>(rank, world, v, device, timeout_s, fingerprint);
+           }),
+           py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"), py::arg("timeout_s") = 600.0,
+           py::arg("fingerprint") = false)
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("world", &RcclComm::world)
+      .def_property_readonly("device", &RcclComm::device)
+      .def_property_readonly("seq", &RcclComm::seq)
+      .def("all_reduce",
+           [](RcclComm& c, Tensor t, int op, int64_t stream) {
+             TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "all_reduce: contiguous GPU tensor");
+             c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dt(t), (ncclRedOp_t)op, stream_arg(t, stream));
+           },
+           py::arg("t"), py::arg("op") = 0, py::arg("stream") = 0)
+      .def("broadcast",
+           [](RcclComm& c, Tensor t, int root, int64_t stream) {
+             TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "broadcast: contiguous GPU tensor");
+             c.broadcast(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dt(t), root, stream_arg(t, stream));
+           },
+           py::arg("t"), py::arg("root") = 0, py::arg("stream") = 0)
+      .def("reduce",
+           [](RcclComm& c, Tensor t, int root, int op, int64_t stream) {
+             TORCH_CHECK(t.is_cuda() && t.is_contiguous());
+             c.reduce(t.data_ptr(), t.data_ptr(), t.numel(), nccl_dt(t), (ncclRedOp_t)op, root, stream_arg(t, stream));
+           },
+           py::arg("t"), py::arg("root") = 0, py::arg("op") = 0, py::arg("stream") = 0)
+      .def("all_gather",
+           [](RcclComm& c, Tensor out, Tensor in, int64_t stream) {
+             TORCH_CHECK(out.is_cuda() && in.is_cuda() && out.is_contiguous() && in.is_contiguous());
+             TORCH_CHECK(out.numel() == in.numel() * c.world(), "all_gather: out must be world x in");
+             c.all_gather(in.data_ptr(), out.data_ptr(), in.numel(), nccl_dt(in), stream_arg(in, stream));
+           },
+           py::arg("out"), py::arg("inp"), py::arg("stream") = 0)
+      .def("reduce_scatter",
+           [](RcclComm& c, Tensor out, Tensor in, int op, int64_t stream) {
+             TORCH_CHECK(out.is_cuda() && in.is_cuda() && out.is_contiguous() && in.is_contiguous());
+             TORCH_CHECK(in.numel() == out.numel() * c.world(), "reduce_scatter: in must be world x out");
+             c.reduce_scatter(in.data_ptr(), out.data_ptr(), out.numel(), nccl_dt(in), (ncclRedOp_t)op,
+                              stream_arg(in, stream));
+           },
+           py::arg("out"), py::arg("inp"), py::arg("op") = 0, py::arg("stream") = 0)
+      .def("all_to_all",
+           [](RcclComm& c, Tensor out, Tensor in, int64_t stream) {
+             TORCH_CHECK(out.is_cuda() && in.is_cuda() && out.numel() == in.numel() && in.numel() % c.world() == 0);
+             c.all_to_all(in.data_ptr(), out.data_ptr(), in.numel() / c.world(), nccl_dt(in), stream_arg(in, stream));
+           },
+           py::arg("out"), py::arg("inp"), py::arg("stream") = 0)
+      .def("send",
+           [](RcclComm& c, Tensor t, int peer, int64_t stream) {
+             TORCH_CHECK(t.is_cuda() && t.is_contiguous());
+             c.send(t.data_ptr(), t.numel(), nccl_dt(t), peer, stream_arg(t, stream));
+           },
+           py::arg("t"), py::arg("peer"), py::arg("stream") = 0)
+      .def("recv",
+           [](RcclComm& c, Tensor t, int peer, int64_t stream) {
+             TORCH_CHECK(t.is_cuda() && t.is_contiguous());
+             c.recv(t.data_ptr(), t.numel(), nccl_dt(t), peer, stream_arg(t, stream));
+           },
+           py::arg("t"), py::arg("peer"), py::arg("stream") = 0)
+      .def("group_start", &RcclComm::group_start)
+      .def("group_end", &RcclComm::group_end)
+      .def("error", &RcclComm::error)
+      .def("abort", &RcclComm::abort)
+      .def_property_readonly("aborted", &RcclComm::aborted)
+      .def("fingerprints", &RcclComm::fingerprints);
+
+  py::class_<RcclClique, std::shared_ptr<RcclClique>>(m, "RcclClique")
+      .def(py::init<const std::vector<int>&>())
+      .def_property_readonly("size", &RcclClique::size)
+      .def("broadcast",
+           [](RcclClique& c, std::vector<Tensor> ts, int root) {
+             std::vector<void*> b;
+             std::vector<hipStream_t> s;
+             for (auto& t : ts) {
+               b.push_back(t.data_ptr());
+               s.push_back(cur_stream(t));
+             }
+             c.broadcast(b, ts.at(0).numel(), nccl_dt(ts.at(0)), root, s);
+           })
+      .def("reduce",
+           [](RcclClique& c, std::vector<Tensor> ts, int root) {
+             std::vector<void*> b;
+             std::vector<hipStream_t> s;
+             for (auto& t : ts) {
+               b.push_back(t.data_ptr());
+               s.push_back(cur_stream(t));
+             }
+             c.reduce(b, ts.at(0).numel(), nccl_dt(ts.at(0)), root, s);
+           })
+      .def("all_reduce", [](RcclClique& c, std::vector<Tensor> ts) {
+        std::vector<void*> b;
+        std::vector<hipStream_t> s;
+        for (auto& t : ts) {
+          b.push_back(t.data_ptr());
+          s.push_back(cur_stream(t));
+        }
+        c.all_reduce(b, ts.at(0).numel(), nccl_dt(ts.at(0)), s);
+      });
+
+  py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
+      .def(py::init([](std::vector<Tensor> params, std::vector<std::vector<int64_t>> buckets,
+                       std::shared_ptr<RcclComm> comm, py::object py_allreduce, bool find_unused) {
+             Reducer::PyAllReduce fn;
+             if (!py_allreduce.is_none()) {
+               fn = [py_allreduce](Tensor t) {
+                 py::gil_scoped_acquire g;
+                 py_allreduce(t);
+               };
+             }
+             return std::make_shared<Reducer>(std::move(params), std::move(buckets), std::move(comm), fn,
+                                              find_unused);
+           }),
+           py::arg("params"), py::arg("buckets"), py::arg("comm"), py::arg("py_allreduce"),
+           py::arg("find_unused") = false)
+      .def("prepare_for_backward", &Reducer::prepare_for_backward)
+      .def("mark_ready", &Reducer::mark_ready)
+      .def("finalize", &Reducer::finalize)
+      .def("rebuild", &Reducer::rebuild)
+      .def("ready_order", &Reducer::ready_order)
+      .def("buckets", &Reducer::buckets)
+      .def("bucket_tensors", &Reducer::bucket_tensors)
+      .def("zero_grads", &Reducer::zero_grads)
+      .def_property_readonly("iteration", &Reducer::iteration)
+      .def_property_readonly("in_backward", &Reducer::in_backward);
+}

@@ -1,0 +1,127 @@
+// Elementwise / reduction helpers (gfx950), all grid-stride with capped grids
+// (<= 2048 workgroups = 256 CUs x 8) and 16-byte vector accesses on the fp32
+// fast paths.
+#include "common.h"
+#include "kernels.h"
+
+namespace ptdt {
+namespace {
+
+constexpr int kBlock = 256;
+
+inline int grid_for(int64_t n, int per_thread = 4) {
+  int64_t g = (n + (int64_t)kBlock * per_thread - 1) / ((int64_t)kBlock * per_thread);
+  return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kBlock) relu_bwd_kernel(const T* dy, const T* y, T* dx, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+    Cvt<T>::store(dx, i, Cvt<T>::load(y, i) > 0.f ? Cvt<T>::load(dy, i) : 0.f);
+}
+
+// out[c] (+)= sum_r x[r, c]; one thread per column strip, rows split over blockIdx.y.
+template <typename T>
+__global__ void __launch_bounds__(kBlock) col_sum_kernel(const T* x, int64_t rows, int64_t cols,
+                                                         float* out, int rows_per) {
+  const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (c >= cols) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per;
+  const int64_t r1 = min(rows, r0 + rows_per);
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) s += Cvt<T>::load(x, r * cols + c);
+  atomicAdd(out + c, s);
+}
+
+__global__ void __launch_bounds__(kBlock) fill_kernel(float* x, float v, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) x[i] = v;
+}
+
+__global__ void __launch_bounds__(kBlock) f32_to_bf16_kernel(const float* x, uint16_t* y, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) y[i] = f32_to_bf16(x[i]);
+}
+__global__ void __launch_bounds__(kBlock) bf16_to_f32_kernel(const uint16_t* x, float* y, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) y[i] = bf16_to_f32(x[i]);
+}
+
+// y = relu?(x * scale[c] + shift[c]) over NCHW (flat grid-stride, c = (i / HW) % C).
+template <typename T>
+__global__ void __launch_bounds__(kBlock) bn_relu_kernel(const T* x, const float* scale,
+                                                         const float* shift, int64_t n, int64_t C,
+                                                         int64_t HW, int relu, T* y) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) {
+    const int c = (int)((i / HW) % C);
+    float v = fmaf(Cvt<T>::load(x, i), scale[c], shift[c]);
+    if (relu) v = fmaxf(v, 0.f);
+    Cvt<T>::store(y, i, v);
+  }
+}
+
+}  // namespace
+
+hipError_t relu_backward(const void* dy, const void* y, void* dx, int dtype, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  if (dtype == kF32)
+    hipLaunchKernelGGL(relu_bwd_kernel<float>, dim3(grid_for(n)), dim3(kBlock), 0, s,
+                       (const float*)dy, (const float*)y, (float*)dx, n);
+  else
+    hipLaunchKernelGGL(relu_bwd_kernel<uint16_t>, dim3(grid_for(n)), dim3(kBlock), 0, s,
+                       (const uint16_t*)dy, (const uint16_t*)y, (uint16_t*)dx, n);
+  return hipGetLastError();
+}
+
+hipError_t col_sum(const void* x, int dtype, int64_t rows, int64_t cols, float* out, int accumulate,
+                   hipStream_t s) {
+  if (cols <= 0) return hipSuccess;
+  if (!accumulate) PTDT_HIP_CHECK(hipMemsetAsync(out, 0, cols * sizeof(float), s));
+  if (rows <= 0) return hipSuccess;
+  const int gx = (int)((cols + kBlock - 1) / kBlock);
+  int gy = (int)((rows + 63) / 64);
+  if (gy > 1024) gy = 1024;
+  const int rows_per = (int)((rows + gy - 1) / gy);
+  if (dtype == kF32)
+    hipLaunchKernelGGL(col_sum_kernel<float>, dim3(gx, gy), dim3(kBlock), 0, s, (const float*)x, rows,
+                       cols, out, rows_per);
+  else
+    hipLaunchKernelGGL(col_sum_kernel<uint16_t>, dim3(gx, gy), dim3(kBlock), 0, s, (const uint16_t*)x,
+                       rows, cols, out, rows_per);
+  return hipGetLastError();
+}
+
+hipError_t fill_f32(float* x, float v, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, x, v, n);
+  return hipGetLastError();
+}
+
+hipError_t cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, x, y, n);
+  return hipGetLastError();
+}
+
+hipError_t cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(bf16_to_f32_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, x, y, n);
+  return hipGetLastError();
+}
+
+hipError_t bn_relu_apply(const void* x, int dtype, const float* scale, const float* shift, int64_t N,
+                         int64_t C, int64_t HW, int relu, void* y, hipStream_t s) {
+  const int64_t n = N * C * HW;
+  if (n <= 0) return hipSuccess;
+  if (dtype == kF32)
+    hipLaunchKernelGGL(bn_relu_kernel<float>, dim3(grid_for(n)), dim3(kBlock), 0, s, (const float*)x,
+                       scale, shift, n, C, HW, relu, (float*)y);
+  else
+    hipLaunchKernelGGL(bn_relu_kernel<uint16_t>, dim3(grid_for(n)), dim3(kBlock), 0, s,
+                       (const uint16_t*)x, scale, shift, n, C, HW, relu, (uint16_t*)y);
+  return hipGetLastError();
+}
+
+}  // namespace ptdt

@@ -1,0 +1,171 @@
+// Host-side launch API of every gfx950 kernel in this framework.
+//
+// The kernels are compiled by hipcc without any torch headers (fast, torch-ABI
+// independent); csrc/bindings.cpp wraps them for at::Tensor. Every launcher
+// takes an explicit hipStream_t and never allocates, copies host<->device or
+// synchronises, so all of them can be captured into a hipGraph.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ptdt {
+
+enum DType : int { kF32 = 0, kBF16 = 1 };
+
+// --------------------------------------------------------------------------
+// Fused small-MLP train step (csrc/kernels/fused_mlp.hip).
+//
+// One workgroup runs the whole per-rank step of a Linear[-ReLU-Linear] model
+// for the DDP toy workloads (reference ddp_gpus.py:34-39, Linear(20,1)+CE):
+// on-device batch gather by sampler indices -> forward -> loss -> backward ->
+// gradients written (pre-scaled by 1/world_size) straight into the flat DDP
+// bucket. Optionally it first applies the pending SGD update of the previous
+// step from the (already all-reduced) bucket ("deferred update"), which folds
+// the optimizer kernel into the next step's launch.
+enum LossKind : int { kLossCESoft = 0, kLossCEIndex = 1, kLossMSE = 2 };
+
+struct FusedMlpArgs {
+  const float* X;        // [N, Din] device-resident dataset
+  const float* Yf;       // [N, Dout] float targets (CE soft / MSE), or nullptr
+  const int64_t* Yi;     // [N] class indices (CE index), or nullptr
+  const int32_t* idx;    // [B] dataset rows of this step; nullptr => rows 0..B-1
+  float* P;              // flat params [W1 H*Din | b1 H | W2 Dout*H | b2 Dout]; H==0: [W Dout*Din | b Dout]
+  float* G;              // flat grads, same layout (the DDP bucket)
+  float* mom;            // SGD momentum buffer (same layout) or nullptr
+  int32_t* opt_step;     // device step counter for momentum init (may be nullptr)
+  float* loss_out;       // [1] mean loss of this step
+  int B, Din, H, Dout;
+  int loss_kind;
+  int ignore_index;      // CE index: rows with this label are skipped (torch default -100)
+  int has_bias;
+  float grad_scale;      // 1/world_size (DDP pre-division)
+  int accumulate;        // 1: G += grads (no_sync accumulation), 0: G = grads
+  // deferred SGD of the previous step (applied before the forward), lr<=0 disables
+  float pre_lr, pre_momentum, pre_dampening, pre_weight_decay;
+  int pre_nesterov;
+};
+hipError_t fused_mlp_step(const FusedMlpArgs& a, hipStream_t s);
+// LDS bytes the step needs (host check against the 160 KiB per-CU budget).
+size_t fused_mlp_lds_bytes(int B, int Din, int H, int Dout);
+
+// --------------------------------------------------------------------------
+// Optimizers on flat buffers and multi-tensor lists (csrc/kernels/optim.hip).
+// torch.optim.SGD semantics: d = g + wd*p; buf = (first ? d : mu*buf + (1-damp)*d);
+// d = nesterov ? d + mu*buf : buf; p -= lr*d.
+hipError_t sgd_flat(float* p, const float* g, float* mom, int32_t* step, int64_t n, float lr,
+                    float momentum, float dampening, float weight_decay, int nesterov,
+                    float grad_scale, hipStream_t s);
+// Adam/AdamW; step is a device counter already incremented for this step.
+hipError_t adam_flat(float* p, const float* g, float* m, float* v, const int32_t* step, int64_t n,
+                     float lr, float beta1, float beta2, float eps, float weight_decay,
+                     int decoupled, float grad_scale, hipStream_t s);
+
+constexpr int kMaxTensorsPerLaunch = 32;
+struct TensorList {
+  int n;                                   // tensors in this launch
+  int64_t numel[kMaxTensorsPerLaunch];
+  void* p[kMaxTensorsPerLaunch];           // param (f32 or bf16, see dtype)
+  const void* g[kMaxTensorsPerLaunch];     // grad (same dtype as param)
+  float* s1[kMaxTensorsPerLaunch];         // momentum / exp_avg (f32) or nullptr
+  float* s2[kMaxTensorsPerLaunch];         // exp_avg_sq (f32) or nullptr
+};
+hipError_t sgd_multi(const TensorList& tl, int dtype, int32_t* step, float lr, float momentum,
+                     float dampening, float weight_decay, int nesterov, float grad_scale,
+                     hipStream_t s);
+hipError_t adam_multi(const TensorList& tl, int dtype, const int32_t* step, float lr, float beta1,
+                      float beta2, float eps, float weight_decay, int decoupled, float grad_scale,
+                      hipStream_t s);
+// dst[i] = src_i * scale over a list (bucket pack) or the reverse (unpack).
+struct CopyList {
+  int n;
+  int64_t numel[kMaxTensorsPerLaunch];
+  int64_t offset[kMaxTensorsPerLaunch];    // element offset inside the flat buffer
+  void* t[kMaxTensorsPerLaunch];           // the per-parameter tensors
+};
+hipError_t bucket_pack(const CopyList& cl, void* flat, int dtype, float scale, hipStream_t s);
+hipError_t bucket_unpack(const CopyList& cl, const void* flat, int dtype, float scale, hipStream_t s);
+hipError_t scale_inplace(void* x, int64_t n, int dtype, float scale, hipStream_t s);
+
+// --------------------------------------------------------------------------
+// Losses (csrc/kernels/loss.hip). Row-wise log-softmax CE (soft or index
+// targets, mean reduction) and MSE mean. Forward writes the mean loss and the
+// per-row logsumexp; backward writes dlogits = g_out * dL/dlogits.
+hipError_t ce_forward(const void* logits, int dtype, const float* soft, const int64_t* index,
+                      int B, int C, int ignore_index, float label_smoothing, float* loss,
+                      float* lse, float* valid_count, hipStream_t s);
+hipError_t ce_backward(const void* logits, int dtype, const float* soft, const int64_t* index,
+                       const float* lse, const float* valid_count, const float* grad_out, int B,
+                       int C, int ignore_index, float label_smoothing, void* dlogits,
+                       hipStream_t s);
+hipError_t mse_forward(const void* x, const void* y, int dtype, int64_t n, float* loss,
+                       hipStream_t s);
+hipError_t mse_backward(const void* x, const void* y, int dtype, int64_t n, const float* grad_out,
+                        void* dx, void* dy, hipStream_t s);
+
+// --------------------------------------------------------------------------
+// GEMM on MFMA (csrc/kernels/gemm.hip).
+// C[M,N] = alpha * A[M,K] * B[K,N] (+ beta*C) (+ bias[N]) (ReLU), A and B addressed
+// by (row, col) strides so NN/NT/TN layouts need no transposed copies.
+// f32 operands use v_mfma_f32_32x32x2_f32 (exact fp32), bf16 operands
+// v_mfma_f32_16x16x32_bf16; accumulation is always fp32.
+struct GemmArgs {
+  int M, N, K;
+  const void* A; int64_t sam, sak;      // A(m,k) = A[m*sam + k*sak]
+  const void* B; int64_t sbk, sbn;      // B(k,n) = B[k*sbk + n*sbn]
+  void* C; int64_t scm, scn;            // C(m,n)
+  int in_dtype, out_dtype;
+  const void* bias;                     // [N] (in out_dtype precision rules: f32 or bf16), or nullptr
+  int bias_dtype;
+  const void* amask; int64_t smm, smk;  // optional ReLU mask on A: A(m,k) used only where mask(m,k) > 0
+  int relu;                             // ReLU epilogue
+  float alpha, beta;                    // beta!=0 reads C (accumulate)
+  float* colsum_out;                    // optional: colsum_out[m] += sum_k A(m,k) (masked) -> bias grads
+  int split_k;                          // >1: fp32 atomics into C (C must be f32 and pre-zeroed by caller)
+};
+hipError_t gemm(const GemmArgs& g, hipStream_t s);
+
+// Elementwise helpers (csrc/kernels/elementwise.hip)
+hipError_t relu_backward(const void* dy, const void* y, void* dx, int dtype, int64_t n, hipStream_t s);
+hipError_t col_sum(const void* x, int dtype, int64_t rows, int64_t cols, float* out, int accumulate,
+                   hipStream_t s);
+hipError_t fill_f32(float* x, float v, int64_t n, hipStream_t s);
+hipError_t cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
+hipError_t cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t s);
+
+// --------------------------------------------------------------------------
+// Synthetic data on device (csrc/kernels/rng.hip): counter-based Philox4x32-10.
+// dist 0 = uniform [0,1) (torch.rand-like), 1 = standard normal (Box-Muller).
+hipError_t philox_fill(float* out, int64_t n, uint64_t seed, uint64_t offset, int dist,
+                       hipStream_t s);
+// one_hot[b, idx[b]] = 1, zeros elsewhere (reference NB03:958 scatter_).
+hipError_t one_hot(const int64_t* idx, float* out, int B, int C, hipStream_t s);
+// out[i, :] = src[idx[i], :] (device batch gather of a resident dataset).
+hipError_t gather_rows(const void* src, const int32_t* idx, void* out, int64_t rows, int64_t cols,
+                       int elem_bytes, hipStream_t s);
+
+// Device-side DistributedSampler: out[i] = perm_e(rank + W*i mod N) for
+// i < num_samples, where perm_e is a keyed Feistel bijection of [0, N)
+// (cycle-walking) for epoch e. The epoch lives in device memory: the kernel
+// computes epoch = *epoch_ptr + 1 and stores it back, so a hipGraph holding
+// this kernel advances epochs by itself on every replay. Same sharding /
+// padding semantics as torch's DistributedSampler (different permutation).
+hipError_t device_sampler(int32_t* out, int64_t N, int W, int rank, int64_t num_samples, uint64_t seed,
+                          int32_t* epoch_ptr, int shuffle, hipStream_t s);
+
+// --------------------------------------------------------------------------
+// Int8 weight-only quantization + GEMM (csrc/kernels/int8.hip), LLM.int8-style
+// row-wise absmax (reference NB03:52-56 BitsAndBytesConfig(load_in_8bit)).
+hipError_t quantize_rowwise_int8(const void* w, int dtype, int64_t rows, int64_t cols, int8_t* q,
+                                 float* scale, hipStream_t s);
+// y[M,N] = x[M,K] (bf16/f32) * dequant(q[N,K])^T (+bias), i8 weights dequantised in LDS
+// into bf16 and multiplied on v_mfma_f32_16x16x32_bf16.
+hipError_t int8_weight_gemm(const void* x, int x_dtype, const int8_t* q, const float* scale,
+                            const void* bias, int M, int N, int K, void* y, int y_dtype,
+                            hipStream_t s);
+
+// BatchNorm(train stats applied) + ReLU fused epilogue over NCHW (csrc/kernels/elementwise.hip)
+hipError_t bn_relu_apply(const void* x, int dtype, const float* scale, const float* shift, int64_t N,
+                         int64_t C, int64_t HW, int relu, void* y, hipStream_t s);
+
+}  // namespace ptdt

@@ -1,0 +1,127 @@
+"""Native build driver: compiles csrc/ for gfx950 with hipcc into the in-tree
+extension ``pytorch_distributed_training_tutorials_amd/_C*.so``.
+
+No hipify, no torch JIT cache: every ``.hip`` kernel file is compiled with
+``hipcc --offload-arch=gfx950`` without torch headers (fast, ABI independent),
+the C++ runtime (RCCL communicator, reducer, bindings) with torch headers, and
+the objects are linked against the HIP/RCCL libraries torch itself ships (same
+sonames, so one copy of each runtime is loaded per process).
+
+Usage: ``python -m pytorch_distributed_training_tutorials_amd._build [--force] [-j N]``
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ARCH = "gfx950"
+PKG_DIR = Path(__file__).resolve().parent
+REPO = PKG_DIR.parent
+CSRC = REPO / "csrc"
+BUILD = REPO / "build" / "native"
+EXT_SUFFIX = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+TARGET = PKG_DIR / f"_C{EXT_SUFFIX}"
+
+
+def _hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and Path(c).exists():
+            return c
+    raise RuntimeError("hipcc not found (ROCm toolchain required to build the native extension)")
+
+
+def _torch_paths():
+    import torch  # noqa: F401  (import only for paths / ABI flag)
+    from torch.utils import cpp_extension as ce
+
+    tdir = Path(torch.__file__).resolve().parent
+    incs = [str(tdir / "include"), str(tdir / "include" / "torch" / "csrc" / "api" / "include")]
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    return incs, str(tdir / "lib"), abi, ce
+
+
+def _sources():
+    kernels = sorted((CSRC / "kernels").glob("*.hip"))
+    hosts = [CSRC / "comm" / "rccl_comm.cpp", CSRC / "reducer" / "reducer.cpp", CSRC / "bindings.cpp"]
+    return kernels, hosts
+
+
+def _headers():
+    return sorted(list(CSRC.rglob("*.h")))
+
+
+def _newer(src: Path, obj: Path, deps) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return src.stat().st_mtime > t or any(d.stat().st_mtime > t for d in deps)
+
+
+def _run(cmd):
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    if p.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{p.stdout}")
+    return p.stdout
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
+    hipcc = _hipcc()
+    incs, tlib, abi, _ = _torch_paths()
+    py_inc = sysconfig.get_paths()["include"]
+    BUILD.mkdir(parents=True, exist_ok=True)
+    kernels, hosts = _sources()
+    hdrs = _headers()
+    common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", f"-I{CSRC}", "-Wno-unused-result"]
+    host_flags = common + [
+        "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+        "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1", "-DHIPBLAS_V2",
+        f"-I{py_inc}", *[f"-I{i}" for i in incs], "-I/opt/rocm/include",
+        "-Wno-deprecated-declarations", "-Wno-unused-parameter",
+    ]
+    jobs = jobs or min(8, (os.cpu_count() or 2))
+    todo = []
+    objs = []
+    for src in kernels:
+        obj = BUILD / (src.stem + ".o")
+        objs.append(obj)
+        if force or _newer(src, obj, hdrs):
+            todo.append([hipcc, *common, "-c", str(src), "-o", str(obj)])
+    for src in hosts:
+        obj = BUILD / (src.stem + ".host.o")
+        objs.append(obj)
+        if force or _newer(src, obj, hdrs):
+            # host-only translation units: -x hip keeps hipcc's HIP headers/macros, no device code is emitted
+            todo.append([hipcc, *host_flags, "-x", "hip", "-c", str(src), "-o", str(obj)])
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+            for out in ex.map(_run, todo):
+                if verbose and out.strip():
+                    print(out)
+    relink = force or bool(todo) or not TARGET.exists() or any(o.stat().st_mtime > TARGET.stat().st_mtime for o in objs)
+    if relink:
+        tmp = TARGET.with_suffix(".tmp.so")
+        _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs),
+              f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
+              "-lrccl", "-lamdhip64", f"-Wl,-rpath,{tlib}", "-Wl,--no-as-needed"])
+        os.replace(tmp, TARGET)
+    return TARGET
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("-v", "--verbose", action="store_true")
+    a = ap.parse_args(argv)
+    out = build(force=a.force, jobs=a.jobs, verbose=a.verbose)
+    print(f"built {out}")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

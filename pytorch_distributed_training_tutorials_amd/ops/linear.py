@@ -1,0 +1,130 @@
+"""Linear layer on the native MFMA GEMM (csrc/kernels/gemm.hip).
+
+Reference call sites: ``torch.nn.Linear`` in every model of the reference
+(``ddp_gpus.py:81`` Linear(20,1); ``SampleModel`` Linear(32,2) NB01:168-175;
+``ToyModel`` Linear(10000,10)+ReLU+Linear(10,5) NB03:440-450; ResNet-50 ``fc``
+2048->1000 NB03:560). SURVEY K1/K3/K6/K8/K10/K11/K13.
+
+Forward  : y = act(x W^T + b)         -- one launch, bias + ReLU in the epilogue
+Backward : dx = (dy * relu'(y)) W      -- ReLU mask applied while staging dy
+           dW = (dy * relu'(y))^T x    -- same mask, bias grad = row sums of the
+           db = sum_rows(dy * relu'(y))   staged operand, fused in the dW launch
+Long-K / tiny-MN shapes (ToyModel's K=10000, M=20, N=10) run split-K over
+workgroups with fp32 atomics so the launch has enough workgroups to fill the
+chip instead of one workgroup walking 10000 columns.
+CPU tensors use ``torch.nn.functional.linear`` (plumbing tests only).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .._ext import native, use_native
+
+_KTILE = {torch.float32: 16, torch.bfloat16: 32}
+_CUS = 256
+
+
+def _split_k(M: int, N: int, K: int, dtype) -> int:
+    """Split K when the output tile grid cannot fill the chip and K is long."""
+    tiles = math.ceil(M / 64) * math.ceil(N / 64)
+    ktiles = math.ceil(K / _KTILE.get(dtype, 32))
+    if tiles >= 64 or ktiles < 8:
+        return 1
+    want = max(1, min(ktiles // 4, _CUS // tiles))
+    return int(want)
+
+
+def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor | None = None, *, bias=None, amask=None,
+         relu: bool = False, alpha: float = 1.0, beta: float = 0.0, colsum=None, out_dtype=None):
+    """C = alpha*A@B (+beta*C) (+bias) (relu) on MFMA, with optional split-K."""
+    M, K = A.shape
+    N = B.shape[1]
+    odt = out_dtype or (out.dtype if out is not None else A.dtype)
+    split = _split_k(M, N, K, A.dtype) if beta == 0.0 else 1
+    C = _ext_gemm(A, B, out, odt, bias, amask, relu, alpha, beta, colsum, split)
+    return C
+
+
+def _ext_gemm(A, B, out, odt, bias, amask, relu, alpha, beta, colsum, split):
+    C_ = native()
+    if split > 1:
+        acc = torch.zeros((A.shape[0], B.shape[1]), device=A.device, dtype=torch.float32)
+        C_.gemm_(A, B, acc, bias, amask, False, alpha, 0.0, colsum, split)
+        if relu:
+            acc.relu_()
+        if out is None:
+            return acc if odt == torch.float32 else acc.to(odt)
+        out.copy_(acc)
+        return out
+    if out is None:
+        out = torch.empty((A.shape[0], B.shape[1]), device=A.device, dtype=odt)
+    C_.gemm_(A, B, out, bias, amask, relu, alpha, beta, colsum, 1)
+    return out
+
+
+class _LinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu: bool):
+        shape = x.shape
+        x2 = x.reshape(-1, shape[-1])
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        y = gemm(x2, weight.t(), bias=bias, relu=relu, out_dtype=x.dtype)
+        ctx.relu = relu
+        ctx.has_bias = bias is not None
+        ctx.in_shape = shape
+        ctx.save_for_backward(x2, weight, y if relu else None)
+        return y.reshape(*shape[:-1], weight.shape[0])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, weight, y = ctx.saved_tensors
+        dy2 = dy.reshape(-1, weight.shape[0])
+        if not dy2.is_contiguous():
+            dy2 = dy2.contiguous()
+        mask = y if ctx.relu else None
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm(dy2, weight, amask=mask, out_dtype=x2.dtype).reshape(ctx.in_shape)
+        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+            colsum = None
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                colsum = torch.zeros(weight.shape[0], device=dy.device, dtype=torch.float32)
+            dw = gemm(dy2.t(), x2, amask=mask.t() if mask is not None else None, colsum=colsum,
+                      out_dtype=weight.dtype)
+            if colsum is not None:
+                db = colsum if weight.dtype == torch.float32 else colsum.to(weight.dtype)
+            if not ctx.needs_input_grad[1]:
+                dw = None
+        return dx, dw, db, None
+
+
+def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, relu: bool = False):
+    """``relu?(x @ weight.T + bias)``: native MFMA path on GPU, ATen on CPU."""
+    if use_native(x, weight):
+        if x.dtype not in (torch.float32, torch.bfloat16) or weight.dtype != x.dtype:
+            raise TypeError(f"native linear supports fp32/bf16 with matching dtypes, got {x.dtype}/{weight.dtype}")
+        return _LinearFn.apply(x, weight, bias, relu)
+    y = F.linear(x, weight, bias)
+    return F.relu(y) if relu else y
+
+
+class Linear(nn.Linear):
+    """Drop-in ``nn.Linear`` (same parameters, init and state_dict keys) whose
+    GPU forward/backward run on the native MFMA kernels; ``relu=True`` fuses
+    the activation into the epilogue."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, relu: bool = False,
+                 device=None, dtype=None):
+        super().__init__(in_features, out_features, bias=bias, device=device, dtype=dtype)
+        self.relu = relu
+
+    def forward(self, x):
+        return linear(x, self.weight, self.bias, self.relu)
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + (", relu=True" if self.relu else "")

@@ -1,0 +1,30 @@
+#!/bin/bash
+# GPU validation: tests, smoke, short bench runs, rocprofv3 stats.
+# Each GPU step has its own time limit; a crash/timeout (exit >= 124 or signal)
+# stops the script, plain test failures (exit 1) do not.
+cd "$(dirname "$0")/.." || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+ok() { local c=$1; [ "$c" -eq 0 ] || [ "$c" -eq 1 ]; }
+step() {  # name, seconds, cmd...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  local c=$?
+  echo "=== $name exit $c"; tail -5 "gpurun_out/$name.log"
+  if ! ok $c; then echo "STOP after $name (exit $c)"; exit $c; fi
+}
+STAGES=${STAGES:-"tests smoke bench prof"}
+for s in $STAGES; do
+  case $s in
+    tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench_fused 300 python bench.py --steps 2000 --warmup 200
+           step bench_autograd 300 python bench.py --engine autograd --steps 300 --warmup 50
+           step bench_reference 300 python bench.py --engine reference --steps 300 --warmup 50
+           step bench_mlp 300 python bench.py --model mlp --steps 2000 --warmup 200 ;;
+    prof)  cd /tmp && cd - >/dev/null
+           step prof_fused 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fused -o run -- python3 bench.py --steps 500 --warmup 64 ;;
+  esac
+done
+echo "=== done"
