@@ -265,7 +265,7 @@ Tensor mse_fwd(Tensor x, Tensor y) {
   Tensor ws = at::empty({1 + 1024}, x.options().dtype(at::kFloat));
   hip_check(mse_forward(x.data_ptr(), y.data_ptr(), dt_of(x), x.numel(), ws.data_ptr<float>(), cur_stream(x)),
             "mse_forward");
-  return ws.narrow(0, 0, 1).view({});
+  return ws.narrow(0, 0, 1).reshape({}).clone();
 }
 
 std::vector<Tensor> mse_bwd(Tensor x, Tensor y, c10::optional<Tensor> grad_out, bool need_dx, bool need_dy) {

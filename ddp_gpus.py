@@ -3,8 +3,9 @@
 Same entrypoint/CLI as the reference ``ddp_gpus.py``:
 ``python ddp_gpus.py --max_epochs 5 --batch_size 32``. ``world_size`` is the
 number of visible GPUs (``--nprocs`` overrides, e.g. CPU/gloo runs). Rendezvous
-on ``MASTER_ADDR=localhost``/``MASTER_PORT=12345`` like the reference
-(``PTDT_MASTER_PORT`` overrides; quirk Q6).
+on port 12345 like the reference (``PTDT_MASTER_PORT`` overrides, fixing quirk
+Q6) at 127.0.0.1 instead of ``localhost`` (the hostname may not resolve in
+containers; ``PTDT_MASTER_ADDR`` overrides).
 """
 import torch
 
@@ -15,7 +16,7 @@ from pytorch_distributed_training_tutorials_amd.parallel.launcher import spawn
 
 def main(rank: int, world_size: int, args):
     ddp_setup(rank, world_size)
-    run(args, rank if torch.cuda.is_available() else 0)
+    run(args, rank)
     destroy_process_group()
 
 

@@ -69,7 +69,7 @@ class DeviceDataLoader:
         idx = self.host_indices().to(torch.int32)
         dev = self.device
         if dev.type == "cuda":
-            if self._pinned is None or self._pinned.numel() < idx.numel():
+            if self._pinned is None or self._pinned[0].numel() < idx.numel():
                 self._pinned = [torch.empty(idx.numel(), dtype=torch.int32).pin_memory() for _ in range(2)]
                 self._pin_ev = [None, None]
                 self._pin_slot = 0

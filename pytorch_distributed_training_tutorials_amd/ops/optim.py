@@ -88,8 +88,8 @@ class FusedSGD(Optimizer):
                     self._cpu_step(ps, lr, mu, damp, wd, nest, gscale)
                     continue
                 grads = [p.grad for p in ps]
+                step = self._counter(gi, device)  # before creating buffers: "first step" is decided here
                 moms = self._momentum_buffers(gi, ps) if mu != 0.0 else []
-                step = self._counter(gi, device)
                 C = native()
                 pflat = contiguous_span([p.data for p in ps])
                 gflat = contiguous_span(grads)

@@ -104,7 +104,7 @@ def destroy_process_group() -> None:
         dist.destroy_process_group()
 
 
-def ddp_setup(rank: int | None = None, world_size: int | None = None, *, master_addr: str = "localhost",
+def ddp_setup(rank: int | None = None, world_size: int | None = None, *, master_addr: str = "127.0.0.1",
               master_port: str | int = "12345", backend: str | None = "nccl") -> None:
     """Both reference flavours in one call.
 

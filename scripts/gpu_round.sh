@@ -23,8 +23,9 @@ for s in $STAGES; do
            step bench_autograd 300 python bench.py --engine autograd --steps 300 --warmup 50
            step bench_reference 300 python bench.py --engine reference --steps 300 --warmup 50
            step bench_mlp 300 python bench.py --model mlp --steps 2000 --warmup 200 ;;
-    prof)  cd /tmp && cd - >/dev/null
-           step prof_fused 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_fused -o run -- python3 bench.py --steps 500 --warmup 64 ;;
+    prof)  step prof_fused 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fused -o run -- python3 bench.py --steps 500 --warmup 64
+           step prof_mlp 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_mlp -o run -- python3 bench.py --model mlp --steps 500 --warmup 64
+           step prof_reference 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_reference -o run -- python3 bench.py --engine reference --steps 200 --warmup 20 ;;
   esac
 done
 echo "=== done"

@@ -1,0 +1,78 @@
+"""DDP + communicator over gloo with world_size 2 (CPU plumbing)."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from pytorch_distributed_training_tutorials_amd.parallel.env import free_port
+from pytorch_distributed_training_tutorials_amd.parallel.launcher import spawn
+
+from . import _workers
+
+pytestmark = pytest.mark.slow
+
+
+def _load(d, w):
+    return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(w)]
+
+
+def test_ddp_matches_single_process_large_batch(tmp_path):
+    world = 2
+    spawn(_workers.ddp_equivalence, args=(world, free_port(), str(tmp_path), 0.0005), nprocs=world)
+    res = _load(tmp_path, world)
+    # ranks agree exactly
+    for a, b in zip(res[0]["params"], res[1]["params"]):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    # and equal a single process on the concatenated batch, starting from rank 0's init
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP
+
+    torch.manual_seed(100)
+    m = ToyMLP(20, 16, 5)
+    opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(4, 8 * world, 20, generator=g)
+    Y = torch.randint(0, 5, (4, 8 * world), generator=g)
+    for it in range(4):
+        opt.zero_grad()
+        F.cross_entropy(m(X[it]), Y[it]).backward()
+        opt.step()
+    for a, b in zip(res[0]["params"], m.parameters()):
+        torch.testing.assert_close(a, b.detach(), rtol=1e-5, atol=1e-6)
+    assert len(res[0]["buckets"]) >= 2  # tiny caps -> several buckets (rebuilt after iteration 0)
+    assert all(k.startswith("module.") for k in res[0]["keys"])
+
+
+def test_ddp_no_sync_and_find_unused(tmp_path):
+    world = 2
+    spawn(_workers.ddp_no_sync_and_unused, args=(world, free_port(), str(tmp_path)), nprocs=world)
+    res = _load(tmp_path, world)
+    # rank r contributes 3 micro-batches of x=(r+1): d(sum a(x))/dW = 2 rows * x per column
+    # rank-local accumulation 3*2*(r+1); the synced step averages the bucket (incl. accumulated grads)
+    expect = (3 * 2 * 1 + 3 * 2 * 2) / 2
+    torch.testing.assert_close(res[0]["ga"], torch.full((4, 4), expect))
+    torch.testing.assert_close(res[1]["ga"], res[0]["ga"])
+    assert (res[0]["gu"] == 0).all()
+
+
+def test_ddp_unused_parameter_error(tmp_path):
+    world = 2
+    spawn(_workers.ddp_missing_grad_raises, args=(world, free_port(), str(tmp_path)), nprocs=world)
+    assert all(r["raised"] for r in _load(tmp_path, world))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_communicator_collectives_gloo(tmp_path, world):
+    spawn(_workers.comm_collectives, args=(world, free_port(), str(tmp_path)), nprocs=world)
+    res = _load(tmp_path, world)
+    tot = sum(range(1, world + 1))
+    for r, d in enumerate(res):
+        torch.testing.assert_close(d["sum"], torch.full((3,), float(tot)))
+        torch.testing.assert_close(d["avg"], torch.full((3,), tot / world))
+        torch.testing.assert_close(d["max"], torch.full((3,), float(world)))
+        torch.testing.assert_close(d["bcast"], torch.zeros(2))
+        torch.testing.assert_close(d["gather"], torch.tensor([v for q in range(world) for v in (q, q * 10.0)]))
+        torch.testing.assert_close(d["rs"], torch.tensor([2.0 * r, 2.0 * r + 1]) * world)
+        torch.testing.assert_close(d["a2a"], torch.tensor([r + 100.0 * q for q in range(world)]))
+        assert d["obj"] == {"r": 0}
+    torch.testing.assert_close(res[1]["p2p"], torch.tensor([42.0]))

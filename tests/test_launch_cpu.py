@@ -1,0 +1,108 @@
+"""Launchers, entrypoints, status lines, fault injection and checkpoint/resume (CPU/gloo)."""
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from pytorch_distributed_training_tutorials_amd.parallel.env import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.slow
+
+
+def _env(**kw):
+    e = dict(os.environ)
+    e["PYTHONPATH"] = ROOT + os.pathsep + e.get("PYTHONPATH", "")
+    e.update({k: str(v) for k, v in kw.items()})
+    return e
+
+
+def _run(cmd, timeout=240, **env):
+    return subprocess.run(cmd, cwd=ROOT, env=_env(**env), capture_output=True, text=True, timeout=timeout)
+
+
+STATUS = re.compile(r"\[GPU: (\d+) Epoch: (\d+), Batch size: (\d+) \| Steps (\d+)\]")
+
+
+def test_ddp_gpus_spawn_status_lines():
+    p = _run([sys.executable, "ddp_gpus.py", "--max_epochs", "2", "--batch_size", "32", "--nprocs", "2"],
+             PTDT_MASTER_PORT=free_port())
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = STATUS.findall(p.stdout)
+    assert sorted(lines) == sorted([(str(r), str(e), "32", "32") for r in range(2) for e in range(2)])
+
+
+def test_torchrun_script_via_our_launcher_env_contract():
+    port = free_port()
+    p = _run([sys.executable, "-m", "pytorch_distributed_training_tutorials_amd.launch", "--nproc-per-node", "2",
+              "--master-port", str(port), "ddp_gpus_torchrun.py", "--max_epochs", "1"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert sorted(STATUS.findall(p.stdout)) == [("0", "0", "32", "32"), ("1", "0", "32", "32")]
+    assert "OMP_NUM_THREADS" in p.stderr  # torchrun's warning when nproc > 1
+
+
+def test_torchrun_default_single_worker_steps_64():
+    """NB02:268-272: torchrun without --nproc-per-node -> W=1 -> Steps 64."""
+    p = _run([sys.executable, "-m", "pytorch_distributed_training_tutorials_amd.launch", "--master-port",
+              str(free_port()), "ddp_gpus_torchrun.py", "--max_epochs", "1"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert STATUS.findall(p.stdout) == [("0", "0", "32", "64")]
+
+
+def test_launcher_env_contract(tmp_path):
+    script = tmp_path / "envdump.py"
+    script.write_text("import os, json\nkeys=['RANK','LOCAL_RANK','WORLD_SIZE','LOCAL_WORLD_SIZE','GROUP_RANK',"
+                      "'MASTER_ADDR','MASTER_PORT','TORCHELASTIC_RESTART_COUNT','TORCHELASTIC_MAX_RESTARTS',"
+                      "'TORCHELASTIC_RUN_ID']\nprint(json.dumps({k: os.environ.get(k) for k in keys}))\n")
+    p = _run([sys.executable, "-m", "pytorch_distributed_training_tutorials_amd.launch", "--nproc-per-node", "2",
+              "--nnodes", "2", "--node-rank", "1", "--master-port", "29999", "--run-id", "abc", str(script)])
+    assert p.returncode == 0
+    import json
+
+    envs = sorted((json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")), key=lambda d: d["RANK"])
+    assert [d["RANK"] for d in envs] == ["2", "3"]
+    assert [d["LOCAL_RANK"] for d in envs] == ["0", "1"]
+    assert all(d["WORLD_SIZE"] == "4" and d["GROUP_RANK"] == "1" and d["MASTER_PORT"] == "29999"
+               and d["TORCHELASTIC_RUN_ID"] == "abc" and d["LOCAL_WORLD_SIZE"] == "2" for d in envs)
+
+
+def test_fault_injection_tears_group_down():
+    """Rank 1 dies at step 3: the launcher must kill rank 0 (blocked in a collective) and fail."""
+    p = _run([sys.executable, "-m", "pytorch_distributed_training_tutorials_amd.launch", "--nproc-per-node", "2",
+              "--master-port", str(free_port()), "--timeout", "120", "ddp_gpus_torchrun.py", "--max_epochs", "3"],
+             PTDT_FAULT_RANK=1, PTDT_FAULT_STEP=3, PTDT_FAULT_MODE="exit", timeout=200)
+    assert p.returncode not in (0, 124), (p.returncode, p.stderr[-2000:])
+    assert "fault injection: rank 1 fails at step 3" in p.stdout
+
+
+def test_launcher_restarts(tmp_path):
+    marker = tmp_path / "count"
+    script = tmp_path / "flaky.py"
+    script.write_text(f"import os,sys\np={str(marker)!r}\n"
+                      "n=int(open(p).read()) if os.path.exists(p) else 0\n"
+                      "if os.environ['RANK']=='0': open(p,'w').write(str(n+1))\n"
+                      "sys.exit(3 if os.environ['TORCHELASTIC_RESTART_COUNT']=='0' else 0)\n")
+    p = _run([sys.executable, "-m", "pytorch_distributed_training_tutorials_amd.launch", "--nproc-per-node", "2",
+              "--max-restarts", "1", str(script)])
+    assert p.returncode == 0
+    assert int(marker.read_text()) == 2
+
+
+def test_snapshot_save_and_resume(tmp_path):
+    snap = tmp_path / "snap.pt"
+    cmd = [sys.executable, "-m", "pytorch_distributed_training_tutorials_amd.launch", "--nproc-per-node", "2",
+           "--master-port", str(free_port()), "ddp_gpus_torchrun.py", "--max_epochs", "2", "--save_every", "1",
+           "--snapshot", str(snap), "--model", "mlp"]
+    p = _run(cmd)
+    assert p.returncode == 0, p.stderr[-2000:]
+    st = torch.load(snap, weights_only=True)
+    assert st["epoch"] == 1 and all(k.startswith("module.") for k in st["model"])
+    cmd[cmd.index("2", cmd.index("--max_epochs"))] = "3"
+    cmd[cmd.index("--master-port") + 1] = str(free_port())
+    p = _run(cmd)
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert "Resuming training from snapshot at Epoch 2" in p.stdout
+    assert [e for _, e, _, _ in STATUS.findall(p.stdout)] == ["2", "2"]
