@@ -10,6 +10,7 @@
 #include <c10/hip/HIPGuard.h>
 
 #include "comm/rccl_comm.h"
+#include "comm/xgmi_comm.h"
 #include "kernels/kernels.h"
 #include "reducer/reducer.h"
 
@@ -47,8 +48,8 @@ void fused_mlp_step_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<Tensor>
                     c10::optional<Tensor> idx, Tensor P, Tensor G, c10::optional<Tensor> mom,
                     c10::optional<Tensor> opt_step, Tensor loss_out, int64_t B, int64_t Din, int64_t H,
                     int64_t Dout, int64_t loss_kind, int64_t ignore_index, bool has_bias,
-                    double grad_scale, bool accumulate, double pre_lr, double pre_momentum,
-                    double pre_dampening, double pre_weight_decay, bool pre_nesterov) {
+                    double grad_scale, bool accumulate, int64_t update_mode, double lr, double momentum,
+                    double dampening, double weight_decay, bool nesterov, std::shared_ptr<XgmiComm> ar) {
   check_gpu(X, "X");
   check_gpu(P, "P");
   check_gpu(G, "G");
@@ -96,11 +97,18 @@ void fused_mlp_step_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<Tensor>
   a.has_bias = has_bias ? 1 : 0;
   a.grad_scale = (float)grad_scale;
   a.accumulate = accumulate ? 1 : 0;
-  a.pre_lr = (float)pre_lr;
-  a.pre_momentum = (float)pre_momentum;
-  a.pre_dampening = (float)pre_dampening;
-  a.pre_weight_decay = (float)pre_weight_decay;
-  a.pre_nesterov = pre_nesterov ? 1 : 0;
+  a.update_mode = (int)update_mode;
+  a.lr = (float)lr;
+  a.momentum = (float)momentum;
+  a.dampening = (float)dampening;
+  a.weight_decay = (float)weight_decay;
+  a.nesterov = nesterov ? 1 : 0;
+  if (ar) {
+    TORCH_CHECK(ar->ready(), "fused_mlp_step: xGMI communicator not opened");
+    TORCH_CHECK(np <= ar->max_elems(), "fused_mlp_step: bucket larger than the xGMI buffer");
+    TORCH_CHECK(update_mode != 1 && !accumulate, "fused_mlp_step: in-kernel all-reduce needs update_mode 0/2");
+    a.ar = ar->args();
+  }
   hip_check(ptdt::fused_mlp_step(a, cur_stream(X)), "fused_mlp_step");
 }
 
@@ -459,8 +467,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("fused_mlp_step", &fused_mlp_step_py, py::arg("X"), py::arg("Yf"), py::arg("Yi"), py::arg("idx"),
         py::arg("P"), py::arg("G"), py::arg("mom"), py::arg("opt_step"), py::arg("loss_out"), py::arg("B"),
         py::arg("Din"), py::arg("H"), py::arg("Dout"), py::arg("loss_kind"), py::arg("ignore_index"),
-        py::arg("has_bias"), py::arg("grad_scale"), py::arg("accumulate"), py::arg("pre_lr"),
-        py::arg("pre_momentum"), py::arg("pre_dampening"), py::arg("pre_weight_decay"), py::arg("pre_nesterov"));
+        py::arg("has_bias"), py::arg("grad_scale"), py::arg("accumulate"), py::arg("update_mode"), py::arg("lr"),
+        py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"), py::arg("nesterov"),
+        py::arg("ar") = nullptr);
   m.def("fused_mlp_lds_bytes", [](int B, int Din, int H, int Dout) { return fused_mlp_lds_bytes(B, Din, H, Dout); });
   m.def("sgd_flat_", &sgd_flat_);
   m.def("adam_flat_", &adam_flat_);
@@ -562,6 +571,30 @@ PYBIND11_MODULE(_C, m) {
       .def("abort", &RcclComm::abort)
       .def_property_readonly("aborted", &RcclComm::aborted)
       .def("fingerprints", &RcclComm::fingerprints);
+
+  py::class_<XgmiComm, std::shared_ptr<XgmiComm>>(m, "XgmiComm")
+      .def(py::init<int, int, int, int>(), py::arg("rank"), py::arg("world"), py::arg("max_elems"), py::arg("device"))
+      .def("handle", [](XgmiComm& c) { return py::bytes(c.handle()); })
+      .def("open", [](XgmiComm& c, std::vector<py::bytes> hs) {
+        std::vector<std::string> v;
+        for (auto& h : hs) v.push_back(std::string(h));
+        c.open(v);
+      })
+      .def_property_readonly("ready", &XgmiComm::ready)
+      .def_property_readonly("rank", &XgmiComm::rank)
+      .def_property_readonly("world", &XgmiComm::world)
+      .def_property_readonly("max_elems", &XgmiComm::max_elems)
+      .def("error", &XgmiComm::error)
+      .def("reset_error", &XgmiComm::reset_error)
+      .def("all_reduce_avg", [](XgmiComm& c, Tensor t) {
+        check_gpu(t, "xgmi all_reduce tensor");
+        TORCH_CHECK(t.scalar_type() == at::kFloat, "xgmi all_reduce: fp32");
+        TORCH_CHECK(c.ready(), "xgmi all_reduce: communicator not opened");
+        TORCH_CHECK(t.numel() <= c.max_elems(), "xgmi all_reduce: tensor larger than the xGMI buffer");
+        c10::hip::HIPGuard guard(t.device().index());
+        hip_check(xgmi_allreduce_avg(c.args(), t.data_ptr<float>(), (int)t.numel(), cur_stream(t)),
+                  "xgmi_allreduce_avg");
+      });
 
   py::class_<RcclClique, std::shared_ptr<RcclClique>>(m, "RcclClique")
       .def(py::init<const std::vector<int>&>())

@@ -1,0 +1,83 @@
+// One-shot all-reduce over xGMI peer memory for latency-bound buckets.
+//
+// Why: the reference's DDP toy all-reduces one 84-byte bucket per step
+// (SURVEY M5); at that size RCCL's cost is pure latency (a kernel launch plus
+// its protocol round trips). An 8x MI355X node is a fully connected xGMI mesh,
+// so every rank can write straight into every peer's memory: one hop, no ring.
+//
+// Protocol (NCCL's "LL" idea, CDNA-native): each 4-byte value travels as an
+// 8-byte word {seq:32 | value:32} written with ONE 64-bit system-scope store
+// into slot [parity][src_rank][i] of every peer's buffer. A reader polls its
+// own buffer until the word's seq matches, so data and flag arrive together:
+// no __threadfence_system, no separate flag round trip. The buffer is
+// allocated uncached (hipDeviceMallocUncached) and shared by IPC handles, so
+// remote xGMI writes are visible to the owner's polls without L2 staleness.
+// Two parities (seq & 1) make slot reuse safe: a rank can only start
+// collective s+2 after it has read every peer's data of s+1, which each peer
+// wrote after finishing s. Every rank sums the W contributions in rank order,
+// so all ranks get bit-identical results (DDP replicas stay in sync). Polls are
+// bounded: a peer that never arrives sets *err and the kernel completes (with
+// garbage) instead of hanging the GPU; the host checks *err.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ptdt {
+
+constexpr int kXgmiMaxRanks = 8;
+
+struct XgmiArgs {
+  uint64_t* local;                       // this rank's LL buffer
+  uint64_t* peers[kXgmiMaxRanks];        // every rank's LL buffer (peers[rank] == local)
+  uint32_t* seq;                         // this rank's collective counter (device)
+  int* err;                              // nonzero after a timed-out poll
+  int rank, world, max_elems;            // world == 0: disabled
+};
+
+#ifdef __HIPCC__
+__device__ __forceinline__ uint64_t* xgmi_slot(uint64_t* base, int parity, int src, int world, int max_elems,
+                                               int i) {
+  return base + ((int64_t)(parity * world + src) * max_elems + i);
+}
+
+// Push this rank's n values (vals: any memory readable by the caller's threads).
+__device__ __forceinline__ void xgmi_push(const XgmiArgs& x, uint32_t s, const float* vals, int n, int tid,
+                                          int nt) {
+  const int parity = (int)(s & 1u);
+  const int64_t tot = (int64_t)x.world * n;
+  for (int64_t e = tid; e < tot; e += nt) {
+    const int p = (int)(e / n), i = (int)(e % n);
+    const uint64_t w = ((uint64_t)s << 32) | (uint64_t)__float_as_uint(vals[i]);
+    __hip_atomic_store(xgmi_slot(x.peers[p], parity, x.rank, x.world, x.max_elems, i), w, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Wait for element i of every rank and return the sum in rank order.
+__device__ __forceinline__ float xgmi_gather_sum(const XgmiArgs& x, uint32_t s, int i) {
+  const int parity = (int)(s & 1u);
+  float acc = 0.f;
+  for (int p = 0; p < x.world; ++p) {
+    uint64_t* slot = xgmi_slot(x.local, parity, p, x.world, x.max_elems, i);
+    uint64_t w = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t polls = 0;
+    while ((uint32_t)(w >> 32) != s) {
+      if (++polls > (1u << 26)) {  // ~seconds: a peer is gone; fail loudly, never hang
+        __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      w = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    acc += __uint_as_float((uint32_t)w);
+  }
+  return acc;
+}
+#endif
+
+// Standalone in-place average of a small fp32 buffer (n <= max_elems), one
+// workgroup, graph-capturable (seq lives in device memory).
+hipError_t xgmi_allreduce_avg(const XgmiArgs& x, float* data, int n, hipStream_t s);
+
+}  // namespace ptdt

@@ -19,8 +19,6 @@
 namespace ptdt {
 namespace {
 
-constexpr int kThreads = 256;
-
 __device__ __forceinline__ float sgd_one(float p, float g, float* mom, int64_t i, bool first,
                                          float lr, float mu, float damp, float wd, int nesterov) {
   float d = g + wd * p;
@@ -32,9 +30,32 @@ __device__ __forceinline__ float sgd_one(float p, float g, float* mom, int64_t i
   return p - lr * d;
 }
 
-__global__ void __launch_bounds__(kThreads) fused_mlp_step_kernel(FusedMlpArgs a) {
+// dot(x[0:n], w[0:n]) from LDS; 16-B reads when both rows are 16-B aligned.
+__device__ __forceinline__ float dot_lds(const float* x, const float* w, int n, bool vec4) {
+  float acc0 = 0.f, acc1 = 0.f;
+  int k = 0;
+  if (vec4) {
+    for (; k + 4 <= n; k += 4) {
+      const float4 xv = *reinterpret_cast<const float4*>(x + k);
+      const float4 wv = *reinterpret_cast<const float4*>(w + k);
+      acc0 = fmaf(xv.x, wv.x, acc0);
+      acc1 = fmaf(xv.y, wv.y, acc1);
+      acc0 = fmaf(xv.z, wv.z, acc0);
+      acc1 = fmaf(xv.w, wv.w, acc1);
+    }
+  }
+  for (; k < n; ++k) acc0 = fmaf(x[k], w[k], acc0);
+  return acc0 + acc1;
+}
+
+// Critical path = two dependent global round trips: (sampler indices || params,
+// grads, opt state) -> barrier -> (dataset rows X, Y gathered by index) ->
+// barrier; everything after runs out of LDS. blockDim.x is 256 for the
+// reference's single Linear, 1024 (16 waves) when a hidden layer gives enough
+// independent work to hide LDS latency.
+__global__ void __launch_bounds__(1024) fused_mlp_step_kernel(FusedMlpArgs a) {
   extern __shared__ float lds[];
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, NT = blockDim.x;
   const int B = a.B, Din = a.Din, H = a.H, Dout = a.Dout;
   const int Dh = H > 0 ? H : Din;                 // width feeding the output layer
   const int64_t nW1 = H > 0 ? (int64_t)H * Din : 0;
@@ -42,71 +63,83 @@ __global__ void __launch_bounds__(kThreads) fused_mlp_step_kernel(FusedMlpArgs a
   const int64_t nW2 = (int64_t)Dout * Dh;
   const int64_t nb2 = a.has_bias ? Dout : 0;
   const int64_t np = nW1 + nb1 + nW2 + nb2;
+  const bool soft_or_mse = a.loss_kind != kLossCEIndex;
 
-  float* Ps = lds;                    // [np]
-  float* xs = Ps + np;                // [B*Din]
-  float* as = xs + (int64_t)B * Din;  // [B*H]
-  float* zs = as + (int64_t)B * H;    // [B*Dout]  logits -> dlogits
-  float* ds = zs + (int64_t)B * Dout; // [B*H]     d(pre-activation)
-  float* red = ds + (int64_t)B * H;   // [16]
+  // LDS carve-up (floats); every array starts 16-B aligned
+  auto al4 = [](int64_t n) { return (n + 3) & ~(int64_t)3; };
+  float* Ps = lds;                           // [np]
+  float* xs = Ps + al4(np);                  // [B*Din]
+  float* as = xs + al4((int64_t)B * Din);    // [B*H]
+  float* zs = as + al4((int64_t)B * H);      // [B*Dout]  logits -> dlogits
+  float* ds = zs + al4((int64_t)B * Dout);   // [B*H]     d(pre-activation)
+  float* ys = ds + al4((int64_t)B * H);      // [B*Dout] float targets, or [B] labels (as int)
+  int* sidx = reinterpret_cast<int*>(ys + al4((int64_t)B * (soft_or_mse ? Dout : 1)));  // [B]
+  float* red = reinterpret_cast<float*>(sidx + al4(B));  // [32]
+  float* gs = red + 32;                      // [np] local grads (in-kernel all-reduce only)
+  const bool use_ar = a.ar.world > 0;
+  const uint32_t ar_seq = use_ar ? *a.ar.seq + 1u : 0u;
+  const bool step_first = (a.opt_step != nullptr) ? (*a.opt_step == 0) : false;
 
-  // ---- 1. deferred optimizer step of the previous iteration + param staging
-  if (a.pre_lr > 0.f) {
-    const bool first = (a.opt_step != nullptr) ? (*a.opt_step == 0) : false;
-    for (int64_t i = tid; i < np; i += kThreads) {
-      float p = sgd_one(a.P[i], a.G[i], a.mom, i, first, a.pre_lr, a.pre_momentum,
-                        a.pre_dampening, a.pre_weight_decay, a.pre_nesterov);
+  // ---- trip 1: sampler indices, and the deferred optimizer step of the previous iteration
+  for (int b = tid; b < B; b += NT) sidx[b] = a.idx ? a.idx[b] : b;
+  const bool pre = a.update_mode == 1 && a.lr > 0.f;
+  if (pre) {
+    for (int64_t i = tid; i < np; i += NT) {
+      const float p = sgd_one(a.P[i], a.G[i], a.mom, i, step_first, a.lr, a.momentum, a.dampening,
+                              a.weight_decay, a.nesterov);
       a.P[i] = p;
       Ps[i] = p;
     }
-    __syncthreads();
-    if (tid == 0 && a.opt_step != nullptr) *a.opt_step += 1;
   } else {
-    for (int64_t i = tid; i < np; i += kThreads) Ps[i] = a.P[i];
+    for (int64_t i = tid; i < np; i += NT) Ps[i] = a.P[i];
   }
+  __syncthreads();
+  if (pre && tid == 0 && a.opt_step != nullptr) *a.opt_step += 1;
   const float* W1 = Ps;
   const float* b1 = Ps + nW1;
   const float* W2 = Ps + nW1 + nb1;
   const float* b2 = W2 + nW2;
 
-  // ---- 2. batch gather (sampler indices -> rows of the resident dataset)
-  for (int64_t e = tid; e < (int64_t)B * Din; e += kThreads) {
+  // ---- trip 2: gather the batch rows (features and targets) into LDS
+  for (int64_t e = tid; e < (int64_t)B * Din; e += NT) {
     const int b = (int)(e / Din), k = (int)(e % Din);
-    const int64_t row = a.idx ? (int64_t)a.idx[b] : b;
-    xs[e] = a.X[row * Din + k];
+    xs[e] = a.X[(int64_t)sidx[b] * Din + k];
+  }
+  if (soft_or_mse) {
+    for (int64_t e = tid; e < (int64_t)B * Dout; e += NT) {
+      const int b = (int)(e / Dout), c = (int)(e % Dout);
+      ys[e] = a.Yf[(int64_t)sidx[b] * Dout + c];
+    }
+  } else {
+    int* yl = reinterpret_cast<int*>(ys);
+    for (int b = tid; b < B; b += NT) yl[b] = (int)a.Yi[sidx[b]];
   }
   __syncthreads();
 
-  // ---- 3. forward
+  // ---- forward
+  const bool v_in = (Din & 3) == 0 && ((nW1 + 0) & 3) == 0;
   if (H > 0) {
-    for (int64_t e = tid; e < (int64_t)B * H; e += kThreads) {
+    for (int64_t e = tid; e < (int64_t)B * H; e += NT) {
       const int b = (int)(e / H), j = (int)(e % H);
-      float acc = nb1 ? b1[j] : 0.f;
-      const float* xr = xs + (int64_t)b * Din;
-      const float* wr = W1 + (int64_t)j * Din;
-      for (int k = 0; k < Din; ++k) acc = fmaf(xr[k], wr[k], acc);
+      const float acc = (nb1 ? b1[j] : 0.f) + dot_lds(xs + (int64_t)b * Din, W1 + (int64_t)j * Din, Din, v_in);
       as[e] = fmaxf(acc, 0.f);
     }
     __syncthreads();
   }
   const float* act = H > 0 ? as : xs;
-  for (int64_t e = tid; e < (int64_t)B * Dout; e += kThreads) {
+  const bool v_out = (Dh & 3) == 0 && ((nW1 + nb1) & 3) == 0;
+  for (int64_t e = tid; e < (int64_t)B * Dout; e += NT) {
     const int b = (int)(e / Dout), c = (int)(e % Dout);
-    float acc = nb2 ? b2[c] : 0.f;
-    const float* ar = act + (int64_t)b * Dh;
-    const float* wr = W2 + (int64_t)c * Dh;
-    for (int j = 0; j < Dh; ++j) acc = fmaf(ar[j], wr[j], acc);
-    zs[e] = acc;
+    zs[e] = (nb2 ? b2[c] : 0.f) + dot_lds(act + (int64_t)b * Dh, W2 + (int64_t)c * Dh, Dh, v_out);
   }
   __syncthreads();
 
-  // ---- 4. loss + dL/dlogits (unnormalised; 1/denominator folded into coef)
+  // ---- loss + dL/dlogits (unnormalised; 1/denominator folded into coef)
   float lsum = 0.f, cnt = 0.f;
-  for (int b = tid; b < B; b += kThreads) {
+  for (int b = tid; b < B; b += NT) {
     float* z = zs + (int64_t)b * Dout;
-    const int64_t row = a.idx ? (int64_t)a.idx[b] : b;
     if (a.loss_kind == kLossMSE) {
-      const float* t = a.Yf + row * Dout;
+      const float* t = ys + (int64_t)b * Dout;
       for (int c = 0; c < Dout; ++c) {
         const float d = z[c] - t[c];
         lsum = fmaf(d, d, lsum);
@@ -121,7 +154,7 @@ __global__ void __launch_bounds__(kThreads) fused_mlp_step_kernel(FusedMlpArgs a
     for (int c = 0; c < Dout; ++c) se += expf(z[c] - m);
     const float lse = m + logf(se);
     if (a.loss_kind == kLossCESoft) {
-      const float* t = a.Yf + row * Dout;
+      const float* t = ys + (int64_t)b * Dout;
       float tsum = 0.f, l = 0.f;
       for (int c = 0; c < Dout; ++c) {
         tsum += t[c];
@@ -131,7 +164,7 @@ __global__ void __launch_bounds__(kThreads) fused_mlp_step_kernel(FusedMlpArgs a
       lsum += l;
       cnt += 1.f;
     } else {  // class index
-      const int64_t y = a.Yi[row];
+      const int y = reinterpret_cast<const int*>(ys)[b];
       if (y == a.ignore_index) {
         for (int c = 0; c < Dout; ++c) z[c] = 0.f;
       } else {
@@ -142,19 +175,20 @@ __global__ void __launch_bounds__(kThreads) fused_mlp_step_kernel(FusedMlpArgs a
     }
   }
   lsum = block_sum(lsum, red);
-  cnt = block_sum(cnt, red + 8);
+  cnt = block_sum(cnt, red + 16);
   const float denom = cnt > 0.f ? cnt : 1.f;
   if (tid == 0) *a.loss_out = (cnt > 0.f) ? lsum / denom : (a.loss_kind == kLossCEIndex ? NAN : 0.f);
   const float coef = a.grad_scale / denom;
   __syncthreads();
 
-  // ---- 5. backward, gradients straight into the bucket
-  float* gW1 = a.G;
-  float* gb1 = a.G + nW1;
-  float* gW2 = a.G + nW1 + nb1;
+  // ---- backward, gradients straight into the bucket
+  float* gdst = use_ar ? gs : a.G;  // with the in-kernel all-reduce, local grads stay in LDS
+  float* gW1 = gdst;
+  float* gb1 = gdst + nW1;
+  float* gW2 = gdst + nW1 + nb1;
   float* gb2 = gW2 + nW2;
-  const bool acc = a.accumulate != 0;
-  for (int64_t e = tid; e < nW2 + nb2; e += kThreads) {
+  const bool acc = a.accumulate != 0 && !use_ar;
+  for (int64_t e = tid; e < nW2 + nb2; e += NT) {
     float s = 0.f;
     if (e < nW2) {
       const int c = (int)(e / Dh), j = (int)(e % Dh);
@@ -169,7 +203,7 @@ __global__ void __launch_bounds__(kThreads) fused_mlp_step_kernel(FusedMlpArgs a
     }
   }
   if (H > 0) {
-    for (int64_t e = tid; e < (int64_t)B * H; e += kThreads) {
+    for (int64_t e = tid; e < (int64_t)B * H; e += NT) {
       const int b = (int)(e / H), j = (int)(e % H);
       float s = 0.f;
       if (as[e] > 0.f)
@@ -177,7 +211,7 @@ __global__ void __launch_bounds__(kThreads) fused_mlp_step_kernel(FusedMlpArgs a
       ds[e] = s;
     }
     __syncthreads();
-    for (int64_t e = tid; e < nW1 + nb1; e += kThreads) {
+    for (int64_t e = tid; e < nW1 + nb1; e += NT) {
       float s = 0.f;
       if (e < nW1) {
         const int j = (int)(e / Din), k = (int)(e % Din);
@@ -192,14 +226,35 @@ __global__ void __launch_bounds__(kThreads) fused_mlp_step_kernel(FusedMlpArgs a
       }
     }
   }
+  if (!use_ar) return;
+
+  // ---- in-kernel one-shot all-reduce over xGMI, then this step's SGD update
+  __syncthreads();
+  xgmi_push(a.ar, ar_seq, gs, (int)np, tid, NT);
+  const float inv_w = 1.f / (float)a.ar.world;
+  const bool post = a.update_mode == 2 && a.lr > 0.f;
+  for (int64_t i = tid; i < np; i += NT) {
+    const float g = xgmi_gather_sum(a.ar, ar_seq, (int)i) * inv_w;
+    a.G[i] = g;  // .grad holds the global average, as after DDP's finalize
+    if (post)
+      a.P[i] = sgd_one(Ps[i], g, a.mom, i, step_first, a.lr, a.momentum, a.dampening, a.weight_decay,
+                       a.nesterov);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    *a.ar.seq = ar_seq;
+    if (post && a.opt_step != nullptr) *a.opt_step += 1;
+  }
 }
 
 }  // namespace
 
 size_t fused_mlp_lds_bytes(int B, int Din, int H, int Dout) {
+  auto al4 = [](int64_t n) { return (n + 3) & ~(int64_t)3; };
   const int64_t Dh = H > 0 ? H : Din;
   const int64_t np = (H > 0 ? (int64_t)H * Din + H : 0) + (int64_t)Dout * Dh + Dout;
-  const int64_t fl = np + (int64_t)B * Din + 2 * (int64_t)B * H + (int64_t)B * Dout + 16;
+  const int64_t fl = al4(np) + al4((int64_t)B * Din) + 2 * al4((int64_t)B * H) + 2 * al4((int64_t)B * Dout) +
+                     al4(B) + al4(B) + 32 + al4(np);
   return (size_t)fl * sizeof(float);
 }
 
@@ -207,11 +262,18 @@ hipError_t fused_mlp_step(const FusedMlpArgs& a, hipStream_t s) {
   const size_t lds = fused_mlp_lds_bytes(a.B, a.Din, a.H, a.Dout);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   if (a.B <= 0 || a.Din <= 0 || a.Dout <= 0 || a.H < 0) return hipErrorInvalidValue;
+  if (a.ar.world > 0) {
+    const int64_t Dh = a.H > 0 ? a.H : a.Din;
+    const int64_t np = (a.H > 0 ? (int64_t)a.H * a.Din + (a.has_bias ? a.H : 0) : 0) + (int64_t)a.Dout * Dh +
+                       (a.has_bias ? a.Dout : 0);
+    if (np > a.ar.max_elems || a.update_mode == 1 || a.accumulate) return hipErrorInvalidValue;
+  }
   if (lds > 64 * 1024) {
     PTDT_HIP_CHECK(hipFuncSetAttribute((const void*)fused_mlp_step_kernel,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   }
-  hipLaunchKernelGGL(fused_mlp_step_kernel, dim3(1), dim3(kThreads), lds, s, a);
+  const int threads = a.H > 0 ? 1024 : 256;
+  hipLaunchKernelGGL(fused_mlp_step_kernel, dim3(1), dim3(threads), lds, s, a);
   return hipGetLastError();
 }
 

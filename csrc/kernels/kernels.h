@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../comm/xgmi.h"
+
 namespace ptdt {
 
 enum DType : int { kF32 = 0, kBF16 = 1 };
@@ -41,9 +43,13 @@ struct FusedMlpArgs {
   int has_bias;
   float grad_scale;      // 1/world_size (DDP pre-division)
   int accumulate;        // 1: G += grads (no_sync accumulation), 0: G = grads
-  // deferred SGD of the previous step (applied before the forward), lr<=0 disables
-  float pre_lr, pre_momentum, pre_dampening, pre_weight_decay;
-  int pre_nesterov;
+  // SGD update folded into the step: update_mode 0 = none, 1 = "pre" (apply the
+  // previous step's update from the already all-reduced bucket before the
+  // forward), 2 = "post" (in-kernel xGMI all-reduce, then update this step).
+  int update_mode;
+  float lr, momentum, dampening, weight_decay;
+  int nesterov;
+  XgmiArgs ar;           // in-kernel one-shot all-reduce (ar.world == 0: off; needs update_mode 2 or 0)
 };
 hipError_t fused_mlp_step(const FusedMlpArgs& a, hipStream_t s);
 // LDS bytes the step needs (host check against the 160 KiB per-CU budget).

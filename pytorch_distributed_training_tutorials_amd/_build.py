@@ -48,7 +48,8 @@ def _torch_paths():
 
 def _sources():
     kernels = sorted((CSRC / "kernels").glob("*.hip"))
-    hosts = [CSRC / "comm" / "rccl_comm.cpp", CSRC / "reducer" / "reducer.cpp", CSRC / "bindings.cpp"]
+    hosts = [CSRC / "comm" / "rccl_comm.cpp", CSRC / "comm" / "xgmi_comm.cpp", CSRC / "reducer" / "reducer.cpp",
+             CSRC / "bindings.cpp"]
     return kernels, hosts
 
 

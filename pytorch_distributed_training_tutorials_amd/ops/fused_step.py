@@ -47,7 +47,7 @@ def _linears(model: nn.Module):
 class FusedMLPStep:
     def __init__(self, model: nn.Module, *, loss: str = "ce_soft", lr: float = 1e-2, momentum: float = 0.0,
                  dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False, comm=None,
-                 reduce: bool = True, defer_update: bool = True, ignore_index: int = -100):
+                 reduce: bool = True, defer_update: bool = True, ignore_index: int = -100, xgmi=None):
         layers, relu = _linears(model)
         self.model = model
         self.layers = layers
@@ -77,7 +77,8 @@ class FusedMLPStep:
         self.mom = torch.zeros_like(self.P) if momentum != 0 else None
         self.opt_step = torch.zeros(1, dtype=torch.int32, device=dev)
         self.comm = comm
-        self.reduce = reduce and comm is not None
+        self.xgmi = xgmi if (reduce and xgmi is not None) else None  # in-kernel all-reduce + update
+        self.reduce = reduce and comm is not None and self.xgmi is None
         self.defer = defer_update
         self.ignore_index = ignore_index
         self._pending = False
@@ -88,18 +89,23 @@ class FusedMLPStep:
             raise ValueError("model too large for the single-workgroup fused step")
 
     # ------------------------------------------------------------------ steps
-    def _kernel(self, X, Y, idx, B, loss_out, pre_lr):
+    def _kernel(self, X, Y, idx, B, loss_out, update_mode):
         ce_index = self.loss_kind == LOSS_KINDS["ce_index"]
         self._C.fused_mlp_step(X, None if ce_index else Y, Y if ce_index else None, idx, self.P, self.G,
                                self.mom, self.opt_step, loss_out, B, self.Din, self.H, self.Dout,
-                               self.loss_kind, self.ignore_index, self.has_bias, 1.0, False, pre_lr,
-                               self.momentum, self.dampening, self.weight_decay, self.nesterov)
+                               self.loss_kind, self.ignore_index, self.has_bias, 1.0, False, update_mode,
+                               self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
+                               self.xgmi.handle if self.xgmi is not None else None)
 
     def step(self, X: torch.Tensor, Y: torch.Tensor, idx: torch.Tensor | None, B: int,
              loss_out: torch.Tensor | None = None):
         """One DDP step on rows ``idx[:B]`` of the resident dataset ``(X, Y)``."""
-        pre = self.lr if (self.defer and self._pending) else 0.0
-        self._kernel(X, Y, idx, B, self.loss_buf if loss_out is None else loss_out, pre)
+        lo = self.loss_buf if loss_out is None else loss_out
+        if self.xgmi is not None:
+            # ONE launch: fwd + loss + bwd + xGMI all-reduce + SGD update
+            self._kernel(X, Y, idx, B, lo, 2)
+            return
+        self._kernel(X, Y, idx, B, lo, 1 if (self.defer and self._pending) else 0)
         if self.reduce:
             self.comm.all_reduce(self.G, "avg")
         if self.defer:

@@ -125,3 +125,53 @@ def comm_collectives(rank, world, port, out_dir):
     c.barrier()
     torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
     destroy_process_group()
+
+
+def xgmi_two_procs_one_gpu(rank, world, port, out_dir):
+    """Two ranks share cuda:0: exercises the xGMI LL protocol (IPC buffers, parities,
+    rank-ordered sums, in-kernel all-reduce + SGD) without a second GPU."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+    from pytorch_distributed_training_tutorials_amd.parallel.comm import Communicator
+    from pytorch_distributed_training_tutorials_amd.parallel.xgmi import XgmiAllReduce
+
+    dev = torch.device("cuda", 0)
+    ctl = Communicator(device=torch.device("cpu"))
+    xg = XgmiAllReduce(ctl, dev, max_elems=4096)
+    res = {"ok": xg.ok}
+    g = torch.Generator().manual_seed(1234)
+    errs = []
+    for it in range(40):
+        n = [1, 21, 777, 4096][it % 4]
+        vals = [torch.randn(n, generator=g) for _ in range(world)]
+        t = vals[rank].to(dev)
+        xg.all_reduce_avg(t)
+        torch.cuda.synchronize()
+        want = vals[0].clone()
+        for v in vals[1:]:
+            want += v
+        want /= world
+        errs.append(float((t.cpu() - want).abs().max()))
+    res["max_err"] = max(errs)
+    # fused DDP step with the in-kernel all-reduce: rank r trains on its half of each batch
+    torch.manual_seed(5)
+    model = ToyMLP(20, 16, 4).to(dev)
+    eng = FusedMLPStep(model, loss="ce_index", lr=0.1, momentum=0.9, xgmi=xg)
+    X = torch.randn(64, 20, generator=torch.Generator().manual_seed(9)).to(dev)
+    Y = torch.randint(0, 4, (64,), generator=torch.Generator().manual_seed(10)).to(dev)
+    for s in range(6):
+        idx = (torch.arange(8, dtype=torch.int32) + 16 * (s % 4) + 8 * rank).to(dev)
+        eng.step(X, Y, idx, 8)
+    torch.cuda.synchronize()
+    xg.check()
+    res["params"] = eng.P.cpu()
+    res["grads"] = eng.G.cpu()
+    torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
