@@ -50,7 +50,7 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=1e-2)
     ap.add_argument("--model", default="linear", choices=["linear", "mlp"],
                     help="linear = reference Linear(20,1)+soft CE; mlp = Linear(20,64)-ReLU-Linear(64,10)+CE")
-    ap.add_argument("--engine", default="fused", choices=["fused", "autograd", "reference"])
+    ap.add_argument("--engine", default="persistent", choices=["persistent", "fused", "autograd", "reference"])
     ap.add_argument("--graph_steps", type=int, default=128, help="target steps per captured hipGraph")
     ap.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl"],
                     help="gradient all-reduce of the fused engine: in-kernel one-shot xGMI (auto: if its "
@@ -158,6 +158,45 @@ def run_fused(args, rank, world, dev, comm):
     return t, extra
 
 
+# --------------------------------------------------------------------------- persistent
+def run_persistent(args, rank, world, dev, comm):
+    """Persistent DDP step engine: K steps in ceil(K/8192) launches, params/momentum/sampler
+    shard resident in LDS, in-kernel xGMI all-reduce + SGD every step."""
+    from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+    from pytorch_distributed_training_tutorials_amd.parallel.xgmi import maybe_create
+
+    model, loss = _build_model(args, dev)
+    ds = _dataset(args, dev, loss)
+    X, Y = ds.tensors
+    xg = None
+    if world > 1:
+        xg = maybe_create(comm, dev, mode="on")
+        if xg is None:
+            raise SystemExit("persistent engine: the xGMI all-reduce is unavailable on this node; use --engine fused")
+    eng = FusedMLPStep(model, loss=loss, lr=args.lr, comm=comm, xgmi=xg)
+    if world > 1:
+        comm.broadcast(eng.P, 0)  # DDP init: rank 0's parameters everywhere
+    sampler = DeviceDistributedSampler(len(ds), world, rank, seed=args.seed, device=dev)
+    S = math.ceil(sampler.num_samples / args.batch_size)
+    cursor = torch.zeros(2, dtype=torch.int32, device=dev)
+    chunk = 8192
+    losses = torch.zeros(min(chunk, max(args.steps, args.warmup, 1)), device=dev)
+    eng.run_persistent(X, Y, max(args.warmup, 1), args.batch_size, sampler, cursor, losses, chunk)
+    torch.cuda.synchronize(dev)
+    t = _timed(comm, dev, lambda: eng.run_persistent(X, Y, args.steps, args.batch_size, sampler, cursor, losses,
+                                                     chunk))
+    if xg is not None:
+        xg.check()
+    last = (args.steps - 1) % chunk
+    extra = {"steps_per_epoch": S, "launches_timed": math.ceil(args.steps / chunk),
+             "final_loss": float(losses[last].item()),
+             "allreduce": "xgmi-oneshot (in-kernel)" if world > 1 else "identity (world 1)",
+             "kernels": "persistent DDP step engine: per step gather+fwd+loss+bwd+all-reduce+SGD in one resident "
+                        "workgroup; sampler shard recomputed in-kernel each epoch"}
+    return t, extra
+
+
 # --------------------------------------------------------------------------- autograd
 def run_autograd(args, rank, world, dev, comm):
     from pytorch_distributed_training_tutorials_amd.data import DeviceDataLoader, DistributedSampler
@@ -262,7 +301,8 @@ def main(argv=None):
     from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
 
     comm = comm_mod.get_default(dev)
-    runner = {"fused": run_fused, "autograd": run_autograd, "reference": run_reference}[args.engine]
+    runner = {"persistent": run_persistent, "fused": run_fused, "autograd": run_autograd,
+              "reference": run_reference}[args.engine]
     elapsed, extra = runner(args, rank, world, dev, comm)
     gb = args.batch_size * world
     samples = args.steps * gb

@@ -112,6 +112,73 @@ void fused_mlp_step_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<Tensor>
   hip_check(ptdt::fused_mlp_step(a, cur_stream(X)), "fused_mlp_step");
 }
 
+void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<Tensor> Yi, Tensor P, Tensor G,
+                             c10::optional<Tensor> mom, c10::optional<Tensor> opt_step, int64_t B, int64_t Din,
+                             int64_t H, int64_t Dout, int64_t loss_kind, int64_t ignore_index, bool has_bias,
+                             double lr, double momentum, double dampening, double weight_decay, bool nesterov,
+                             std::shared_ptr<XgmiComm> ar, int64_t n_steps, int64_t W, int64_t rank,
+                             int64_t num_samples, bool shuffle, int64_t seed, Tensor cursor, Tensor losses) {
+  check_gpu(X, "X");
+  check_gpu(P, "P");
+  check_gpu(G, "G");
+  TORCH_CHECK(X.scalar_type() == at::kFloat && P.scalar_type() == at::kFloat && G.scalar_type() == at::kFloat);
+  TORCH_CHECK(X.dim() == 2 && X.size(1) == Din, "persistent: X must be [N, Din]");
+  const int64_t N = X.size(0);
+  const int64_t Dh = H > 0 ? H : Din;
+  const int64_t np = (H > 0 ? H * Din + (has_bias ? H : 0) : 0) + Dout * Dh + (has_bias ? Dout : 0);
+  TORCH_CHECK(P.numel() == np && G.numel() == np, "persistent: flat param/grad size mismatch");
+  TORCH_CHECK(cursor.is_cuda() && cursor.scalar_type() == at::kInt && cursor.numel() == 2, "cursor: int32[2] GPU");
+  TORCH_CHECK(losses.is_cuda() && losses.scalar_type() == at::kFloat && losses.numel() >= n_steps, "losses: f32[n]");
+  TORCH_CHECK(num_samples > 0 && num_samples * W >= N && W > 0 && rank >= 0 && rank < W, "persistent: bad sampler");
+  if (loss_kind == kLossCEIndex) {
+    TORCH_CHECK(Yi.has_value() && Yi->defined() && Yi->scalar_type() == at::kLong && Yi->numel() == N);
+  } else {
+    TORCH_CHECK(Yf.has_value() && Yf->defined() && Yf->scalar_type() == at::kFloat && Yf->numel() == N * Dout);
+  }
+  if (mom.has_value() && mom->defined()) TORCH_CHECK(mom->numel() == np && mom->is_cuda());
+  const int world = ar ? ar->world() : 1;
+  TORCH_CHECK(world == W, "persistent: all-reduce world != sampler world");
+  TORCH_CHECK(fused_mlp_persistent_lds_bytes((int)B, (int)Din, (int)H, (int)Dout, (int)num_samples, world) <=
+                  160 * 1024,
+              "persistent: model + epoch index list do not fit one workgroup's LDS");
+  c10::hip::HIPGuard guard(X.device().index());
+  FusedMlpArgs a{};
+  a.X = X.data_ptr<float>();
+  a.Yf = ptr_or_null<const float>(Yf);
+  a.Yi = ptr_or_null<const int64_t>(Yi);
+  a.P = P.data_ptr<float>();
+  a.G = G.data_ptr<float>();
+  a.mom = ptr_or_null<float>(mom);
+  a.opt_step = ptr_or_null<int32_t>(opt_step);
+  a.B = (int)B; a.Din = (int)Din; a.H = (int)H; a.Dout = (int)Dout;
+  a.loss_kind = (int)loss_kind;
+  a.ignore_index = (int)ignore_index;
+  a.has_bias = has_bias ? 1 : 0;
+  a.grad_scale = 1.f;
+  a.update_mode = 2;
+  a.lr = (float)lr; a.momentum = (float)momentum; a.dampening = (float)dampening;
+  a.weight_decay = (float)weight_decay; a.nesterov = nesterov ? 1 : 0;
+  if (ar && ar->world() > 1) {
+    TORCH_CHECK(ar->ready(), "persistent: xGMI communicator not opened");
+    TORCH_CHECK(np <= ar->max_elems(), "persistent: bucket larger than the xGMI buffer");
+    TORCH_CHECK(ar->rank() == rank, "persistent: rank mismatch");
+    a.ar = ar->args();
+  } else {
+    a.ar.world = 1;
+  }
+  PersistArgs pa{};
+  pa.n_steps = (int)n_steps;
+  pa.N = (int)N;
+  pa.W = (int)W;
+  pa.rank = (int)rank;
+  pa.num_samples = (int)num_samples;
+  pa.shuffle = shuffle ? 1 : 0;
+  pa.seed = (uint64_t)seed;
+  pa.cursor = cursor.data_ptr<int32_t>();
+  pa.losses = losses.data_ptr<float>();
+  hip_check(fused_mlp_persistent(a, pa, cur_stream(X)), "fused_mlp_persistent");
+}
+
 // ------------------------------------------------------------- optimizers
 void sgd_flat_(Tensor p, Tensor g, c10::optional<Tensor> mom, c10::optional<Tensor> step, double lr,
                double momentum, double dampening, double wd, bool nesterov, double grad_scale) {
@@ -470,6 +537,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("has_bias"), py::arg("grad_scale"), py::arg("accumulate"), py::arg("update_mode"), py::arg("lr"),
         py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"), py::arg("nesterov"),
         py::arg("ar") = nullptr);
+  m.def("fused_mlp_persistent", &fused_mlp_persistent_py, py::arg("X"), py::arg("Yf"), py::arg("Yi"), py::arg("P"),
+        py::arg("G"), py::arg("mom"), py::arg("opt_step"), py::arg("B"), py::arg("Din"), py::arg("H"),
+        py::arg("Dout"), py::arg("loss_kind"), py::arg("ignore_index"), py::arg("has_bias"), py::arg("lr"),
+        py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"), py::arg("nesterov"), py::arg("ar"),
+        py::arg("n_steps"), py::arg("W"), py::arg("rank"), py::arg("num_samples"), py::arg("shuffle"),
+        py::arg("seed"), py::arg("cursor"), py::arg("losses"));
   m.def("fused_mlp_lds_bytes", [](int B, int Din, int H, int Dout) { return fused_mlp_lds_bytes(B, Din, H, Dout); });
   m.def("sgd_flat_", &sgd_flat_);
   m.def("adam_flat_", &adam_flat_);

@@ -76,6 +76,40 @@ __device__ __forceinline__ float xgmi_gather_sum(const XgmiArgs& x, uint32_t s, 
 }
 #endif
 
+#ifdef __HIPCC__
+// Poll every (rank, element) slot of elements [i0, i0+n) in parallel (one
+// outstanding uncached load per lane instead of W sequential round trips) and
+// stage the values in tmp[p * n + i]; the caller barriers, then sums in rank
+// order. A timed-out poll sets *x.err (and *lds_flag when given).
+__device__ __forceinline__ void xgmi_gather_lds(const XgmiArgs& x, uint32_t s, int i0, int n, float* tmp,
+                                                int tid, int nt, int* lds_flag = nullptr) {
+  const int parity = (int)(s & 1u);
+  for (int e = tid; e < x.world * n; e += nt) {
+    const int p = e / n, i = e - p * n;
+    uint64_t* slot = xgmi_slot(x.local, parity, p, x.world, x.max_elems, i0 + i);
+    uint64_t w = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    uint32_t polls = 0;
+    while ((uint32_t)(w >> 32) != s) {
+      if (++polls > (1u << 26)) {
+        __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lds_flag) *lds_flag = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      w = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    tmp[e] = __uint_as_float((uint32_t)w);
+  }
+}
+
+// Sum staged contributions in rank order (bit-identical on every rank).
+__device__ __forceinline__ float xgmi_sum_lds(const float* tmp, int world, int n, int i) {
+  float acc = 0.f;
+  for (int p = 0; p < world; ++p) acc += tmp[p * n + i];
+  return acc;
+}
+#endif
+
 // Standalone in-place average of a small fp32 buffer (n <= max_elems), one
 // workgroup, graph-capturable (seq lives in device memory).
 hipError_t xgmi_allreduce_avg(const XgmiArgs& x, float* data, int n, hipStream_t s);

@@ -52,6 +52,25 @@ struct FusedMlpArgs {
   XgmiArgs ar;           // in-kernel one-shot all-reduce (ar.world == 0: off; needs update_mode 2 or 0)
 };
 hipError_t fused_mlp_step(const FusedMlpArgs& a, hipStream_t s);
+
+// Persistent DDP step engine: ONE launch runs `n_steps` full DDP steps of the
+// same model with parameters, momentum and the epoch's sampler indices kept
+// resident in LDS; per step: gather batch (by the device sampler's index list,
+// recomputed in-kernel at every epoch start) -> fwd/loss/bwd -> in-kernel
+// all-reduce (xGMI one-shot; identity at world 1) -> SGD update. Uses
+// FusedMlpArgs (update_mode must be 2; idx/loss_out unused) plus:
+struct PersistArgs {
+  int n_steps;
+  int N;                 // dataset rows
+  int W, rank;           // sampler sharding (== all-reduce world / rank)
+  int num_samples;       // rows per rank per epoch (DistributedSampler num_samples)
+  int shuffle;
+  uint64_t seed;
+  int32_t* cursor;       // device [epoch, step_in_epoch]; advanced by the kernel
+  float* losses;         // [n_steps] per-step mean loss
+};
+hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s);
+size_t fused_mlp_persistent_lds_bytes(int B, int Din, int H, int Dout, int num_samples, int world);
 // LDS bytes the step needs (host check against the 160 KiB per-CU budget).
 size_t fused_mlp_lds_bytes(int B, int Din, int H, int Dout);
 

@@ -7,6 +7,7 @@
 // consumed, so no PCIe traffic sits in the step.
 #include "common.h"
 #include "kernels.h"
+#include "sampler.h"
 
 namespace ptdt {
 namespace {
@@ -87,48 +88,12 @@ __global__ void __launch_bounds__(kBlock) gather_rows_kernel(const uint8_t* src,
   }
 }
 
-// ---- device DistributedSampler (keyed Feistel permutation, cycle walking)
-__device__ __forceinline__ uint32_t mix32(uint32_t h) {
-  h ^= h >> 16; h *= 0x7feb352dU; h ^= h >> 15; h *= 0x846ca68bU; h ^= h >> 16;
-  return h;
-}
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
-
+// ---- device DistributedSampler (csrc/kernels/sampler.h)
 __global__ void __launch_bounds__(1024) sampler_kernel(int32_t* out, int64_t N, int W, int rank,
                                                        int64_t num_samples, uint64_t seed,
                                                        int32_t* epoch_ptr, int shuffle) {
   const int epoch = *epoch_ptr + 1;
-  int bits = 1;
-  while ((1ll << bits) < N) ++bits;
-  bits += bits & 1;
-  const int half = bits / 2;
-  const uint32_t mask = (1u << half) - 1u;
-  uint32_t key[4];
-  const uint64_t base = splitmix64(seed ^ splitmix64((uint64_t)epoch + 0x1234567ull));
-#pragma unroll
-  for (int r = 0; r < 4; ++r) key[r] = (uint32_t)splitmix64(base + r);
-  for (int64_t i = threadIdx.x; i < num_samples; i += blockDim.x) {
-    uint32_t x = (uint32_t)(((int64_t)rank + (int64_t)W * i) % N);
-    if (shuffle) {
-      do {
-        uint32_t L = x >> half, R = x & mask;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t F = mix32(R ^ key[r]) & mask;
-          const uint32_t nL = R;
-          R = L ^ F;
-          L = nL;
-        }
-        x = (L << half) | R;
-      } while (x >= (uint32_t)N);
-    }
-    out[i] = (int32_t)x;
-  }
+  rank_epoch_indices(out, (uint32_t)N, W, rank, (int)num_samples, seed, epoch, shuffle, threadIdx.x, blockDim.x);
   __syncthreads();
   if (threadIdx.x == 0) *epoch_ptr = epoch;
 }

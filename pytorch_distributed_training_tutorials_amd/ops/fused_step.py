@@ -130,6 +130,31 @@ class FusedMLPStep:
             self.step(X, Y, idx[start:start + size], size, lo)
         self.flush()
 
+    # ------------------------------------------------------------ persistent engine
+    def run_persistent(self, X, Y, n_steps: int, batch_size: int, sampler, cursor: torch.Tensor,
+                       losses: torch.Tensor, max_steps_per_launch: int = 8192):
+        """Run ``n_steps`` DDP steps in persistent launches (csrc/kernels/fused_mlp.hip):
+        parameters, momentum and the epoch's sampler shard stay resident in LDS,
+        each step = gather -> fwd/loss/bwd -> all-reduce (in-kernel xGMI one-shot;
+        identity at world 1) -> SGD. ``sampler`` is a DeviceDistributedSampler
+        (sharding/permutation parameters); ``cursor`` an int32[2] device tensor
+        ``[epoch, step_in_epoch]`` advanced by the kernel; ``losses[i]`` receives
+        step i's mean loss (``losses`` must hold ``min(n_steps, max_steps_per_launch)``)."""
+        if self.xgmi is None and self.comm is not None and self.comm.world > 1:
+            raise RuntimeError("the persistent engine needs the xGMI all-reduce for world > 1")
+        ce_index = self.loss_kind == LOSS_KINDS["ce_index"]
+        done = 0
+        while done < n_steps:
+            n = min(max_steps_per_launch, n_steps - done)
+            self._C.fused_mlp_persistent(
+                X, None if ce_index else Y, Y if ce_index else None, self.P, self.G, self.mom, self.opt_step,
+                batch_size, self.Din, self.H, self.Dout, self.loss_kind, self.ignore_index, self.has_bias,
+                self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
+                self.xgmi.handle if self.xgmi is not None else None, n, sampler.num_replicas, sampler.rank,
+                sampler.num_samples, sampler.shuffle, sampler.seed, cursor, losses)
+            done += n
+        self._pending = False
+
     # ------------------------------------------------------------ hipGraphs
     def state(self):
         return [t for t in (self.P, self.G, self.mom, self.opt_step) if t is not None]

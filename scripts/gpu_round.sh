@@ -18,14 +18,18 @@ STAGES=${STAGES:-"tests smoke bench prof"}
 for s in $STAGES; do
   case $s in
     tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    micro) step microbench 120 tools/bin/microbench_launch ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    bench) step bench_fused 300 python bench.py --steps 2000 --warmup 200
-           step bench_fused_rccl 300 python bench.py --steps 2000 --warmup 200 --allreduce rccl
+    bench) step bench_persistent 300 python bench.py --steps 20000 --warmup 2000
+           step bench_fused 300 python bench.py --engine fused --steps 2000 --warmup 200
+           step bench_fused_rccl 300 python bench.py --engine fused --steps 2000 --warmup 200 --allreduce rccl
            step bench_autograd 300 python bench.py --engine autograd --steps 300 --warmup 50
            step bench_reference 300 python bench.py --engine reference --steps 300 --warmup 50
-           step bench_mlp 300 python bench.py --model mlp --steps 2000 --warmup 200 ;;
-    prof)  step prof_fused 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fused -o run -- python3 bench.py --steps 500 --warmup 64
-           step prof_fused_rccl 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fused_rccl -o run -- python3 bench.py --steps 500 --warmup 64 --allreduce rccl
+           step bench_mlp 300 python bench.py --model mlp --steps 20000 --warmup 2000
+           step bench_mlp_fused 300 python bench.py --engine fused --model mlp --steps 2000 --warmup 200 ;;
+    prof)  step prof_persistent 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_persistent -o run -- python3 bench.py --steps 20000 --warmup 2000
+           step prof_fused 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fused -o run -- python3 bench.py --engine fused --steps 500 --warmup 64
+           step prof_fused_rccl 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fused_rccl -o run -- python3 bench.py --engine fused --steps 500 --warmup 64 --allreduce rccl
            step prof_mlp 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_mlp -o run -- python3 bench.py --model mlp --steps 500 --warmup 64
            step prof_reference 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_reference -o run -- python3 bench.py --engine reference --steps 200 --warmup 20 ;;
   esac

@@ -175,3 +175,87 @@ def xgmi_two_procs_one_gpu(rank, world, port, out_dir):
     torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def pipeline_two_stage(rank, world, port, out_dir, micro):
+    """ToyModel split over 2 ranks (net1+ReLU | net2) with send/recv."""
+    _init(rank, world, port)
+    import torch.nn as nn
+
+    from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+    from pytorch_distributed_training_tutorials_amd.parallel.pipeline import PipelineStage
+
+    torch.manual_seed(0)
+    net1, net2 = nn.Linear(1000, 10), nn.Linear(10, 5)
+    stage_mod = nn.Sequential(net1, nn.ReLU()) if rank == 0 else net2
+    c = comm_mod.get_default()
+    st = PipelineStage(stage_mod, c, loss_fn=nn.MSELoss(), micro_batches=micro)
+    opt = torch.optim.SGD(stage_mod.parameters(), lr=1e-3)
+    g = torch.Generator().manual_seed(1)
+    losses = []
+    for _ in range(3):
+        x = torch.randn(20, 1000, generator=g)
+        y = torch.randn(20, 5, generator=g)
+        opt.zero_grad()
+        l = st.train_step(x if rank == 0 else None, y if rank == 1 else None)
+        opt.step()
+        losses.append(None if l is None else float(l))
+    torch.save({"params": [p.detach() for p in stage_mod.parameters()], "losses": losses},
+               os.path.join(out_dir, f"r{rank}.pt"))
+    destroy_process_group()
+
+
+def _per_step_reference(eng, X, Y, sampler, n_steps, B, dev):
+    """The same n DDP steps through the per-step kernel + standalone device sampler."""
+    import math
+
+    S = math.ceil(sampler.num_samples / B)
+    idx = torch.zeros(sampler.num_samples, dtype=torch.int32, device=dev)
+    sampler.set_epoch(0)
+    for g in range(n_steps):
+        j = g % S
+        if j == 0:
+            sampler.generate(idx)
+        b = min(B, sampler.num_samples - j * B)
+        eng.step(X, Y, idx[j * B:j * B + b], b)
+    eng.flush()
+
+
+def persistent_two_procs_one_gpu(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+    from pytorch_distributed_training_tutorials_amd.parallel.comm import Communicator
+    from pytorch_distributed_training_tutorials_amd.parallel.xgmi import XgmiAllReduce
+
+    dev = torch.device("cuda", 0)
+    ctl = Communicator(device=torch.device("cpu"))
+    xg = XgmiAllReduce(ctl, dev, max_elems=4096)
+    X = torch.randn(300, 20, generator=torch.Generator().manual_seed(9)).to(dev)
+    Y = torch.randint(0, 4, (300,), generator=torch.Generator().manual_seed(10)).to(dev)
+    out = {}
+    for mode in ("persistent", "per_step"):
+        torch.manual_seed(5)
+        eng = FusedMLPStep(ToyMLP(20, 16, 4).to(dev), loss="ce_index", lr=0.05, momentum=0.9, xgmi=xg)
+        sampler = DeviceDistributedSampler(300, world, rank, seed=3, device=dev)
+        if mode == "persistent":
+            cursor = torch.zeros(2, dtype=torch.int32, device=dev)
+            losses = torch.zeros(7, device=dev)
+            eng.run_persistent(X, Y, 23, 16, sampler, cursor, losses, max_steps_per_launch=7)
+            torch.cuda.synchronize()
+            out["cursor"] = cursor.cpu()
+        else:
+            _per_step_reference(eng, X, Y, sampler, 23, 16, dev)
+        torch.cuda.synchronize()
+        xg.check()
+        out[mode] = eng.P.cpu()
+    torch.save(out, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()

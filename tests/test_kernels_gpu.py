@@ -49,7 +49,7 @@ def test_fused_mlp_step_matches_torch(native, dev, H, Dout, loss_kind):
     loss = torch.zeros(1, device=dev)
     kind = {"ce_soft": 0, "ce_index": 1, "mse": 2}[loss_kind]
     native.fused_mlp_step(X, None if kind == 1 else Y, Y if kind == 1 else None, idx, P, G, None, None, loss,
-                          B, Din, H, Dout, kind, -100, True, 1.0, False, 0.0, 0.0, 0.0, 0.0, False)
+                          B, Din, H, Dout, kind, -100, True, 1.0, False, 0, 0.0, 0.0, 0.0, 0.0, False)
     rl, rg = _ref_step(X, Y, idx, params, H, loss_kind)
     torch.testing.assert_close(loss[0], rl, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(G, torch.cat([g.reshape(-1) for g in rg]), rtol=1e-4, atol=1e-6)
@@ -63,7 +63,7 @@ def test_fused_reference_toy_is_exactly_zero(native, dev):
     G = torch.full_like(P, 7.0)
     loss = torch.full((1,), 3.0, device=dev)
     native.fused_mlp_step(X, Y, None, None, P, G, None, None, loss, 32, 20, 0, 1, 0, -100, True, 1.0, False,
-                          0.0, 0.0, 0.0, 0.0, False)
+                          0, 0.0, 0.0, 0.0, 0.0, False)
     assert loss.abs().item() == 0.0
     assert (G == 0).all()
 
@@ -92,9 +92,9 @@ def test_fused_deferred_update_equals_sgd(native, dev, momentum):
     step = torch.zeros(1, dtype=torch.int32, device=dev)
     loss = torch.zeros(1, device=dev)
     for i, idx in enumerate(idxs):
-        pre = 0.1 if i > 0 else 0.0
+        mode = 1 if i > 0 else 0  # deferred ("pre") update of the previous step
         native.fused_mlp_step(X, None, Y, idx, P, G, mom, step, loss, B, Din, H, Dout, 1, -100, True, 1.0, False,
-                              pre, momentum, 0.0, 0.0, False)
+                              mode, 0.1, momentum, 0.0, 0.0, False)
     native.sgd_flat_(P, G, mom, step, 0.1, momentum, 0.0, 0.0, False, 1.0)
     torch.testing.assert_close(P, torch.cat([p.detach().reshape(-1) for p in ref]), rtol=1e-4, atol=1e-5)
 

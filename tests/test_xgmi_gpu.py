@@ -68,3 +68,47 @@ def test_xgmi_single_rank_in_kernel_path(dev):
         outs.append(eng.P.clone())
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-6, atol=1e-7)
     env.destroy_process_group()
+
+
+def test_persistent_engine_world1_equals_per_step(dev):
+    from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP, ddp_toy_model
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+
+    from ._workers import _per_step_reference
+
+    for kind in ("mlp", "toy"):
+        if kind == "mlp":
+            X = torch.randn(500, 20, device=dev)
+            Y = torch.randint(0, 10, (500,), device=dev)
+            mk, loss, mom = (lambda: ToyMLP(20, 64, 10)), "ce_index", 0.9
+        else:
+            X = torch.rand(2048, 20, device=dev)
+            Y = torch.rand(2048, 1, device=dev)
+            mk, loss, mom = (lambda: ddp_toy_model()), "ce_soft", 0.0
+        res = []
+        for mode in ("persistent", "per_step"):
+            torch.manual_seed(7)
+            eng = FusedMLPStep(mk().to(dev), loss=loss, lr=0.05, momentum=mom)
+            sampler = DeviceDistributedSampler(X.shape[0], 1, 0, seed=1, device=dev)
+            if mode == "persistent":
+                cursor = torch.zeros(2, dtype=torch.int32, device=dev)
+                losses = torch.zeros(40, device=dev)
+                eng.run_persistent(X, Y, 150, 32, sampler, cursor, losses, max_steps_per_launch=40)
+                torch.cuda.synchronize()
+                S = -(-X.shape[0] // 32)
+                assert cursor.tolist() == [150 // S, 150 % S]
+            else:
+                _per_step_reference(eng, X, Y, sampler, 150, 32, dev)
+            torch.cuda.synchronize()
+            res.append(eng.P.clone())
+        torch.testing.assert_close(res[0], res[1], rtol=1e-6, atol=1e-6)
+
+
+def test_persistent_engine_two_ranks_one_gpu(tmp_path):
+    world = 2
+    spawn(_workers.persistent_two_procs_one_gpu, args=(world, free_port(), str(tmp_path)), nprocs=world)
+    res = [torch.load(os.path.join(tmp_path, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    assert torch.equal(res[0]["persistent"], res[1]["persistent"])  # replicas in sync
+    torch.testing.assert_close(res[0]["persistent"], res[0]["per_step"], rtol=1e-6, atol=1e-6)
+    assert res[0]["cursor"].tolist() == [23 // 10, 23 % 10]  # 150 samples/rank / 16 -> 10 steps per epoch
