@@ -56,6 +56,8 @@ def parse(argv=None):
                     help="gradient all-reduce of the fused engine: in-kernel one-shot xGMI (auto: if its "
                          "self-test passes on every rank) or RCCL")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--stamps", action="store_true",
+                    help="persistent engine: diagnostic run with in-kernel phase timers (separate from the timed run)")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
     return ap.parse_args(argv)
 
@@ -172,8 +174,10 @@ def run_persistent(args, rank, world, dev, comm):
     xg = None
     if world > 1:
         xg = maybe_create(comm, dev, mode="on")
-        if xg is None:
-            raise SystemExit("persistent engine: the xGMI all-reduce is unavailable on this node; use --engine fused")
+        if xg is None:  # no usable peer memory on this node: per-step engine with RCCL instead
+            print("[bench] xGMI all-reduce unavailable; falling back to --engine fused --allreduce rccl", flush=True)
+            args.allreduce = "rccl"
+            return run_fused(args, rank, world, dev, comm)
     eng = FusedMLPStep(model, loss=loss, lr=args.lr, comm=comm, xgmi=xg)
     if world > 1:
         comm.broadcast(eng.P, 0)  # DDP init: rank 0's parameters everywhere
@@ -188,12 +192,23 @@ def run_persistent(args, rank, world, dev, comm):
                                                      chunk))
     if xg is not None:
         xg.check()
+    phase = None
+    if args.stamps:  # diagnostic pass AFTER the timed region (timers cost a little)
+        st = torch.zeros(9, dtype=torch.int64, device=dev)
+        eng.run_persistent(X, Y, args.steps, args.batch_size, sampler, cursor, losses, chunk, stamps=st)
+        v = st.tolist()
+        names = ["prefetch_issue", "forward", "loss", "backward", "allreduce", "sgd_land", "epoch_indices"]
+        clk = v[7] / (v[8] * 10e-9) if v[8] else 0.0
+        phase = {"cycles_per_step": {n: round(v[k] / args.steps, 1) for k, n in enumerate(names)},
+                 "total_cycles_per_step": round(v[7] / args.steps, 1), "clock_GHz": round(clk / 1e9, 3)}
     last = (args.steps - 1) % chunk
     extra = {"steps_per_epoch": S, "launches_timed": math.ceil(args.steps / chunk),
              "final_loss": float(losses[last].item()),
              "allreduce": "xgmi-oneshot (in-kernel)" if world > 1 else "identity (world 1)",
              "kernels": "persistent DDP step engine: per step gather+fwd+loss+bwd+all-reduce+SGD in one resident "
                         "workgroup; sampler shard recomputed in-kernel each epoch"}
+    if phase:
+        extra["phase_timers"] = phase
     return t, extra
 
 

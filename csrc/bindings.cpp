@@ -117,7 +117,8 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
                              int64_t H, int64_t Dout, int64_t loss_kind, int64_t ignore_index, bool has_bias,
                              double lr, double momentum, double dampening, double weight_decay, bool nesterov,
                              std::shared_ptr<XgmiComm> ar, int64_t n_steps, int64_t W, int64_t rank,
-                             int64_t num_samples, bool shuffle, int64_t seed, Tensor cursor, Tensor losses) {
+                             int64_t num_samples, bool shuffle, int64_t seed, Tensor cursor, Tensor losses,
+                             c10::optional<Tensor> stamps) {
   check_gpu(X, "X");
   check_gpu(P, "P");
   check_gpu(G, "G");
@@ -176,6 +177,10 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
   pa.seed = (uint64_t)seed;
   pa.cursor = cursor.data_ptr<int32_t>();
   pa.losses = losses.data_ptr<float>();
+  if (stamps.has_value() && stamps->defined()) {
+    TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == at::kLong && stamps->numel() >= 9, "stamps: int64[9]");
+    pa.stamps = stamps->data_ptr<int64_t>();
+  }
   hip_check(fused_mlp_persistent(a, pa, cur_stream(X)), "fused_mlp_persistent");
 }
 
@@ -542,7 +547,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("Dout"), py::arg("loss_kind"), py::arg("ignore_index"), py::arg("has_bias"), py::arg("lr"),
         py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"), py::arg("nesterov"), py::arg("ar"),
         py::arg("n_steps"), py::arg("W"), py::arg("rank"), py::arg("num_samples"), py::arg("shuffle"),
-        py::arg("seed"), py::arg("cursor"), py::arg("losses"));
+        py::arg("seed"), py::arg("cursor"), py::arg("losses"), py::arg("stamps") = py::none());
   m.def("fused_mlp_lds_bytes", [](int B, int Din, int H, int Dout) { return fused_mlp_lds_bytes(B, Din, H, Dout); });
   m.def("sgd_flat_", &sgd_flat_);
   m.def("adam_flat_", &adam_flat_);

@@ -26,6 +26,9 @@
 namespace ptdt {
 
 constexpr int kXgmiMaxRanks = 8;
+// Poll budget per slot (~1 us per uncached round trip): a few seconds, far above
+// any launch skew between ranks, far below a hang.
+constexpr uint32_t kXgmiMaxPolls = 1u << 22;
 
 struct XgmiArgs {
   uint64_t* local;                       // this rank's LL buffer
@@ -63,7 +66,7 @@ __device__ __forceinline__ float xgmi_gather_sum(const XgmiArgs& x, uint32_t s, 
     uint64_t w = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t polls = 0;
     while ((uint32_t)(w >> 32) != s) {
-      if (++polls > (1u << 26)) {  // ~seconds: a peer is gone; fail loudly, never hang
+      if (++polls > kXgmiMaxPolls) {  // ~seconds: a peer is gone; fail loudly, never hang
         __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
@@ -90,7 +93,7 @@ __device__ __forceinline__ void xgmi_gather_lds(const XgmiArgs& x, uint32_t s, i
     uint64_t w = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint32_t polls = 0;
     while ((uint32_t)(w >> 32) != s) {
-      if (++polls > (1u << 26)) {
+      if (++polls > kXgmiMaxPolls) {
         __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (lds_flag) *lds_flag = 1;
         break;

@@ -42,15 +42,44 @@ template <> struct Cvt<uint16_t> {
 };
 
 // ----------------------------------------------------------- wave64 reductions
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, PTDT_WAVE);
+// DPP / permlane based: every step is one VALU instruction (v_add_f32_dpp,
+// v_permlane16/32_swap) instead of an LDS-crossbar ds_bpermute round trip
+// (what __shfl_xor lowers to). All 64 lanes must be active.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int kDppXor1 = 0xB1;        // quad_perm [1,0,3,2]
+constexpr int kDppXor2 = 0x4E;        // quad_perm [2,3,0,1]
+constexpr int kDppHalfMirror = 0x141; // lane i <-> 7-i within 8 (pairs the two quads)
+constexpr int kDppMirror = 0x140;     // lane i <-> 15-i within 16 (pairs the two halves)
+
+// sum over aligned groups of G lanes (G in 1,2,4,8,16); result in every lane of the group
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+  if constexpr (G >= 2) v += dpp_f<kDppXor1>(v);
+  if constexpr (G >= 4) v += dpp_f<kDppXor2>(v);
+  if constexpr (G >= 8) v += dpp_f<kDppHalfMirror>(v);
+  if constexpr (G >= 16) v += dpp_f<kDppMirror>(v);
   return v;
 }
+
+__device__ __forceinline__ float wave_sum(float v) {
+  v = group_sum<16>(v);
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  v = __int_as_float(p[0]) + __int_as_float(p[1]);
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(q[0]) + __int_as_float(q[1]);
+}
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, PTDT_WAVE));
-  return v;
+  v = fmaxf(v, dpp_f<kDppXor1>(v));
+  v = fmaxf(v, dpp_f<kDppXor2>(v));
+  v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
+  v = fmaxf(v, dpp_f<kDppMirror>(v));
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  v = fmaxf(__int_as_float(p[0]), __int_as_float(p[1]));
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return fmaxf(__int_as_float(q[0]), __int_as_float(q[1]));
 }
 
 // Block-wide sum for blockDim.x a multiple of 64 (<= 1024). `scratch` needs
@@ -65,6 +94,25 @@ __device__ __forceinline__ float block_sum(float v, float* scratch) {
   for (int i = 0; i < nw; ++i) r += scratch[i];
   return r;
 }
+// Two sums in one pass (one barrier pair instead of two). scratch: 2*nwaves floats.
+__device__ __forceinline__ float2 block_sum2(float2 v, float* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v.x = wave_sum(v.x);
+  v.y = wave_sum(v.y);
+  __syncthreads();
+  if (lane == 0) {
+    scratch[2 * wid] = v.x;
+    scratch[2 * wid + 1] = v.y;
+  }
+  __syncthreads();
+  float2 r = make_float2(0.f, 0.f);
+  for (int i = 0; i < nw; ++i) {
+    r.x += scratch[2 * i];
+    r.y += scratch[2 * i + 1];
+  }
+  return r;
+}
+
 __device__ __forceinline__ float block_max(float v, float* scratch) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   v = wave_max(v);

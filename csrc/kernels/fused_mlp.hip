@@ -103,12 +103,114 @@ __device__ __forceinline__ void gather_batch(const FusedMlpArgs& a, const Dims& 
   }
 }
 
+// out[e] = sum_{r<R} term(e, r) for e < E, each output reduced by a group of G
+// adjacent lanes (G | 16): lane g of a group takes r = g, g+G, ... with four
+// independent accumulators (so LDS loads overlap instead of forming one
+// dependent chain), then log2(G) DPP adds inside the group. Replaces
+// one-thread-per-output serial loops whose dependent LDS loads made the step
+// latency-bound (profiles/).
+template <int G, typename Term, typename Store>
+__device__ __forceinline__ void group_reduce(int E, int R, Term term, Store store, int tid, int NT) {
+  const int g = tid & (G - 1);
+  // every lane runs the same number of outer iterations so the DPP adds see a full wave
+  const int rounds = (E + NT / G - 1) / (NT / G);
+  for (int it = 0; it < rounds; ++it) {
+    const int e = it * (NT / G) + tid / G;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    if (e < E) {
+      int r = g;
+      for (; r + 3 * G < R; r += 4 * G) {
+        a0 += term(e, r);
+        a1 += term(e, r + G);
+        a2 += term(e, r + 2 * G);
+        a3 += term(e, r + 3 * G);
+      }
+      for (; r < R; r += G) a0 += term(e, r);
+    }
+    const float v = group_sum<G>((a0 + a1) + (a2 + a3));
+    if (e < E && g == 0) store(e, v);
+  }
+}
+
+// out[e] = dot(x_row(e), w_row(e)) of length R with groups of G lanes, each
+// lane owning contiguous 4-float chunks (ds_read_b128) when vec4 holds.
+template <int G, typename XRow, typename WRow, typename Store>
+__device__ __forceinline__ void group_dot(int E, int R, bool vec4, XRow xrow, WRow wrow, Store store, int tid,
+                                          int NT) {
+  const int g = tid & (G - 1);
+  const int rounds = (E + NT / G - 1) / (NT / G);
+  for (int it = 0; it < rounds; ++it) {
+    const int e = it * (NT / G) + tid / G;
+    float a0 = 0.f, a1 = 0.f;
+    if (e < E) {
+      const float* x = xrow(e);
+      const float* w = wrow(e);
+      int k = 0;
+      if (vec4) {
+        for (k = 4 * g; k + 4 <= R; k += 4 * G) {
+          const float4 xv = *reinterpret_cast<const float4*>(x + k);
+          const float4 wv = *reinterpret_cast<const float4*>(w + k);
+          a0 = fmaf(xv.x, wv.x, a0);
+          a1 = fmaf(xv.y, wv.y, a1);
+          a0 = fmaf(xv.z, wv.z, a0);
+          a1 = fmaf(xv.w, wv.w, a1);
+        }
+        for (k = (R & ~3) + g; k < R; k += G) a0 = fmaf(x[k], w[k], a0);
+      } else {
+        for (k = g; k < R; k += G) a0 = fmaf(x[k], w[k], a0);
+      }
+    }
+    const float v = group_sum<G>(a0 + a1);
+    if (e < E && g == 0) store(e, v);
+  }
+}
+
+// Lanes per output: spread a reduction over a lane group only while the
+// outputs alone cannot occupy the workgroup (E * G <= NT) and each lane keeps
+// >= 2 terms; with enough outputs (the MLP's hidden layer) one lane per output
+// with 16-B LDS reads is cheaper than any shuffle tree.
+__device__ __forceinline__ int pick_group(int E, int R, int NT, int min_terms = 4) {
+  int g = 1;
+  while (g < 16 && E * (g * 2) <= NT && R >= min_terms * g * 2) g *= 2;
+  return g;
+}
+
+#define PTDT_GROUP_DISPATCH(FN, G, ...)           \
+  do {                                            \
+    switch (G) {                                  \
+      case 16: FN<16>(__VA_ARGS__); break;        \
+      case 8: FN<8>(__VA_ARGS__); break;          \
+      case 4: FN<4>(__VA_ARGS__); break;          \
+      case 2: FN<2>(__VA_ARGS__); break;          \
+      default: FN<1>(__VA_ARGS__); break;         \
+    }                                             \
+  } while (0)
+#define PTDT_GROUP_REDUCE(G, ...) PTDT_GROUP_DISPATCH(group_reduce, G, __VA_ARGS__)
+
+// Diagnostic phase timers (thread 0, s_memtime cycles); `on` is false in
+// production launches, so every tick is one uniform branch.
+struct Stamps {
+  bool on = false;
+  int64_t prev = 0;
+  int64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  __device__ __forceinline__ void start() {
+    if (on) prev = (int64_t)__builtin_amdgcn_s_memtime();
+  }
+  __device__ __forceinline__ void tick(int k) {
+    if (on) {
+      const int64_t t = (int64_t)__builtin_amdgcn_s_memtime();
+      acc[k] += t - prev;
+      prev = t;
+    }
+  }
+};
+
 // forward + loss + backward of one batch staged in LDS. Gradients (times
 // grad_scale / loss denominator) go to gdst (accumulated when acc); the mean
-// loss to *loss_out (thread 0). Ends with every gdst write issued (no barrier).
+// loss to *loss_out. Ends with every gdst write issued (no trailing barrier).
 template <bool HID, int LOSS>
 __device__ __forceinline__ void step_body(const FusedMlpArgs& a, const Dims& d, const float* Ps, const Scratch& s,
-                                          float* gdst, bool acc, float* loss_out, int tid, int NT) {
+                                          float* gdst, bool acc, float* loss_out, int tid, int NT, Stamps& st) {
   const int B = d.B, Din = d.Din, H = d.H, Dout = d.Dout, Dh = d.Dh;
   const float* W1 = Ps;
   const float* b1 = Ps + d.nW1;
@@ -117,25 +219,29 @@ __device__ __forceinline__ void step_body(const FusedMlpArgs& a, const Dims& d, 
   float *as = s.as, *zs = s.zs, *ds = s.ds;
   const float* xs = s.xs;
   const float* ys = s.ys;
+  const bool bias1 = d.nb1 != 0, bias2 = d.nb2 != 0;
 
+  // ---- forward
   if constexpr (HID) {
     const bool v_in = (Din & 3) == 0;
-    for (int e = tid; e < B * H; e += NT) {
-      const int b = e / H, j = e - b * H;
-      const float v = (d.nb1 ? b1[j] : 0.f) + dot_lds(xs + b * Din, W1 + j * Din, Din, v_in);
-      as[e] = fmaxf(v, 0.f);
-    }
+    PTDT_GROUP_DISPATCH(group_dot, pick_group(B * H, Din, NT, 8), B * H, Din, v_in,
+                        [&](int e) { return xs + (e / H) * Din; }, [&](int e) { return W1 + (e % H) * Din; },
+                        [&](int e, float v) { as[e] = fmaxf(v + (bias1 ? b1[e % H] : 0.f), 0.f); }, tid, NT);
     __syncthreads();
   }
   const float* act = HID ? as : xs;
-  const bool v_out = (Dh & 3) == 0 && ((d.nW1 + d.nb1) & 3) == 0;
-  for (int e = tid; e < B * Dout; e += NT) {
-    const int b = e / Dout, c = e - b * Dout;
-    zs[e] = (d.nb2 ? b2[c] : 0.f) + dot_lds(act + b * Dh, W2 + c * Dh, Dh, v_out);
+  {
+    const bool v_out = (Dh & 3) == 0 && ((d.nW1 + d.nb1) & 3) == 0;
+    PTDT_GROUP_DISPATCH(group_dot, pick_group(B * Dout, Dh, NT, 8), B * Dout, Dh, v_out,
+                        [&](int e) { return act + (e / Dout) * Dh; }, [&](int e) { return W2 + (e % Dout) * Dh; },
+                        [&](int e, float v) { zs[e] = v + (bias2 ? b2[e % Dout] : 0.f); }, tid, NT);
   }
   __syncthreads();
+  st.tick(1);
 
-  // loss + dL/dlogits (unnormalised; 1/denominator folded into coef)
+  // ---- loss + dL/dlogits. Rows are spread over lanes; the loss SUM is only
+  // needed for reporting, the gradient scale only needs the denominator
+  // (B for soft CE, B*Dout for MSE, #valid rows for CE with ignore_index).
   float lsum = 0.f, cnt = 0.f;
   for (int b = tid; b < B; b += NT) {
     float* z = zs + b * Dout;
@@ -146,7 +252,6 @@ __device__ __forceinline__ void step_body(const FusedMlpArgs& a, const Dims& d, 
         lsum = fmaf(df, df, lsum);
         z[c] = 2.f * df;
       }
-      cnt += (float)Dout;
     } else {
       float m = -INFINITY;
       for (int c = 0; c < Dout; ++c) m = fmaxf(m, z[c]);
@@ -162,7 +267,6 @@ __device__ __forceinline__ void step_body(const FusedMlpArgs& a, const Dims& d, 
         }
         for (int c = 0; c < Dout; ++c) z[c] = __expf(z[c] - lse) * tsum - t[c];
         lsum += l;
-        cnt += 1.f;
       } else {
         const int y = reinterpret_cast<const int*>(ys)[b];
         if (y == a.ignore_index) {
@@ -175,31 +279,43 @@ __device__ __forceinline__ void step_body(const FusedMlpArgs& a, const Dims& d, 
       }
     }
   }
-  lsum = block_sum(lsum, s.red);
-  cnt = block_sum(cnt, s.red + 16);
-  const float denom = cnt > 0.f ? cnt : 1.f;
-  if (tid == 0) *loss_out = (cnt > 0.f) ? lsum / denom : (LOSS == kLossCEIndex ? NAN : 0.f);
+  float denom;
+  if constexpr (LOSS == kLossCEIndex) {
+    // the only case whose denominator depends on the data
+    const float2 r2 = block_sum2(make_float2(lsum, cnt), s.red);
+    lsum = r2.x;
+    cnt = r2.y;
+    denom = cnt > 0.f ? cnt : 1.f;
+    if (tid == 0) *loss_out = cnt > 0.f ? lsum / denom : NAN;
+  } else {
+    denom = (LOSS == kLossMSE) ? (float)(B * Dout) : (float)B;
+    // loss sum off the critical path: per-wave partials now, one lane adds them after the backward
+    const float w = wave_sum(lsum);
+    if ((tid & 63) == 0) s.red[16 + (tid >> 6)] = w;
+    __syncthreads();
+  }
   const float coef = a.grad_scale / denom;
-  __syncthreads();
+  st.tick(2);
 
+  // ---- backward, gradients into gdst
   float* gW1 = gdst;
   float* gb1 = gdst + d.nW1;
   float* gW2 = gdst + d.nW1 + d.nb1;
   float* gb2 = gW2 + d.nW2;
-  for (int e = tid; e < d.nW2 + d.nb2; e += NT) {
-    float sm = 0.f;
-    if (e < d.nW2) {
-      const int c = e / Dh, j = e - c * Dh;
-      for (int b = 0; b < B; ++b) sm = fmaf(zs[b * Dout + c], act[b * Dh + j], sm);
-      sm *= coef;
-      gW2[e] = acc ? gW2[e] + sm : sm;
-    } else {
-      const int c = e - d.nW2;
-      for (int b = 0; b < B; ++b) sm += zs[b * Dout + c];
-      sm *= coef;
-      gb2[c] = acc ? gb2[c] + sm : sm;
-    }
-  }
+  PTDT_GROUP_REDUCE(pick_group(d.nW2 + d.nb2, B, NT), d.nW2 + d.nb2, B,
+                    [&](int e, int b) {
+                      if (e < d.nW2) {
+                        const int c = e / Dh, j = e - c * Dh;
+                        return zs[b * Dout + c] * act[b * Dh + j];
+                      }
+                      return zs[b * Dout + (e - d.nW2)];
+                    },
+                    [&](int e, float v) {
+                      v *= coef;
+                      if (e < d.nW2) gW2[e] = acc ? gW2[e] + v : v;
+                      else gb2[e - d.nW2] = acc ? gb2[e - d.nW2] + v : v;
+                    },
+                    tid, NT);
   if constexpr (HID) {
     for (int e = tid; e < B * H; e += NT) {
       const int b = e / H, j = e - b * H;
@@ -209,19 +325,26 @@ __device__ __forceinline__ void step_body(const FusedMlpArgs& a, const Dims& d, 
       ds[e] = sm;
     }
     __syncthreads();
-    for (int e = tid; e < d.nW1 + d.nb1; e += NT) {
-      float sm = 0.f;
-      if (e < d.nW1) {
-        const int j = e / Din, k = e - j * Din;
-        for (int b = 0; b < B; ++b) sm = fmaf(ds[b * H + j], xs[b * Din + k], sm);
-        sm *= coef;
-        gW1[e] = acc ? gW1[e] + sm : sm;
-      } else {
-        const int j = e - d.nW1;
-        for (int b = 0; b < B; ++b) sm += ds[b * H + j];
-        sm *= coef;
-        gb1[j] = acc ? gb1[j] + sm : sm;
-      }
+    PTDT_GROUP_REDUCE(pick_group(d.nW1 + d.nb1, B, NT), d.nW1 + d.nb1, B,
+                      [&](int e, int b) {
+                        if (e < d.nW1) {
+                          const int j = e / Din, k = e - j * Din;
+                          return ds[b * H + j] * xs[b * Din + k];
+                        }
+                        return ds[b * H + (e - d.nW1)];
+                      },
+                      [&](int e, float v) {
+                        v *= coef;
+                        if (e < d.nW1) gW1[e] = acc ? gW1[e] + v : v;
+                        else gb1[e - d.nW1] = acc ? gb1[e - d.nW1] + v : v;
+                      },
+                      tid, NT);
+  }
+  if constexpr (LOSS != kLossCEIndex) {
+    if (tid == 0) {
+      float l = 0.f;
+      for (int w = 0; w < (NT >> 6); ++w) l += s.red[16 + w];
+      *loss_out = l / denom;
     }
   }
 }
@@ -266,7 +389,11 @@ __global__ void __launch_bounds__(1024) fused_mlp_step_kernel(FusedMlpArgs a) {
 
   const bool first = (a.opt_step != nullptr) ? (*a.opt_step == 0) : false;
   uint32_t ar_seq = 0;
-  if constexpr (AR) ar_seq = *a.ar.seq + 1u;
+  XgmiArgs ar = a.ar;
+  if constexpr (AR) {
+    ar_seq = *a.ar.seq + 1u;
+    if (ar.world > 1 && *a.ar.err != 0) ar.world = 1;  // a peer already timed out: do not wait again
+  }
 
   // trip 1: sampler indices, params (with the deferred update of the previous step)
   for (int b = tid; b < B; b += NT) sidx[b] = a.idx ? a.idx[b] : b;
@@ -288,11 +415,12 @@ __global__ void __launch_bounds__(1024) fused_mlp_step_kernel(FusedMlpArgs a) {
   gather_batch<LOSS>(a, d, sidx, s, tid, NT);
   __syncthreads();
 
-  step_body<HID, LOSS>(a, d, Ps, s, AR ? gs : a.G, !AR && a.accumulate != 0, a.loss_out, tid, NT);
+  Stamps st;
+  step_body<HID, LOSS>(a, d, Ps, s, AR ? gs : a.G, !AR && a.accumulate != 0, a.loss_out, tid, NT, st);
 
   if constexpr (AR) {
     __syncthreads();
-    allreduce_lds(a.ar, ar_seq, gs, tmp, np, tid, NT);
+    allreduce_lds(ar, ar_seq, gs, tmp, np, tid, NT);
     for (int i = tid; i < np; i += NT) {
       const float g = gs[i];
       a.G[i] = g;  // .grad holds the global average, as after DDP's finalize
@@ -300,13 +428,56 @@ __global__ void __launch_bounds__(1024) fused_mlp_step_kernel(FusedMlpArgs a) {
         a.P[i] = sgd_one(Ps[i], g, a.mom, i, first, a.lr, a.momentum, a.dampening, a.weight_decay, a.nesterov);
     }
     if (tid == 0) {
-      if (a.ar.world > 1) *a.ar.seq = ar_seq;
+      if (ar.world > 1) *a.ar.seq = ar_seq;
       if (MODE == kArPost && a.opt_step != nullptr) *a.opt_step += 1;
     }
   }
 }
 
 // ------------------------------------------------------------------ persistent engine
+// Per-thread register prefetch of the NEXT step's batch rows: the global loads
+// are issued before this step's compute and written to the other LDS batch
+// buffer after it, so the gather latency is off the critical path.
+constexpr int kPf = 4;  // prefetched elements per thread (B*Din and B*Dout must be <= kPf * blockDim)
+
+template <int LOSS>
+struct Prefetch {
+  float x[kPf];
+  float y[kPf];
+  int yi[kPf];
+  __device__ __forceinline__ void issue(const FusedMlpArgs& a, const int* sel, int B, int Din, int Dout, int tid,
+                                        int NT) {
+#pragma unroll
+    for (int q = 0; q < kPf; ++q) {
+      const int e = tid + q * NT;
+      if (e < B * Din) {
+        const int b = e / Din;
+        x[q] = a.X[(int64_t)sel[b] * Din + (e - b * Din)];
+      }
+      if constexpr (LOSS != kLossCEIndex) {
+        if (e < B * Dout) {
+          const int b = e / Dout;
+          y[q] = a.Yf[(int64_t)sel[b] * Dout + (e - b * Dout)];
+        }
+      } else {
+        if (e < B) yi[q] = (int)a.Yi[sel[e]];
+      }
+    }
+  }
+  __device__ __forceinline__ void land(float* xs, float* ys, int B, int Din, int Dout, int tid, int NT) const {
+#pragma unroll
+    for (int q = 0; q < kPf; ++q) {
+      const int e = tid + q * NT;
+      if (e < B * Din) xs[e] = x[q];
+      if constexpr (LOSS != kLossCEIndex) {
+        if (e < B * Dout) ys[e] = y[q];
+      } else {
+        if (e < B) reinterpret_cast<int*>(ys)[e] = yi[q];
+      }
+    }
+  }
+};
+
 template <bool HID, int LOSS>
 __global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs a, PersistArgs pa) {
   extern __shared__ float lds[];
@@ -315,23 +486,30 @@ __global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs
   const Dims full(a.B, a.Din, HID ? a.H : 0, a.Dout, a.has_bias != 0);
   const int np = full.np, B = full.B;
   const bool use_mom = a.mom != nullptr && a.momentum != 0.f;
+  const int ylen = al4(FY ? B * full.Dout : B);
 
   float* Ps = lds;                                 // live parameters
   float* Ms = Ps + al4(np);                        // live momentum
   float* gs = Ms + al4(np);                        // grads of the current step
+  float* xsb[2];
+  float* ysb[2];
+  xsb[0] = gs + al4(np);
+  xsb[1] = xsb[0] + al4(B * full.Din);
+  ysb[0] = xsb[1] + al4(B * full.Din);
+  ysb[1] = ysb[0] + ylen;
   Scratch s;
-  s.xs = gs + al4(np);
-  s.as = s.xs + al4(B * full.Din);
+  s.as = ysb[1] + ylen;
   s.zs = s.as + al4(B * full.H);
   s.ds = s.zs + al4(B * full.Dout);
-  s.ys = s.ds + al4(B * full.H);
-  s.red = s.ys + al4(FY ? B * full.Dout : B);
+  s.red = s.ds + al4(B * full.H);
   float* tmp = s.red + 32;                         // [world * np]
-  int* eidx = reinterpret_cast<int*>(tmp + al4((a.ar.world > 1 ? a.ar.world : 1) * np));  // [num_samples]
-  int* lds_err = eidx + al4(pa.num_samples);       // set by a timed-out poll
+  int* ebuf[2];
+  ebuf[0] = reinterpret_cast<int*>(tmp + al4((a.ar.world > 1 ? a.ar.world : 1) * np));  // epoch index lists
+  ebuf[1] = ebuf[0] + al4(pa.num_samples);
+  int* lds_err = ebuf[1] + al4(pa.num_samples);   // set by a timed-out poll
   if (tid == 0) *lds_err = 0;
 
-  // ---- load resident state
+  // ---- load resident state; index lists of the current and the next epoch
   for (int i = tid; i < np; i += NT) {
     Ps[i] = a.P[i];
     Ms[i] = use_mom ? a.mom[i] : 0.f;
@@ -340,34 +518,78 @@ __global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs
   const int steps_per_epoch = (pa.num_samples + B - 1) / B;
   int opt_step = a.opt_step ? *a.opt_step : 0;
   uint32_t seq = a.ar.world > 1 ? *a.ar.seq : 0u;
-  if (j != 0) rank_epoch_indices(eidx, (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch, pa.shuffle,
-                                 tid, NT);
+  rank_epoch_indices(ebuf[epoch & 1], (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch, pa.shuffle,
+                     tid, NT);
+  rank_epoch_indices(ebuf[(epoch + 1) & 1], (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
+                     pa.shuffle, tid, NT);
+  __syncthreads();
+  const bool pf_ok = B * full.Din <= kPf * NT && B * (FY ? full.Dout : 1) <= kPf * NT;
+  auto batch_size = [&](int jj) { return pa.num_samples - jj * B < B ? pa.num_samples - jj * B : B; };
+  {  // first batch (synchronous)
+    Scratch s0 = s;
+    s0.xs = xsb[0];
+    s0.ys = ysb[0];
+    const Dims d0(batch_size(j), full.Din, full.H, full.Dout, a.has_bias != 0);
+    gather_batch<LOSS>(a, d0, ebuf[epoch & 1] + j * B, s0, tid, NT);
+  }
   __syncthreads();
 
+  Stamps st;
+  st.on = pa.stamps != nullptr && tid == 0;
+  const int64_t t_begin = st.on ? (int64_t)__builtin_amdgcn_s_memtime() : 0;
+  const int64_t r_begin = st.on ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  st.start();
+
   for (int step = 0; step < pa.n_steps; ++step) {
-    if (j == 0) {  // new epoch: this rank's DistributedSampler shard, computed in place
-      rank_epoch_indices(eidx, (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch, pa.shuffle, tid, NT);
+    const int cur = step & 1;
+    // next step's position, and the epoch after next computed one epoch ahead
+    int nj = j + 1, ne = epoch;
+    if (nj == steps_per_epoch) {
+      nj = 0;
+      ++ne;
+    }
+    if (j == 0 && step > 0) {
+      rank_epoch_indices(ebuf[(epoch + 1) & 1], (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
+                         pa.shuffle, tid, NT);
       __syncthreads();
     }
-    const int b0 = j * B;
-    const int bsz = pa.num_samples - b0 < B ? pa.num_samples - b0 : B;
-    const Dims d(bsz, full.Din, full.H, full.Dout, a.has_bias != 0);
-    gather_batch<LOSS>(a, d, eidx + b0, s, tid, NT);
+    st.tick(6);
+    Prefetch<LOSS> pf;
+    const int nb = batch_size(nj);
+    const bool have_next = step + 1 < pa.n_steps;
+    if (pf_ok && have_next) pf.issue(a, ebuf[ne & 1] + nj * B, nb, full.Din, full.Dout, tid, NT);
+    st.tick(0);
+
+    s.xs = xsb[cur];
+    s.ys = ysb[cur];
+    const Dims d(batch_size(j), full.Din, full.H, full.Dout, a.has_bias != 0);
+    step_body<HID, LOSS>(a, d, Ps, s, gs, false, pa.losses + step, tid, NT, st);
     __syncthreads();
-    step_body<HID, LOSS>(a, d, Ps, s, gs, false, pa.losses + step, tid, NT);
-    __syncthreads();
+    st.tick(3);
     seq += 1u;
     allreduce_lds(a.ar, seq, gs, tmp, np, tid, NT, lds_err);
+    st.tick(4);
     const bool first = opt_step == 0;
     for (int i = tid; i < np; i += NT)
       Ps[i] = sgd_one(Ps[i], gs[i], use_mom ? Ms : nullptr, i, first, a.lr, a.momentum, a.dampening,
                       a.weight_decay, a.nesterov);
     ++opt_step;
-    if (++j == steps_per_epoch) {
-      j = 0;
-      ++epoch;
+    // land the prefetched batch in the other buffer (last read two steps ago)
+    if (have_next) {
+      if (pf_ok) {
+        pf.land(xsb[cur ^ 1], ysb[cur ^ 1], nb, full.Din, full.Dout, tid, NT);
+      } else {
+        Scratch sn = s;
+        sn.xs = xsb[cur ^ 1];
+        sn.ys = ysb[cur ^ 1];
+        const Dims dn(nb, full.Din, full.H, full.Dout, a.has_bias != 0);
+        gather_batch<LOSS>(a, dn, ebuf[ne & 1] + nj * B, sn, tid, NT);
+      }
     }
+    j = nj;
+    epoch = ne;
     __syncthreads();
+    st.tick(5);
     if (*lds_err) break;  // a peer vanished: stop instead of timing out on every remaining step
   }
 
@@ -382,6 +604,12 @@ __global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs
     pa.cursor[1] = j;
     if (a.opt_step) *a.opt_step = opt_step;
     if (a.ar.world > 1) *a.ar.seq = seq;
+    if (st.on) {
+      // [0] prefetch issue, [1] forward, [2] loss, [3] backward, [4] all-reduce, [5] sgd+land, [6] epoch indices
+      for (int k = 0; k < 7; ++k) pa.stamps[k] += st.acc[k];
+      pa.stamps[7] += (int64_t)__builtin_amdgcn_s_memtime() - t_begin;
+      pa.stamps[8] += (int64_t)__builtin_amdgcn_s_memrealtime() - r_begin;
+    }
   }
 }
 
@@ -439,8 +667,9 @@ size_t fused_mlp_lds_bytes(int B, int Din, int H, int Dout) {
 size_t fused_mlp_persistent_lds_bytes(int B, int Din, int H, int Dout, int num_samples, int world) {
   const int Dh = H > 0 ? H : Din;
   const int np = (H > 0 ? H * Din + H : 0) + Dout * Dh + Dout;
-  const int64_t fl = 3 * (int64_t)al4(np) + al4(B * Din) + 2 * al4(B * H) + 2 * al4(B * Dout) + al4(B) + 32 +
-                     al4((world > 1 ? world : 1) * np) + al4(num_samples) + 4;
+  const int64_t fl = 3 * (int64_t)al4(np) + 2 * al4(B * Din) + 2 * al4(B * H) + al4(B * Dout) +
+                     2 * al4(B * Dout > B ? B * Dout : B) + 32 + al4((world > 1 ? world : 1) * np) +
+                     2 * al4(num_samples) + 4;
   return (size_t)fl * sizeof(float);
 }
 

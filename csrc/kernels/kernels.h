@@ -68,6 +68,8 @@ struct PersistArgs {
   uint64_t seed;
   int32_t* cursor;       // device [epoch, step_in_epoch]; advanced by the kernel
   float* losses;         // [n_steps] per-step mean loss
+  int64_t* stamps;       // optional [9] diagnostic phase timers (s_memtime cycles, thread 0): prefetch issue,
+                         // forward, loss, backward, all-reduce, sgd+land, epoch indices, total, realtime (100 MHz)
 };
 hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s);
 size_t fused_mlp_persistent_lds_bytes(int B, int Din, int H, int Dout, int num_samples, int world);

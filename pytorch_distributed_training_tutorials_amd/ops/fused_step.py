@@ -132,7 +132,7 @@ class FusedMLPStep:
 
     # ------------------------------------------------------------ persistent engine
     def run_persistent(self, X, Y, n_steps: int, batch_size: int, sampler, cursor: torch.Tensor,
-                       losses: torch.Tensor, max_steps_per_launch: int = 8192):
+                       losses: torch.Tensor, max_steps_per_launch: int = 8192, stamps: torch.Tensor | None = None):
         """Run ``n_steps`` DDP steps in persistent launches (csrc/kernels/fused_mlp.hip):
         parameters, momentum and the epoch's sampler shard stay resident in LDS,
         each step = gather -> fwd/loss/bwd -> all-reduce (in-kernel xGMI one-shot;
@@ -151,7 +151,7 @@ class FusedMLPStep:
                 batch_size, self.Din, self.H, self.Dout, self.loss_kind, self.ignore_index, self.has_bias,
                 self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
                 self.xgmi.handle if self.xgmi is not None else None, n, sampler.num_replicas, sampler.rank,
-                sampler.num_samples, sampler.shuffle, sampler.seed, cursor, losses)
+                sampler.num_samples, sampler.shuffle, sampler.seed, cursor, losses, stamps)
             done += n
         self._pending = False
 

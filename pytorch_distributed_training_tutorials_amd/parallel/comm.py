@@ -57,6 +57,7 @@ class Communicator:
         self.debug_sync = os.environ.get("PTDT_DEBUG_SYNC", "0") == "1"
         self._native = None
         self.name = name
+        self._fp: list = []  # collective fingerprints (op, numel, dtype) when enabled
         if self.device.type == "cuda":
             if not has_native():
                 native()  # raises: the GPU path must not silently fall back
@@ -93,6 +94,10 @@ class Communicator:
         if self._native is not None and self._native.aborted:
             raise RuntimeError(f"communicator aborted: {self._native.error()}")
 
+    def _record(self, op: str, t: torch.Tensor):
+        if self.fingerprint:
+            self._fp.append(f"{len(self._fp)}:{op}:{t.numel()}:{str(t.dtype).replace('torch.', '')}")
+
     def _after(self, stream=None):
         if self.debug_sync and self._native is not None:
             (stream or torch.cuda.current_stream(self.device)).synchronize()
@@ -100,6 +105,7 @@ class Communicator:
 
     # ------------------------------------------------------------ collectives
     def all_reduce(self, t: torch.Tensor, op: str = "sum", stream=None) -> torch.Tensor:
+        self._record(f"all_reduce.{op}", t)
         if t.is_cuda and self._native is not None:
             self._native.all_reduce(t, _OPS[op], _stream_handle(stream))
             self._after(stream)
@@ -114,6 +120,7 @@ class Communicator:
         return t
 
     def broadcast(self, t: torch.Tensor, src: int = 0, stream=None) -> torch.Tensor:
+        self._record("broadcast", t)
         if t.is_cuda and self._native is not None:
             self._native.broadcast(t, src, _stream_handle(stream))
             self._after(stream)
@@ -123,6 +130,7 @@ class Communicator:
         return t
 
     def reduce(self, t: torch.Tensor, dst: int = 0, op: str = "sum", stream=None) -> torch.Tensor:
+        self._record(f"reduce.{op}", t)
         if t.is_cuda and self._native is not None:
             self._native.reduce(t, dst, _OPS[op], _stream_handle(stream))
             self._after(stream)
@@ -133,6 +141,7 @@ class Communicator:
 
     def all_gather(self, out: torch.Tensor, inp: torch.Tensor, stream=None) -> torch.Tensor:
         """``out`` is ``[world * inp.numel()]`` (rank-major)."""
+        self._record("all_gather", inp)
         if inp.is_cuda and self._native is not None:
             self._native.all_gather(out, inp, _stream_handle(stream))
             self._after(stream)
@@ -144,6 +153,7 @@ class Communicator:
         return out
 
     def reduce_scatter(self, out: torch.Tensor, inp: torch.Tensor, op: str = "sum", stream=None):
+        self._record(f"reduce_scatter.{op}", inp)
         if inp.is_cuda and self._native is not None:
             self._native.reduce_scatter(out, inp, _OPS[op], _stream_handle(stream))
             self._after(stream)
@@ -160,6 +170,7 @@ class Communicator:
         return out
 
     def all_to_all(self, out: torch.Tensor, inp: torch.Tensor, stream=None):
+        self._record("all_to_all", inp)
         if inp.is_cuda and self._native is not None:
             self._native.all_to_all(out, inp, _stream_handle(stream))
             self._after(stream)
@@ -171,6 +182,7 @@ class Communicator:
         return out
 
     def send(self, t: torch.Tensor, dst: int, stream=None):
+        self._record("send", t)
         if t.is_cuda and self._native is not None:
             self._native.send(t, dst, _stream_handle(stream))
             self._after(stream)
@@ -178,6 +190,7 @@ class Communicator:
         dist.send(t, dst, group=self.group)
 
     def recv(self, t: torch.Tensor, src: int, stream=None):
+        self._record("recv", t)
         if t.is_cuda and self._native is not None:
             self._native.recv(t, src, _stream_handle(stream))
             self._after(stream)
@@ -220,7 +233,9 @@ class Communicator:
         return out
 
     def fingerprints(self):
-        return self._native.fingerprints() if self._native is not None else []
+        """Python-level collective log (op, numel, dtype in issue order), plus the
+        native communicator's own log when PTDT_DEBUG_FINGERPRINT=1."""
+        return list(self._fp)
 
     def destroy(self):
         self._native = None

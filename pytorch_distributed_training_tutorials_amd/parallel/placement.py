@@ -28,9 +28,17 @@ import torch.nn as nn
 DEFAULT_NO_SPLIT = ("LlamaDecoderLayer", "MistralDecoderLayer", "Bottleneck", "BasicBlock")
 
 
-def _bytes(m: nn.Module) -> int:
-    return sum(t.numel() * t.element_size() for t in list(m.parameters(recurse=True)) +
-               list(m.buffers(recurse=True)))
+def _bytes(m: nn.Module, linear_weight_bytes: int | None = None) -> int:
+    """Parameter + buffer bytes; ``linear_weight_bytes`` prices nn.Linear weights as if
+    quantised (1 = int8) so placement can be planned before quantising (e.g. on meta)."""
+    tot = 0
+    for mod in m.modules():
+        for name, p in mod.named_parameters(recurse=False):
+            esz = linear_weight_bytes if (linear_weight_bytes and isinstance(mod, nn.Linear) and name == "weight"
+                                          and not getattr(mod, "_ptdt_keep_fp", False)) else p.element_size()
+            tot += p.numel() * esz
+        tot += sum(b.numel() * b.element_size() for b in mod.buffers(recurse=False))
+    return tot
 
 
 def placement_units(model: nn.Module, no_split=DEFAULT_NO_SPLIT):
@@ -51,10 +59,11 @@ def placement_units(model: nn.Module, no_split=DEFAULT_NO_SPLIT):
     return out
 
 
-def infer_device_map(model: nn.Module, devices, max_memory: dict | None = None, no_split=DEFAULT_NO_SPLIT):
+def infer_device_map(model: nn.Module, devices, max_memory: dict | None = None, no_split=DEFAULT_NO_SPLIT,
+                     linear_weight_bytes: int | None = None):
     devices = [torch.device(d) for d in devices]
     units = placement_units(model, no_split)
-    sizes = [_bytes(m) for _, m in units]
+    sizes = [_bytes(m, linear_weight_bytes if n != "lm_head" else None) for n, m in units]
     total = sum(sizes) or 1
     n = len(devices)
     dmap = OrderedDict()

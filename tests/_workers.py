@@ -259,3 +259,25 @@ def persistent_two_procs_one_gpu(rank, world, port, out_dir):
     torch.save(out, os.path.join(out_dir, f"r{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def fingerprint_check(rank, world, port, out_dir, diverge):
+    os.environ["PTDT_DEBUG_FINGERPRINT"] = "1"
+    _init(rank, world, port)
+    from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+    from pytorch_distributed_training_tutorials_amd.utils.debug import CollectiveMismatch, check_fingerprints
+
+    c = comm_mod.get_default()
+    c.all_reduce(torch.ones(4))
+    op = "min" if (diverge and rank == 1) else "max"
+    c.all_reduce(torch.ones(4), op)  # a rank issuing a different reduction: silent garbage without the check
+    res = {}
+    try:
+        res["n"] = check_fingerprints(c)
+        res["ok"] = True
+    except CollectiveMismatch as e:
+        res["ok"] = False
+        res["msg"] = str(e)
+    torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+    destroy_process_group()

@@ -76,3 +76,13 @@ def test_communicator_collectives_gloo(tmp_path, world):
         torch.testing.assert_close(d["a2a"], torch.tensor([r + 100.0 * q for q in range(world)]))
         assert d["obj"] == {"r": 0}
     torch.testing.assert_close(res[1]["p2p"], torch.tensor([42.0]))
+
+
+@pytest.mark.parametrize("diverge", [False, True])
+def test_collective_fingerprint_check(tmp_path, diverge):
+    spawn(_workers.fingerprint_check, args=(2, free_port(), str(tmp_path), diverge), nprocs=2)
+    res = _load(tmp_path, 2)
+    if diverge:
+        assert not any(r["ok"] for r in res) and "all_reduce.min" in res[0]["msg"]
+    else:
+        assert all(r["ok"] and r["n"] == 2 for r in res)
