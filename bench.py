@@ -56,6 +56,8 @@ def parse(argv=None):
                     help="gradient all-reduce of the fused engine: in-kernel one-shot xGMI (auto: if its "
                          "self-test passes on every rank) or RCCL")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--persist", default=None, choices=["auto", "wave", "workgroup"],
+                    help="persistent engine variant (default: $PTDT_PERSIST or auto)")
     ap.add_argument("--stamps", action="store_true",
                     help="persistent engine: diagnostic run with in-kernel phase timers (separate from the timed run)")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
@@ -106,6 +108,8 @@ def run_fused(args, rank, world, dev, comm):
     if world > 1:
         comm.broadcast(eng.P, 0)  # DDP init: rank 0's parameters everywhere
     sampler = DeviceDistributedSampler(len(ds), world, rank, seed=args.seed, device=dev)
+    variant = args.persist
+    which = eng.persistent_engine(args.batch_size, sampler, variant)
     B = args.batch_size
     ns = sampler.num_samples
     S = math.ceil(ns / B)
@@ -182,22 +186,26 @@ def run_persistent(args, rank, world, dev, comm):
     if world > 1:
         comm.broadcast(eng.P, 0)  # DDP init: rank 0's parameters everywhere
     sampler = DeviceDistributedSampler(len(ds), world, rank, seed=args.seed, device=dev)
+    variant = args.persist
+    which = eng.persistent_engine(args.batch_size, sampler, variant)
     S = math.ceil(sampler.num_samples / args.batch_size)
     cursor = torch.zeros(2, dtype=torch.int32, device=dev)
     chunk = 8192
     losses = torch.zeros(min(chunk, max(args.steps, args.warmup, 1)), device=dev)
-    eng.run_persistent(X, Y, max(args.warmup, 1), args.batch_size, sampler, cursor, losses, chunk)
+    eng.run_persistent(X, Y, max(args.warmup, 1), args.batch_size, sampler, cursor, losses, chunk, variant=variant)
     torch.cuda.synchronize(dev)
     t = _timed(comm, dev, lambda: eng.run_persistent(X, Y, args.steps, args.batch_size, sampler, cursor, losses,
-                                                     chunk))
+                                                     chunk, variant=variant))
     if xg is not None:
         xg.check()
     phase = None
     if args.stamps:  # diagnostic pass AFTER the timed region (timers cost a little)
         st = torch.zeros(9, dtype=torch.int64, device=dev)
-        eng.run_persistent(X, Y, args.steps, args.batch_size, sampler, cursor, losses, chunk, stamps=st)
+        eng.run_persistent(X, Y, args.steps, args.batch_size, sampler, cursor, losses, chunk, stamps=st,
+                           variant=variant)
         v = st.tolist()
-        names = ["prefetch_issue", "forward", "loss", "backward", "allreduce", "sgd_land", "epoch_indices"]
+        names = (["fetch", "forward", "loss", "backward", "allreduce", "sgd_loss_report"] if which == "wave" else
+                 ["prefetch_issue", "forward", "loss", "backward", "allreduce", "sgd_land", "epoch_indices"])
         clk = v[7] / (v[8] * 10e-9) if v[8] else 0.0
         phase = {"cycles_per_step": {n: round(v[k] / args.steps, 1) for k, n in enumerate(names)},
                  "total_cycles_per_step": round(v[7] / args.steps, 1), "clock_GHz": round(clk / 1e9, 3)}
@@ -205,8 +213,12 @@ def run_persistent(args, rank, world, dev, comm):
     extra = {"steps_per_epoch": S, "launches_timed": math.ceil(args.steps / chunk),
              "final_loss": float(losses[last].item()),
              "allreduce": "xgmi-oneshot (in-kernel)" if world > 1 else "identity (world 1)",
-             "kernels": "persistent DDP step engine: per step gather+fwd+loss+bwd+all-reduce+SGD in one resident "
-                        "workgroup; sampler shard recomputed in-kernel each epoch"}
+             "persistent_engine": which,
+             "kernels": ("persistent DDP step engine, single-wave variant: batch/weights/momentum/grads in VGPRs, "
+                         "DPP row/column reductions, in-kernel xGMI all-reduce + SGD per step, sampler shard "
+                         "rebuilt each epoch by helper waves" if which == "wave" else
+                         "persistent DDP step engine: per step gather+fwd+loss+bwd+all-reduce+SGD in one resident "
+                         "workgroup; sampler shard recomputed in-kernel each epoch")}
     if phase:
         extra["phase_timers"] = phase
     return t, extra

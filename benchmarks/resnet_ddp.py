@@ -35,6 +35,8 @@ def main(argv=None):
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no_channels_last", action="store_true")
     ap.add_argument("--bucket_cap_mb", type=float, default=None)
+    ap.add_argument("--impl", default="native", choices=["native", "torch"],
+                    help="native DDP reducer + fused optimizer, or stock torch DDP + torch.optim.SGD (comparator)")
     a = ap.parse_args(argv)
 
     from pytorch_distributed_training_tutorials_amd import native
@@ -53,8 +55,14 @@ def main(argv=None):
     model = resnet50(num_classes=1000).to(dev)
     if not a.no_channels_last:
         model = model.to(memory_format=torch.channels_last)
-    ddp = DistributedDataParallel(model, device_ids=[dev.index], comm=comm, bucket_cap_mb=a.bucket_cap_mb)
-    opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    if a.impl == "native":
+        ddp = DistributedDataParallel(model, device_ids=[dev.index], comm=comm, bucket_cap_mb=a.bucket_cap_mb)
+        opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    else:
+        from torch.nn.parallel import DistributedDataParallel as TorchDDP
+
+        ddp = TorchDDP(model, device_ids=[dev.index], bucket_cap_mb=a.bucket_cap_mb or 25)
+        opt = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
     x = torch.empty(a.batch_size, 3, a.image, a.image, device=dev)
     native().philox_(x, 1234 + rank, 0, 1)
     if not a.no_channels_last:
@@ -63,7 +71,10 @@ def main(argv=None):
     amp = a.dtype == "bf16"
 
     def step():
-        ddp.zero_grad()
+        if a.impl == "native":
+            ddp.zero_grad()
+        else:
+            opt.zero_grad()
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
             out = ddp(x)
         loss = cross_entropy(out.float(), y)
@@ -92,7 +103,8 @@ def main(argv=None):
             "dtype": a.dtype, "data": "synthetic ImageNet-shaped (generated on device)",
             "config": {"model": "resnet50", "per_device_batch": a.batch_size, "image": a.image,
                        "parallelism": f"dp{world}", "channels_last": not a.no_channels_last},
-            "buckets_MB": [round(b / 2 ** 20, 2) for b in ddp.bucket_sizes_bytes()],
+            "impl": a.impl,
+            "buckets_MB": [round(b / 2 ** 20, 2) for b in ddp.bucket_sizes_bytes()] if a.impl == "native" else None,
             "final_loss": float(loss.detach()),
         }), flush=True)
     env.destroy_process_group()

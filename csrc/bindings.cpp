@@ -118,7 +118,7 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
                              double lr, double momentum, double dampening, double weight_decay, bool nesterov,
                              std::shared_ptr<XgmiComm> ar, int64_t n_steps, int64_t W, int64_t rank,
                              int64_t num_samples, bool shuffle, int64_t seed, Tensor cursor, Tensor losses,
-                             c10::optional<Tensor> stamps) {
+                             c10::optional<Tensor> stamps, int64_t variant) {
   check_gpu(X, "X");
   check_gpu(P, "P");
   check_gpu(G, "G");
@@ -139,9 +139,6 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
   if (mom.has_value() && mom->defined()) TORCH_CHECK(mom->numel() == np && mom->is_cuda());
   const int world = ar ? ar->world() : 1;
   TORCH_CHECK(world == W, "persistent: all-reduce world != sampler world");
-  TORCH_CHECK(fused_mlp_persistent_lds_bytes((int)B, (int)Din, (int)H, (int)Dout, (int)num_samples, world) <=
-                  160 * 1024,
-              "persistent: model + epoch index list do not fit one workgroup's LDS");
   c10::hip::HIPGuard guard(X.device().index());
   FusedMlpArgs a{};
   a.X = X.data_ptr<float>();
@@ -181,7 +178,25 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
     TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == at::kLong && stamps->numel() >= 9, "stamps: int64[9]");
     pa.stamps = stamps->data_ptr<int64_t>();
   }
+  pa.variant = (int)variant;
+  const bool wave = variant != kPersistWorkgroup && linear_wave_supported(a, pa);
+  TORCH_CHECK(wave || variant != kPersistWave, "persistent: the wave engine does not support this configuration");
+  TORCH_CHECK(wave || fused_mlp_persistent_lds_bytes((int)B, (int)Din, (int)H, (int)Dout, (int)num_samples,
+                                                     world) <= 160 * 1024,
+              "persistent: model + epoch index list do not fit one workgroup's LDS");
   hip_check(fused_mlp_persistent(a, pa, cur_stream(X)), "fused_mlp_persistent");
+}
+
+// Which persistent engine fused_mlp_persistent would run for this configuration.
+std::string persistent_engine(int64_t B, int64_t Din, int64_t H, int64_t Dout, int64_t loss_kind, int64_t num_samples,
+                              int64_t world, int64_t variant) {
+  FusedMlpArgs a{};
+  a.B = (int)B; a.Din = (int)Din; a.H = (int)H; a.Dout = (int)Dout; a.loss_kind = (int)loss_kind;
+  a.ar.world = (int)world;
+  PersistArgs pa{};
+  pa.num_samples = (int)num_samples;
+  if (variant != kPersistWorkgroup && linear_wave_supported(a, pa)) return "wave";
+  return "workgroup";
 }
 
 // ------------------------------------------------------------- optimizers
@@ -547,7 +562,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("Dout"), py::arg("loss_kind"), py::arg("ignore_index"), py::arg("has_bias"), py::arg("lr"),
         py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"), py::arg("nesterov"), py::arg("ar"),
         py::arg("n_steps"), py::arg("W"), py::arg("rank"), py::arg("num_samples"), py::arg("shuffle"),
-        py::arg("seed"), py::arg("cursor"), py::arg("losses"), py::arg("stamps") = py::none());
+        py::arg("seed"), py::arg("cursor"), py::arg("losses"), py::arg("stamps") = py::none(),
+        py::arg("variant") = 0);
+  m.def("persistent_engine", &persistent_engine, py::arg("B"), py::arg("Din"), py::arg("H"), py::arg("Dout"),
+        py::arg("loss_kind"), py::arg("num_samples"), py::arg("world"), py::arg("variant") = 0);
   m.def("fused_mlp_lds_bytes", [](int B, int Din, int H, int Dout) { return fused_mlp_lds_bytes(B, Din, H, Dout); });
   m.def("sgd_flat_", &sgd_flat_);
   m.def("adam_flat_", &adam_flat_);

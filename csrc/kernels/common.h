@@ -18,6 +18,21 @@
 
 namespace ptdt {
 
+// Explicit global address space for pointers that arrive inside by-value
+// argument structs: the compiler cannot infer it there and would emit flat_*
+// instructions (slower, and counted in lgkmcnt as well as vmcnt).
+#define PTDT_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ const T PTDT_GLOBAL* gptr(const T* p) {
+  return (const T PTDT_GLOBAL*)p;
+}
+template <typename T>
+__device__ __forceinline__ T PTDT_GLOBAL* gptr_w(T* p) {
+  return (T PTDT_GLOBAL*)p;
+}
+
+__host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
+
 // ---------------------------------------------------------------- bf16 <-> f32
 // bf16 is stored as raw uint16_t in every kernel signature (no vendor types in
 // the ABI), converted with round-to-nearest-even.

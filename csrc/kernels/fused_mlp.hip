@@ -65,7 +65,6 @@ __device__ __forceinline__ float dot_lds(const float* x, const float* w, int n, 
   return acc0 + acc1;
 }
 
-__host__ __device__ __forceinline__ int al4(int n) { return (n + 3) & ~3; }
 
 struct Dims {
   int B, Din, H, Dout, Dh, nW1, nb1, nW2, nb2, np;
@@ -88,18 +87,21 @@ struct Scratch {
 template <int LOSS>
 __device__ __forceinline__ void gather_batch(const FusedMlpArgs& a, const Dims& d, const int* sel, const Scratch& s,
                                              int tid, int NT) {
+  const auto X = gptr(a.X);
   for (int e = tid; e < d.B * d.Din; e += NT) {
     const int b = e / d.Din, k = e - b * d.Din;
-    s.xs[e] = a.X[(int64_t)sel[b] * d.Din + k];
+    s.xs[e] = X[(int64_t)sel[b] * d.Din + k];
   }
   if constexpr (LOSS != kLossCEIndex) {
+    const auto Yf = gptr(a.Yf);
     for (int e = tid; e < d.B * d.Dout; e += NT) {
       const int b = e / d.Dout, c = e - b * d.Dout;
-      s.ys[e] = a.Yf[(int64_t)sel[b] * d.Dout + c];
+      s.ys[e] = Yf[(int64_t)sel[b] * d.Dout + c];
     }
   } else {
+    const auto Yi = gptr(a.Yi);
     int* yl = reinterpret_cast<int*>(s.ys);
-    for (int b = tid; b < d.B; b += NT) yl[b] = (int)a.Yi[sel[b]];
+    for (int b = tid; b < d.B; b += NT) yl[b] = (int)Yi[sel[b]];
   }
 }
 
@@ -109,13 +111,23 @@ __device__ __forceinline__ void gather_batch(const FusedMlpArgs& a, const Dims& 
 // dependent chain), then log2(G) DPP adds inside the group. Replaces
 // one-thread-per-output serial loops whose dependent LDS loads made the step
 // latency-bound (profiles/).
-template <int G, typename Term, typename Store>
-__device__ __forceinline__ void group_reduce(int E, int R, Term term, Store store, int tid, int NT) {
+// runtime group size (1, 2, 4, 8, 16): uniform branches, one code copy
+__device__ __forceinline__ float group_sum_rt(float v, int G) {
+  if (G >= 2) v += dpp_f<kDppXor1>(v);
+  if (G >= 4) v += dpp_f<kDppXor2>(v);
+  if (G >= 8) v += dpp_f<kDppHalfMirror>(v);
+  if (G >= 16) v += dpp_f<kDppMirror>(v);
+  return v;
+}
+
+template <typename Term, typename Store>
+__device__ __forceinline__ void group_reduce(int G, int E, int R, Term term, Store store, int tid, int NT) {
   const int g = tid & (G - 1);
+  const int per = NT / G;
   // every lane runs the same number of outer iterations so the DPP adds see a full wave
-  const int rounds = (E + NT / G - 1) / (NT / G);
+  const int rounds = (E + per - 1) / per;
   for (int it = 0; it < rounds; ++it) {
-    const int e = it * (NT / G) + tid / G;
+    const int e = it * per + tid / G;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     if (e < E) {
       int r = g;
@@ -127,25 +139,26 @@ __device__ __forceinline__ void group_reduce(int E, int R, Term term, Store stor
       }
       for (; r < R; r += G) a0 += term(e, r);
     }
-    const float v = group_sum<G>((a0 + a1) + (a2 + a3));
+    const float v = group_sum_rt((a0 + a1) + (a2 + a3), G);
     if (e < E && g == 0) store(e, v);
   }
 }
 
 // out[e] = dot(x_row(e), w_row(e)) of length R with groups of G lanes, each
 // lane owning contiguous 4-float chunks (ds_read_b128) when vec4 holds.
-template <int G, typename XRow, typename WRow, typename Store>
-__device__ __forceinline__ void group_dot(int E, int R, bool vec4, XRow xrow, WRow wrow, Store store, int tid,
+template <typename XRow, typename WRow, typename Store>
+__device__ __forceinline__ void group_dot(int G, int E, int R, bool vec4, XRow xrow, WRow wrow, Store store, int tid,
                                           int NT) {
   const int g = tid & (G - 1);
-  const int rounds = (E + NT / G - 1) / (NT / G);
+  const int per = NT / G;
+  const int rounds = (E + per - 1) / per;
   for (int it = 0; it < rounds; ++it) {
-    const int e = it * (NT / G) + tid / G;
+    const int e = it * per + tid / G;
     float a0 = 0.f, a1 = 0.f;
     if (e < E) {
       const float* x = xrow(e);
       const float* w = wrow(e);
-      int k = 0;
+      int k;
       if (vec4) {
         for (k = 4 * g; k + 4 <= R; k += 4 * G) {
           const float4 xv = *reinterpret_cast<const float4*>(x + k);
@@ -160,7 +173,7 @@ __device__ __forceinline__ void group_dot(int E, int R, bool vec4, XRow xrow, WR
         for (k = g; k < R; k += G) a0 = fmaf(x[k], w[k], a0);
       }
     }
-    const float v = group_sum<G>(a0 + a1);
+    const float v = group_sum_rt(a0 + a1, G);
     if (e < E && g == 0) store(e, v);
   }
 }
@@ -174,18 +187,6 @@ __device__ __forceinline__ int pick_group(int E, int R, int NT, int min_terms = 
   while (g < 16 && E * (g * 2) <= NT && R >= min_terms * g * 2) g *= 2;
   return g;
 }
-
-#define PTDT_GROUP_DISPATCH(FN, G, ...)           \
-  do {                                            \
-    switch (G) {                                  \
-      case 16: FN<16>(__VA_ARGS__); break;        \
-      case 8: FN<8>(__VA_ARGS__); break;          \
-      case 4: FN<4>(__VA_ARGS__); break;          \
-      case 2: FN<2>(__VA_ARGS__); break;          \
-      default: FN<1>(__VA_ARGS__); break;         \
-    }                                             \
-  } while (0)
-#define PTDT_GROUP_REDUCE(G, ...) PTDT_GROUP_DISPATCH(group_reduce, G, __VA_ARGS__)
 
 // Diagnostic phase timers (thread 0, s_memtime cycles); `on` is false in
 // production launches, so every tick is one uniform branch.
@@ -224,7 +225,7 @@ __device__ __forceinline__ void step_body(const FusedMlpArgs& a, const Dims& d, 
   // ---- forward
   if constexpr (HID) {
     const bool v_in = (Din & 3) == 0;
-    PTDT_GROUP_DISPATCH(group_dot, pick_group(B * H, Din, NT, 8), B * H, Din, v_in,
+    group_dot(pick_group(B * H, Din, NT, 8), B * H, Din, v_in,
                         [&](int e) { return xs + (e / H) * Din; }, [&](int e) { return W1 + (e % H) * Din; },
                         [&](int e, float v) { as[e] = fmaxf(v + (bias1 ? b1[e % H] : 0.f), 0.f); }, tid, NT);
     __syncthreads();
@@ -232,7 +233,7 @@ __device__ __forceinline__ void step_body(const FusedMlpArgs& a, const Dims& d, 
   const float* act = HID ? as : xs;
   {
     const bool v_out = (Dh & 3) == 0 && ((d.nW1 + d.nb1) & 3) == 0;
-    PTDT_GROUP_DISPATCH(group_dot, pick_group(B * Dout, Dh, NT, 8), B * Dout, Dh, v_out,
+    group_dot(pick_group(B * Dout, Dh, NT, 8), B * Dout, Dh, v_out,
                         [&](int e) { return act + (e / Dout) * Dh; }, [&](int e) { return W2 + (e % Dout) * Dh; },
                         [&](int e, float v) { zs[e] = v + (bias2 ? b2[e % Dout] : 0.f); }, tid, NT);
   }
@@ -302,7 +303,7 @@ __device__ __forceinline__ void step_body(const FusedMlpArgs& a, const Dims& d, 
   float* gb1 = gdst + d.nW1;
   float* gW2 = gdst + d.nW1 + d.nb1;
   float* gb2 = gW2 + d.nW2;
-  PTDT_GROUP_REDUCE(pick_group(d.nW2 + d.nb2, B, NT), d.nW2 + d.nb2, B,
+  group_reduce(pick_group(d.nW2 + d.nb2, B, NT), d.nW2 + d.nb2, B,
                     [&](int e, int b) {
                       if (e < d.nW2) {
                         const int c = e / Dh, j = e - c * Dh;
@@ -325,7 +326,7 @@ __device__ __forceinline__ void step_body(const FusedMlpArgs& a, const Dims& d, 
       ds[e] = sm;
     }
     __syncthreads();
-    PTDT_GROUP_REDUCE(pick_group(d.nW1 + d.nb1, B, NT), d.nW1 + d.nb1, B,
+    group_reduce(pick_group(d.nW1 + d.nb1, B, NT), d.nW1 + d.nb1, B,
                       [&](int e, int b) {
                         if (e < d.nW1) {
                           const int j = e / Din, k = e - j * Din;
@@ -447,20 +448,21 @@ struct Prefetch {
   int yi[kPf];
   __device__ __forceinline__ void issue(const FusedMlpArgs& a, const int* sel, int B, int Din, int Dout, int tid,
                                         int NT) {
+    const auto X = gptr(a.X);
 #pragma unroll
     for (int q = 0; q < kPf; ++q) {
       const int e = tid + q * NT;
       if (e < B * Din) {
         const int b = e / Din;
-        x[q] = a.X[(int64_t)sel[b] * Din + (e - b * Din)];
+        x[q] = X[(int64_t)sel[b] * Din + (e - b * Din)];
       }
       if constexpr (LOSS != kLossCEIndex) {
         if (e < B * Dout) {
           const int b = e / Dout;
-          y[q] = a.Yf[(int64_t)sel[b] * Dout + (e - b * Dout)];
+          y[q] = gptr(a.Yf)[(int64_t)sel[b] * Dout + (e - b * Dout)];
         }
       } else {
-        if (e < B) yi[q] = (int)a.Yi[sel[e]];
+        if (e < B) yi[q] = (int)gptr(a.Yi)[sel[e]];
       }
     }
   }
@@ -491,22 +493,22 @@ __global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs
   float* Ps = lds;                                 // live parameters
   float* Ms = Ps + al4(np);                        // live momentum
   float* gs = Ms + al4(np);                        // grads of the current step
-  float* xsb[2];
-  float* ysb[2];
-  xsb[0] = gs + al4(np);
-  xsb[1] = xsb[0] + al4(B * full.Din);
-  ysb[0] = xsb[1] + al4(B * full.Din);
-  ysb[1] = ysb[0] + ylen;
+  // double-buffered batch: buffer k at xs0 + k * xstride (offset arithmetic keeps the
+  // pointers provably LDS -> ds_* instructions, never flat_*)
+  float* const xs0 = gs + al4(np);
+  const int xstride = al4(B * full.Din);
+  float* const ys0 = xs0 + 2 * xstride;
+  const int ystride = ylen;
   Scratch s;
-  s.as = ysb[1] + ylen;
+  s.as = ys0 + 2 * ystride;
   s.zs = s.as + al4(B * full.H);
   s.ds = s.zs + al4(B * full.Dout);
   s.red = s.ds + al4(B * full.H);
   float* tmp = s.red + 32;                         // [world * np]
-  int* ebuf[2];
-  ebuf[0] = reinterpret_cast<int*>(tmp + al4((a.ar.world > 1 ? a.ar.world : 1) * np));  // epoch index lists
-  ebuf[1] = ebuf[0] + al4(pa.num_samples);
-  int* lds_err = ebuf[1] + al4(pa.num_samples);   // set by a timed-out poll
+  int* const eb0 = reinterpret_cast<int*>(tmp + al4((a.ar.world > 1 ? a.ar.world : 1) * np));  // epoch lists
+  const int estride = al4(pa.num_samples);
+  auto ebuf = [&](int e) { return eb0 + (e & 1) * estride; };
+  int* lds_err = eb0 + 2 * estride;               // set by a timed-out poll
   if (tid == 0) *lds_err = 0;
 
   // ---- load resident state; index lists of the current and the next epoch
@@ -518,19 +520,19 @@ __global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs
   const int steps_per_epoch = (pa.num_samples + B - 1) / B;
   int opt_step = a.opt_step ? *a.opt_step : 0;
   uint32_t seq = a.ar.world > 1 ? *a.ar.seq : 0u;
-  rank_epoch_indices(ebuf[epoch & 1], (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch, pa.shuffle,
+  rank_epoch_indices(ebuf(epoch), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch, pa.shuffle,
                      tid, NT);
-  rank_epoch_indices(ebuf[(epoch + 1) & 1], (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
+  rank_epoch_indices(ebuf(epoch + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
                      pa.shuffle, tid, NT);
   __syncthreads();
   const bool pf_ok = B * full.Din <= kPf * NT && B * (FY ? full.Dout : 1) <= kPf * NT;
   auto batch_size = [&](int jj) { return pa.num_samples - jj * B < B ? pa.num_samples - jj * B : B; };
   {  // first batch (synchronous)
     Scratch s0 = s;
-    s0.xs = xsb[0];
-    s0.ys = ysb[0];
+    s0.xs = xs0;
+    s0.ys = ys0;
     const Dims d0(batch_size(j), full.Din, full.H, full.Dout, a.has_bias != 0);
-    gather_batch<LOSS>(a, d0, ebuf[epoch & 1] + j * B, s0, tid, NT);
+    gather_batch<LOSS>(a, d0, ebuf(epoch) + j * B, s0, tid, NT);
   }
   __syncthreads();
 
@@ -549,7 +551,7 @@ __global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs
       ++ne;
     }
     if (j == 0 && step > 0) {
-      rank_epoch_indices(ebuf[(epoch + 1) & 1], (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
+      rank_epoch_indices(ebuf(epoch + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
                          pa.shuffle, tid, NT);
       __syncthreads();
     }
@@ -557,11 +559,11 @@ __global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs
     Prefetch<LOSS> pf;
     const int nb = batch_size(nj);
     const bool have_next = step + 1 < pa.n_steps;
-    if (pf_ok && have_next) pf.issue(a, ebuf[ne & 1] + nj * B, nb, full.Din, full.Dout, tid, NT);
+    if (pf_ok && have_next) pf.issue(a, ebuf(ne) + nj * B, nb, full.Din, full.Dout, tid, NT);
     st.tick(0);
 
-    s.xs = xsb[cur];
-    s.ys = ysb[cur];
+    s.xs = xs0 + cur * xstride;
+    s.ys = ys0 + cur * ystride;
     const Dims d(batch_size(j), full.Din, full.H, full.Dout, a.has_bias != 0);
     step_body<HID, LOSS>(a, d, Ps, s, gs, false, pa.losses + step, tid, NT, st);
     __syncthreads();
@@ -577,13 +579,13 @@ __global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs
     // land the prefetched batch in the other buffer (last read two steps ago)
     if (have_next) {
       if (pf_ok) {
-        pf.land(xsb[cur ^ 1], ysb[cur ^ 1], nb, full.Din, full.Dout, tid, NT);
+        pf.land(xs0 + (cur ^ 1) * xstride, ys0 + (cur ^ 1) * ystride, nb, full.Din, full.Dout, tid, NT);
       } else {
         Scratch sn = s;
-        sn.xs = xsb[cur ^ 1];
-        sn.ys = ysb[cur ^ 1];
+        sn.xs = xs0 + (cur ^ 1) * xstride;
+        sn.ys = ys0 + (cur ^ 1) * ystride;
         const Dims dn(nb, full.Din, full.H, full.Dout, a.has_bias != 0);
-        gather_batch<LOSS>(a, dn, ebuf[ne & 1] + nj * B, sn, tid, NT);
+        gather_batch<LOSS>(a, dn, ebuf(ne) + nj * B, sn, tid, NT);
       }
     }
     j = nj;
@@ -698,6 +700,8 @@ hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hip
     return hipErrorInvalidValue;
   if (a.ar.world > 1 && (num_params(a) > a.ar.max_elems || a.ar.world != p.W || a.ar.rank != p.rank))
     return hipErrorInvalidValue;
+  if (p.variant != kPersistWorkgroup && linear_wave_supported(a, p)) return linear_wave_persistent(a, p, s);
+  if (p.variant == kPersistWave) return hipErrorInvalidValue;
   const size_t lds = fused_mlp_persistent_lds_bytes(a.B, a.Din, a.H, a.Dout, p.num_samples, a.ar.world);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const void* fn = a.H > 0 ? pick_persist<true>(a.loss_kind) : pick_persist<false>(a.loss_kind);

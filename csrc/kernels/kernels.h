@@ -70,8 +70,16 @@ struct PersistArgs {
   float* losses;         // [n_steps] per-step mean loss
   int64_t* stamps;       // optional [9] diagnostic phase timers (s_memtime cycles, thread 0): prefetch issue,
                          // forward, loss, backward, all-reduce, sgd+land, epoch indices, total, realtime (100 MHz)
+  int variant;           // kPersistAuto / kPersistWorkgroup / kPersistWave
 };
+// Engine choice: the register-resident single-wave engine (linear_wave.hip) runs
+// Linear(Din, Dout) models with B <= 64 and small Dout; everything else runs the
+// LDS workgroup engine (fused_mlp.hip). kPersistAuto picks the wave engine when
+// it supports the configuration.
+enum PersistVariant : int { kPersistAuto = 0, kPersistWorkgroup = 1, kPersistWave = 2 };
 hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s);
+bool linear_wave_supported(const FusedMlpArgs& a, const PersistArgs& p);
+hipError_t linear_wave_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s);
 size_t fused_mlp_persistent_lds_bytes(int B, int Din, int H, int Dout, int num_samples, int world);
 // LDS bytes the step needs (host check against the 160 KiB per-CU budget).
 size_t fused_mlp_lds_bytes(int B, int Din, int H, int Dout);

@@ -1,0 +1,514 @@
+// Register-resident single-wave DDP step engine for Linear(Din, Dout) models.
+//
+// The flagship workload (ddp_gpus_torchrun.py:19-40 / SURVEY M4-M5: Linear(20,1),
+// soft-target cross-entropy, SGD, 32 samples per rank per step, one all-reduce
+// per step) is ~2k FLOPs per step: pure latency. The workgroup engine
+// (fused_mlp.hip) keeps everything in LDS but still pays a chain of
+// LDS round trips and s_barriers per phase. This engine removes both:
+//
+//   * ONE wave trains. Lane (r, p) owns batch row r (r < 64 / L) and feature
+//     chunk p (KP consecutive features, L = lanes per row), so the batch, the
+//     weights, the momentum and the gradients all live in VGPRs.
+//   * forward  : KP FMAs + a DPP row-group sum over the L lanes of a row;
+//   * loss     : computed redundantly by the L lanes of a row (no exchange);
+//   * backward : g * x per lane, then a rotation/permlane column sum over the
+//     rows -- every lane ends with the full-batch gradient of ITS chunk, with
+//     the same bits in every lane (each butterfly stage adds a+b / b+a);
+//   * all-reduce (world > 1): lanes of row q push the chunk to peer q and poll
+//     peer q's contribution (xGMI one-shot, LL words, csrc/comm/xgmi.h), then
+//     the same column sum adds the ranks -- identical on every rank;
+//   * SGD      : each lane updates its own chunk in registers.
+//   No s_barrier, no LDS traffic on the critical path. Batches are gathered
+//   from the device-resident dataset NB steps ahead into register buffers
+//   (indices read one step earlier still), so the L2 latency is hidden.
+//   Waves 1-3 build the next epoch's sampler index list (Feistel permutation,
+//   sampler.h) in LDS while wave 0 trains; the two meet at one s_barrier per
+//   epoch.
+// Configurations: KP (features per lane, zero padded), DOUT and the loss are
+// template parameters; anything else runs the workgroup engine.
+#pragma once
+#include "common.h"
+#include "kernels.h"
+#include "sampler.h"
+
+namespace ptdt {
+namespace lw {
+
+constexpr int kNB = 3;           // batches in flight (register buffers)
+constexpr int kThreads = 256;    // wave 0 trains, waves 1-3 build index lists
+
+__device__ __forceinline__ float swap16_add(float v) {
+#pragma clang fp contract(off)
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(p[0]) + __int_as_float(p[1]);
+}
+__device__ __forceinline__ float swap32_add(float v) {
+#pragma clang fp contract(off)
+  auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(p[0]) + __int_as_float(p[1]);
+}
+
+// Sum over the aligned group of L lanes of one batch row (L a power of two).
+// L is a template parameter: a runtime L turns every stage into a branch.
+// No FMA contraction inside the reductions: fma(g_i, x_i, g_j*x_j) on lane i and
+// fma(g_j, x_j, g_i*x_i) on lane j round differently, and replicas would drift.
+template <int L>
+__device__ __forceinline__ float row_sum(float v) {
+#pragma clang fp contract(off)
+  if constexpr (L >= 2) v += dpp_f<kDppXor1>(v);
+  if constexpr (L >= 4) v += dpp_f<kDppXor2>(v);
+  if constexpr (L >= 8) v += dpp_f<kDppHalfMirror>(v);
+  if constexpr (L >= 16) v += dpp_f<kDppMirror>(v);
+  if constexpr (L >= 32) v = swap16_add(v);
+  if constexpr (L >= 64) v = swap32_add(v);
+  return v;
+}
+
+// Sum over all lanes with the same (lane % L): one feature chunk across rows.
+// Rotations by 8,4,2,1 inside a 16-lane DPP row (row_ror), then the two
+// permlane swaps. Each stage pairs lanes symmetrically, so every lane gets the
+// same bits.
+constexpr int kDppRor8 = 0x128, kDppRor4 = 0x124, kDppRor2 = 0x122, kDppRor1 = 0x121;
+template <int L>
+__device__ __forceinline__ float col_sum(float v) {
+#pragma clang fp contract(off)
+  if constexpr (L <= 8) v += dpp_f<kDppRor8>(v);
+  if constexpr (L <= 4) v += dpp_f<kDppRor4>(v);
+  if constexpr (L <= 2) v += dpp_f<kDppRor2>(v);
+  if constexpr (L <= 1) v += dpp_f<kDppRor1>(v);
+  if constexpr (L <= 16) v = swap16_add(v);
+  if constexpr (L <= 32) v = swap32_add(v);
+  return v;
+}
+
+// Optional per-phase s_memtime accounting (PersistArgs::stamps). Accumulators
+// live in LDS, not SGPRs: the untimed build of the loop must not pay register
+// pressure for diagnostics.
+struct Ticks {
+  bool on = false;
+  int64_t prev = 0;
+  unsigned long long* acc = nullptr;  // LDS [8]
+  __device__ __forceinline__ void start() {
+    if (on) prev = (int64_t)__builtin_amdgcn_s_memtime();
+  }
+  __device__ __forceinline__ void tick(int k) {
+    if (on) {
+      const int64_t t = (int64_t)__builtin_amdgcn_s_memtime();
+      if (threadIdx.x == 0) acc[k] += (unsigned long long)(t - prev);
+      prev = t;
+    }
+  }
+};
+
+template <int KP, int DOUT>
+struct Batch {
+  float x[KP];
+  float y[DOUT];
+  int yi;
+  int nb;  // rows in this batch (last batch of an epoch may be short)
+};
+
+template <int L, int KP, int DOUT, int LOSS, bool AR>
+__global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, PersistArgs pa) {
+  extern __shared__ int elist[];  // [2][estride] sampler index lists (epoch parity)
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int B = a.B, Din = a.Din;
+  const int estride = al4(pa.num_samples);
+  const int S = (pa.num_samples + B - 1) / B;  // steps per epoch
+  const int e0 = pa.cursor[0], j0 = pa.cursor[1];
+  const int64_t pos0 = (int64_t)e0 * S + j0;
+  const int n = pa.n_steps;
+  const int T = (int)((pos0 + n - 1) / S - pos0 / S);  // epoch transitions inside this launch
+  auto list = [&](int e) { return elist + (e & 1) * estride; };
+
+  rank_epoch_indices(list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
+                     (int)threadIdx.x, kThreads);
+  if (T > 0)
+    rank_epoch_indices(list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1, pa.shuffle,
+                       (int)threadIdx.x, kThreads);
+  __syncthreads();
+  if (wave != 0) {
+    // producers: after the trainer starts prefetching epoch e0+i, the list of
+    // e0+i-1 is dead; build e0+i+1 into its slot before the next transition.
+    for (int i = 1; i <= T; ++i) {
+      __syncthreads();
+      if (i < T)
+        rank_epoch_indices(list(e0 + i + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + i + 1,
+                           pa.shuffle, (int)threadIdx.x - 64, kThreads - 64);
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------ trainer wave
+  const int lane = (int)threadIdx.x;
+  const int r = lane / L, p = lane % L;    // batch row, feature chunk (L lanes per row, 64 / L >= B)
+  const int k0 = p * KP;
+  const bool hb = a.has_bias != 0;
+  const bool use_mom = a.mom != nullptr && a.momentum != 0.f;
+  const float lr = a.lr, mu = a.momentum, damp = a.dampening, wd = a.weight_decay;
+  const int nesterov = a.nesterov;
+  const auto X = gptr(a.X);
+  const int nW = DOUT * Din;
+
+  float W[DOUT][KP], M[DOUT][KP], Wb[DOUT], Mb[DOUT];
+  {
+    const auto P = gptr(a.P);
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        const bool in = k0 + k < Din;
+        W[c][k] = in ? P[c * Din + k0 + k] : 0.f;
+        M[c][k] = (in && use_mom) ? gptr(a.mom)[c * Din + k0 + k] : 0.f;
+      }
+      Wb[c] = hb ? P[nW + c] : 0.f;
+      Mb[c] = (hb && use_mom) ? gptr(a.mom)[nW + c] : 0.f;
+    }
+  }
+  int opt_step = a.opt_step ? *a.opt_step : 0;
+  const XgmiArgs& ar = a.ar;
+  const int world = AR ? ar.world : 1;  // AR == false: single rank, no all-reduce code at all
+  // this lane's push target (row q pushes to rank q) and poll source, selected
+  // once with uniform compares: indexing peers[] by a lane value would spill
+  // the argument array to scratch
+  uint64_t PTDT_GLOBAL* push_dst = nullptr;
+#pragma unroll
+  for (int q = 0; q < kXgmiMaxRanks; ++q)
+    if (r == q && q < world) push_dst = (uint64_t PTDT_GLOBAL*)ar.peers[q];
+  uint64_t PTDT_GLOBAL* const poll_src = (uint64_t PTDT_GLOBAL*)ar.local;
+  const int my_rank = ar.rank, max_elems = ar.max_elems;
+  float PTDT_GLOBAL* const losses = gptr_w(pa.losses);
+  uint32_t seq = AR ? *ar.seq : 0u;
+  bool failed = AR && *ar.err != 0;  // a peer already timed out earlier: do not wait again
+  const float inv_w = 1.f / (float)world;
+
+  // padded feature slots (L * KP > Din): x masked to 0 so W stays 0 there
+  const bool padded = L * KP != Din;
+  float kmask[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) kmask[k] = k0 + k < Din ? 1.f : 0.f;
+  // index lookahead: the dataset row of position `ipos` is read from LDS one
+  // fetch before the gather that uses it
+  int ie = e0, ij = j0, barriers = 0;
+  int sel_next = 0, nb_next = 0;
+  auto read_index = [&]() {
+    if (ij == 0 && ie != e0) {  // entering a new epoch: its list must be ready, the old one is free
+      __syncthreads();
+      ++barriers;
+    }
+    nb_next = min(B, pa.num_samples - ij * B);
+    sel_next = list(ie)[ij * B + min(r, nb_next - 1)];  // rows past the batch re-read its last row
+    if (++ij == S) {
+      ij = 0;
+      ++ie;
+    }
+  };
+  int fetched = 0;
+  auto fetch = [&](Batch<KP, DOUT>& f) {
+    // Unconditional loads from clamped addresses (no exec-mask branches): rows
+    // past the batch get g = 0 in train(), padded features are masked there.
+    const int sel = sel_next;
+    f.nb = nb_next;
+    const auto xr = X + (int64_t)sel * Din + k0;
+    if (!padded) {  // immediate offsets from one address
+#pragma unroll
+      for (int k = 0; k < KP; ++k) f.x[k] = xr[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) f.x[k] = xr[min(k, Din - 1 - k0)];
+    }
+    if constexpr (LOSS == kLossCEIndex) {
+      f.yi = (int)gptr(a.Yi)[sel];
+    } else {
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) f.y[c] = gptr(a.Yf)[(int64_t)sel * DOUT + c];
+    }
+    ++fetched;
+    if (fetched < n) read_index();
+  };
+
+  Ticks tk;
+  tk.on = pa.stamps != nullptr;
+  tk.acc = reinterpret_cast<unsigned long long*>(elist + 2 * estride);
+  if (tk.on && lane == 0)
+    for (int k = 0; k < 8; ++k) tk.acc[k] = 0ull;
+  const float inv_full = 1.f / (float)((LOSS == kLossMSE) ? B * DOUT : B);
+  const float coef_full = a.grad_scale * inv_full;
+  const int64_t t_begin = tk.on ? (int64_t)__builtin_amdgcn_s_memtime() : 0;
+  const int64_t r_begin = tk.on ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+
+
+  auto train = [&](Batch<KP, DOUT>& f, int step) {
+    const int nb = f.nb;
+    const bool valid = r < nb;
+    if (padded) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) f.x[k] *= kmask[k];
+    }
+    // ---- forward
+    float z[DOUT];
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+      float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+      for (int k = 0; k < KP; k += 2) {
+        acc0 = fmaf(f.x[k], W[c][k], acc0);
+        if (k + 1 < KP) acc1 = fmaf(f.x[k + 1], W[c][k + 1], acc1);
+      }
+      z[c] = row_sum<L>(acc0 + acc1) + Wb[c];
+    }
+    tk.tick(1);
+    // ---- loss and dL/dz (the L lanes of a row compute the same values)
+    float g[DOUT], l = 0.f, cnt = 0.f;
+    if constexpr (LOSS == kLossMSE) {
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) {
+        const float df = z[c] - f.y[c];
+        l = fmaf(df, df, l);
+        g[c] = 2.f * df;
+      }
+    } else {
+      float m = z[0];
+#pragma unroll
+      for (int c = 1; c < DOUT; ++c) m = fmaxf(m, z[c]);
+      float se = 0.f;
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) se += __expf(z[c] - m);
+      const float lse = m + __logf(se);
+      if constexpr (LOSS == kLossCESoft) {
+        float tsum = 0.f;
+#pragma unroll
+        for (int c = 0; c < DOUT; ++c) {
+          tsum += f.y[c];
+          l -= f.y[c] * (z[c] - lse);
+        }
+#pragma unroll
+        for (int c = 0; c < DOUT; ++c) g[c] = __expf(z[c] - lse) * tsum - f.y[c];
+      } else {
+        const bool use = f.yi != a.ignore_index;
+        float zy = 0.f;
+#pragma unroll
+        for (int c = 0; c < DOUT; ++c) {
+          zy = c == f.yi ? z[c] : zy;
+          g[c] = use ? __expf(z[c] - lse) - (c == f.yi ? 1.f : 0.f) : 0.f;
+        }
+        l = use ? lse - zy : 0.f;
+        cnt = use ? 1.f : 0.f;
+      }
+    }
+    if (!valid) {
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) g[c] = 0.f;
+      l = 0.f;
+      cnt = 0.f;
+    }
+    float inv_denom;
+    if constexpr (LOSS == kLossCEIndex) {
+      cnt = wave_sum(p == 0 ? cnt : 0.f);  // the one data-dependent denominator
+      inv_denom = 1.f / (cnt > 0.f ? cnt : 1.f);
+    } else {  // division only for a short last batch
+      inv_denom = nb == B ? inv_full : 1.f / (float)((LOSS == kLossMSE) ? nb * DOUT : nb);
+    }
+    const float coef = a.grad_scale * inv_denom;
+    tk.tick(2);
+    // ---- backward: full-batch gradient of this lane's chunk, in every lane
+    float gW[DOUT][KP], gb[DOUT];
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) gW[c][k] = col_sum<L>(g[c] * f.x[k]) * coef;
+      gb[c] = col_sum<L>(g[c]) * coef;
+    }
+    tk.tick(3);
+    // ---- all-reduce over ranks (average): row q <-> rank q
+    if (AR && !failed) {
+      seq += 1u;
+      const int parity = (int)(seq & 1u);
+      auto slot = [&](uint64_t PTDT_GLOBAL* base, int src, int i) {
+        return base + ((int64_t)(parity * world + src) * max_elems + i);
+      };
+      if (r < world && r != my_rank) {
+        uint64_t PTDT_GLOBAL* dst = push_dst;
+#pragma unroll
+        for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+          for (int k = 0; k < KP; ++k)
+            if (k0 + k < Din)
+              __hip_atomic_store(slot(dst, my_rank, c * Din + k0 + k),
+                                 ((uint64_t)seq << 32) | (uint64_t)__float_as_uint(gW[c][k]), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+          if (hb && p == 0)
+            __hip_atomic_store(slot(dst, my_rank, nW + c), ((uint64_t)seq << 32) | (uint64_t)__float_as_uint(gb[c]),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      float v[DOUT][KP], vb[DOUT];
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) {
+        vb[c] = r == my_rank ? gb[c] : 0.f;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) v[c][k] = r == my_rank ? gW[c][k] : 0.f;
+      }
+      if (r < world && r != my_rank) {
+        // all slots of the chunk in flight together; re-poll until every seq matches
+        uint32_t polls = 0;
+        while (true) {
+          bool all = true;
+#pragma unroll
+          for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+            for (int k = 0; k < KP; ++k) {
+              if (k0 + k < Din) {
+                const uint64_t w = __hip_atomic_load(slot(poll_src, r, c * Din + k0 + k), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_SYSTEM);
+                all &= (uint32_t)(w >> 32) == seq;
+                v[c][k] = __uint_as_float((uint32_t)w);
+              }
+            }
+            if (hb) {
+              const uint64_t w =
+                  __hip_atomic_load(slot(poll_src, r, nW + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              all &= (uint32_t)(w >> 32) == seq;
+              vb[c] = __uint_as_float((uint32_t)w);
+            }
+          }
+          if (all) break;
+          if (++polls > kXgmiMaxPolls) {  // a peer is gone: fail loudly, never hang
+            __hip_atomic_store((int PTDT_GLOBAL*)ar.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            failed = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      failed = __any(failed);
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+        for (int k = 0; k < KP; ++k) gW[c][k] = col_sum<L>(v[c][k]) * inv_w;
+        gb[c] = col_sum<L>(vb[c]) * inv_w;
+      }
+    }
+    tk.tick(4);
+    // ---- SGD (torch.optim.SGD semantics) on this lane's chunk
+    const bool first = opt_step == 0;
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        float d = fmaf(wd, W[c][k], gW[c][k]);
+        if (use_mom) {
+          const float buf = first ? d : fmaf(mu, M[c][k], (1.f - damp) * d);
+          M[c][k] = buf;
+          d = nesterov ? fmaf(mu, buf, d) : buf;
+        }
+        W[c][k] = fmaf(-lr, d, W[c][k]);
+      }
+      if (hb) {
+        float d = fmaf(wd, Wb[c], gb[c]);
+        if (use_mom) {
+          const float buf = first ? d : fmaf(mu, Mb[c], (1.f - damp) * d);
+          Mb[c] = buf;
+          d = nesterov ? fmaf(mu, buf, d) : buf;
+        }
+        Wb[c] = fmaf(-lr, d, Wb[c]);
+      }
+    }
+    ++opt_step;
+    if (step == n - 1 && r == 0) {  // the DDP bucket keeps the last step's averaged gradients
+      const auto Gw = gptr_w(a.G);
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+        for (int k = 0; k < KP; ++k)
+          if (k0 + k < Din) Gw[c * Din + k0 + k] = gW[c][k];
+        if (hb && p == 0) Gw[nW + c] = gb[c];
+      }
+    }
+    // ---- loss report (off the critical path: nothing waits on it)
+    const float ls = wave_sum(p == 0 ? l : 0.f);
+    // every lane stores the same value to the same address: no exec-mask branch
+    if constexpr (LOSS == kLossCEIndex) losses[step] = cnt > 0.f ? ls * inv_denom : NAN;
+    else losses[step] = ls * inv_denom;
+    tk.tick(5);
+  };
+
+  Batch<KP, DOUT> buf[kNB];
+  tk.start();
+  read_index();
+#pragma unroll
+  for (int u = 0; u < kNB; ++u)
+    if (u < n) fetch(buf[u]);
+  tk.tick(0);
+  int done = 0;
+  for (int base = 0; base < n && !failed; base += kNB) {
+#pragma unroll
+    for (int u = 0; u < kNB; ++u) {
+      const int step = base + u;
+      if (step < n && !failed) {
+        train(buf[u], step);
+        if (step + kNB < n) fetch(buf[u]);
+        tk.tick(0);
+        done = step + 1;
+      }
+    }
+  }
+  // a failed all-reduce stops training early: still meet the producers at every barrier
+  while (barriers < T) {
+    __syncthreads();
+    ++barriers;
+  }
+
+  // ---- write back resident state (lanes of row 0 hold every chunk)
+  if (r == 0) {
+    const auto Pw = gptr_w(a.P);
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        if (k0 + k < Din) {
+          Pw[c * Din + k0 + k] = W[c][k];
+          if (use_mom) a.mom[c * Din + k0 + k] = M[c][k];
+        }
+      }
+      if (hb && p == 0) {
+        Pw[nW + c] = Wb[c];
+        if (use_mom) a.mom[nW + c] = Mb[c];
+      }
+    }
+  }
+  if (lane == 0) {
+    const int64_t pos = pos0 + done;
+    pa.cursor[0] = (int)(pos / S);
+    pa.cursor[1] = (int)(pos % S);
+    if (a.opt_step) *a.opt_step = opt_step;
+    if (AR) *ar.seq = seq;
+    if (tk.on) {
+      // [0] fetch (index read + gather issue + epoch barrier), [1] forward, [2] loss,
+      // [3] backward, [4] all-reduce, [5] sgd + loss report
+      for (int k = 0; k < 6; ++k) pa.stamps[k] += (int64_t)tk.acc[k];
+      pa.stamps[7] += (int64_t)__builtin_amdgcn_s_memtime() - t_begin;
+      pa.stamps[8] += (int64_t)__builtin_amdgcn_s_memrealtime() - r_begin;
+    }
+  }
+}
+
+// Instantiation table of one loss: (L, KP, DOUT) combinations whose register
+// footprint fits (no scratch). Returns nullptr for anything else.
+template <int LOSS>
+const void* pick(int L, int kp, int dout, bool ar) {
+#define PTDT_LW(LL, KP, DO) \
+  if (L == LL && kp == KP && dout == DO)  \
+    return ar ? (const void*)linear_wave_kernel<LL, KP, DO, LOSS, true> \
+              : (const void*)linear_wave_kernel<LL, KP, DO, LOSS, false>;
+#define PTDT_LW_L(LL) \
+  PTDT_LW(LL, 4, 1) PTDT_LW(LL, 8, 1) PTDT_LW(LL, 10, 1) PTDT_LW(LL, 16, 1) \
+  PTDT_LW(LL, 4, 2) PTDT_LW(LL, 8, 2) PTDT_LW(LL, 10, 2) PTDT_LW(LL, 4, 4)
+  PTDT_LW_L(1) PTDT_LW_L(2) PTDT_LW_L(4) PTDT_LW_L(8)
+#undef PTDT_LW_L
+#undef PTDT_LW
+  return nullptr;
+}
+
+}  // namespace lw
+}  // namespace ptdt

@@ -23,6 +23,8 @@ parameter buffer, and their ``.grad`` views of the flat gradient bucket, so
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -42,6 +44,16 @@ def _linears(model: nn.Module):
     if len(lin) == 2 and relu:
         return lin, True
     raise ValueError("FusedMLPStep supports Linear or Linear-ReLU-Linear models; use the autograd engine otherwise")
+
+
+_VARIANTS = {"auto": 0, "workgroup": 1, "wave": 2}
+
+
+def _variant_id(variant: str | None) -> int:
+    v = variant or os.environ.get("PTDT_PERSIST", "auto")
+    if v not in _VARIANTS:
+        raise ValueError(f"persistent engine variant must be one of {sorted(_VARIANTS)}, got {v!r}")
+    return _VARIANTS[v]
 
 
 class FusedMLPStep:
@@ -132,17 +144,22 @@ class FusedMLPStep:
 
     # ------------------------------------------------------------ persistent engine
     def run_persistent(self, X, Y, n_steps: int, batch_size: int, sampler, cursor: torch.Tensor,
-                       losses: torch.Tensor, max_steps_per_launch: int = 8192, stamps: torch.Tensor | None = None):
-        """Run ``n_steps`` DDP steps in persistent launches (csrc/kernels/fused_mlp.hip):
-        parameters, momentum and the epoch's sampler shard stay resident in LDS,
-        each step = gather -> fwd/loss/bwd -> all-reduce (in-kernel xGMI one-shot;
-        identity at world 1) -> SGD. ``sampler`` is a DeviceDistributedSampler
+                       losses: torch.Tensor, max_steps_per_launch: int = 8192, stamps: torch.Tensor | None = None,
+                       variant: str | None = None):
+        """Run ``n_steps`` DDP steps in persistent launches: each step = gather ->
+        fwd/loss/bwd -> all-reduce (in-kernel xGMI one-shot; identity at world 1)
+        -> SGD. Two engines (``variant``, default ``$PTDT_PERSIST`` or "auto"):
+        "wave" (csrc/kernels/linear_wave.hip: Linear(Din, Dout) models with
+        B <= 64, one wave, weights/momentum/batch in registers) and "workgroup"
+        (csrc/kernels/fused_mlp.hip: any Linear[-ReLU-Linear], state in LDS);
+        "auto" picks the wave engine when it supports the configuration. ``sampler`` is a DeviceDistributedSampler
         (sharding/permutation parameters); ``cursor`` an int32[2] device tensor
         ``[epoch, step_in_epoch]`` advanced by the kernel; ``losses[i]`` receives
         step i's mean loss (``losses`` must hold ``min(n_steps, max_steps_per_launch)``)."""
         if self.xgmi is None and self.comm is not None and self.comm.world > 1:
             raise RuntimeError("the persistent engine needs the xGMI all-reduce for world > 1")
         ce_index = self.loss_kind == LOSS_KINDS["ce_index"]
+        vid = _variant_id(variant)
         done = 0
         while done < n_steps:
             n = min(max_steps_per_launch, n_steps - done)
@@ -151,9 +168,14 @@ class FusedMLPStep:
                 batch_size, self.Din, self.H, self.Dout, self.loss_kind, self.ignore_index, self.has_bias,
                 self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
                 self.xgmi.handle if self.xgmi is not None else None, n, sampler.num_replicas, sampler.rank,
-                sampler.num_samples, sampler.shuffle, sampler.seed, cursor, losses, stamps)
+                sampler.num_samples, sampler.shuffle, sampler.seed, cursor, losses, stamps, vid)
             done += n
         self._pending = False
+
+    def persistent_engine(self, batch_size: int, sampler, variant: str | None = None) -> str:
+        """Which persistent engine :meth:`run_persistent` runs: "wave" or "workgroup"."""
+        return self._C.persistent_engine(batch_size, self.Din, self.H, self.Dout, self.loss_kind,
+                                         sampler.num_samples, sampler.num_replicas, _variant_id(variant))
 
     # ------------------------------------------------------------ hipGraphs
     def state(self):

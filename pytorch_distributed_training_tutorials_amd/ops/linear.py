@@ -76,6 +76,7 @@ class _LinearFn(torch.autograd.Function):
         y = gemm(x2, weight.t(), bias=bias, relu=relu, out_dtype=x.dtype)
         ctx.relu = relu
         ctx.has_bias = bias is not None
+        ctx.bias_dtype = bias.dtype if bias is not None else None
         ctx.in_shape = shape
         ctx.save_for_backward(x2, weight, y if relu else None)
         return y.reshape(*shape[:-1], weight.shape[0])
@@ -97,7 +98,7 @@ class _LinearFn(torch.autograd.Function):
             dw = gemm(dy2.t(), x2, amask=mask.t() if mask is not None else None, colsum=colsum,
                       out_dtype=weight.dtype)
             if colsum is not None:
-                db = colsum if weight.dtype == torch.float32 else colsum.to(weight.dtype)
+                db = colsum if ctx.bias_dtype == torch.float32 else colsum.to(ctx.bias_dtype)
             if not ctx.needs_input_grad[1]:
                 dw = None
         return dx, dw, db, None
@@ -106,6 +107,12 @@ class _LinearFn(torch.autograd.Function):
 def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = None, relu: bool = False):
     """``relu?(x @ weight.T + bias)``: native MFMA path on GPU, ATen on CPU."""
     if use_native(x, weight):
+        if torch.is_autocast_enabled("cuda"):
+            # autocast region: compute in the autocast dtype on MFMA, grads flow
+            # back to the fp32 master weight through the differentiable casts
+            dt = torch.get_autocast_dtype("cuda")
+            if dt in (torch.bfloat16, torch.float32):
+                x, weight = x.to(dt), weight.to(dt)
         if x.dtype not in (torch.float32, torch.bfloat16) or weight.dtype != x.dtype:
             raise TypeError(f"native linear supports fp32/bf16 with matching dtypes, got {x.dtype}/{weight.dtype}")
         return _LinearFn.apply(x, weight, bias, relu)

@@ -20,11 +20,14 @@ for s in $STAGES; do
     tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
     micro) step microbench 120 tools/bin/microbench_launch ;;
     quick) step bench_persistent 300 python bench.py --steps 20000 --warmup 2000 --stamps
+           step bench_persistent_wg 300 python bench.py --steps 20000 --warmup 2000 --stamps --persist workgroup
            step bench_mlp 300 python bench.py --model mlp --steps 20000 --warmup 2000 --stamps
            step bench_fused 300 python bench.py --engine fused --steps 2000 --warmup 200 ;;
     apps)  step mp_toy 300 python model_parallel.py toy
            step mp_resnet 600 python model_parallel.py resnet --repeat 5 --json gpurun_out/mp_resnet.json --fig gpurun_out/mp_vs_single.png
-           step dp_toy 300 python data_parallel.py --quiet ;;
+           step dp_toy 300 python data_parallel.py --quiet
+           step resnet_ddp_native 600 python benchmarks/resnet_ddp.py --steps 20 --warmup 5
+           step resnet_ddp_torch 600 python benchmarks/resnet_ddp.py --steps 20 --warmup 5 --impl torch ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench_persistent 300 python bench.py --steps 20000 --warmup 2000
            step bench_fused 300 python bench.py --engine fused --steps 2000 --warmup 200

@@ -222,7 +222,7 @@ def _per_step_reference(eng, X, Y, sampler, n_steps, B, dev):
     eng.flush()
 
 
-def persistent_two_procs_one_gpu(rank, world, port, out_dir):
+def persistent_two_procs_one_gpu(rank, world, port, out_dir, kind="mlp"):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -239,11 +239,16 @@ def persistent_two_procs_one_gpu(rank, world, port, out_dir):
     ctl = Communicator(device=torch.device("cpu"))
     xg = XgmiAllReduce(ctl, dev, max_elems=4096)
     X = torch.randn(300, 20, generator=torch.Generator().manual_seed(9)).to(dev)
-    Y = torch.randint(0, 4, (300,), generator=torch.Generator().manual_seed(10)).to(dev)
+    Y = torch.randint(0, 4 if kind == "mlp" else 2, (300,), generator=torch.Generator().manual_seed(10)).to(dev)
     out = {}
     for mode in ("persistent", "per_step"):
         torch.manual_seed(5)
-        eng = FusedMLPStep(ToyMLP(20, 16, 4).to(dev), loss="ce_index", lr=0.05, momentum=0.9, xgmi=xg)
+        # "mlp": workgroup engine; "linear": single-wave engine (Linear(20, 4) -> KP 10, DOUT 4 is not
+        # instantiated, so use Linear(20, 2))
+        model = ToyMLP(20, 16, 4) if kind == "mlp" else torch.nn.Linear(20, 2)
+        eng = FusedMLPStep(model.to(dev), loss="ce_index", lr=0.05, momentum=0.9, xgmi=xg)
+        if mode == "persistent":
+            out["engine"] = eng.persistent_engine(16, DeviceDistributedSampler(300, world, rank, seed=3, device=dev))
         sampler = DeviceDistributedSampler(300, world, rank, seed=3, device=dev)
         if mode == "persistent":
             cursor = torch.zeros(2, dtype=torch.int32, device=dev)

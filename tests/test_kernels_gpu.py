@@ -162,6 +162,24 @@ def test_linear_autograd(native, dev, dtype, relu):
     torch.testing.assert_close(b.grad.float(), br.grad, rtol=tol, atol=tol * 4)
 
 
+def test_linear_under_autocast(native, dev):
+    """bf16 autocast over fp32 master weights (ResNet-50 DDP bench path): bf16 MFMA
+    compute, fp32 grads for the fp32 parameters."""
+    from pytorch_distributed_training_tutorials_amd.ops.linear import Linear
+
+    torch.manual_seed(4)
+    m = Linear(64, 48).to(dev)
+    x = torch.randn(40, 64, device=dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    assert y.dtype == torch.bfloat16
+    y.float().sum().backward()
+    assert m.weight.grad.dtype == torch.float32 and m.bias.grad.dtype == torch.float32
+    ref = F.linear(x, m.weight.detach(), m.bias.detach())
+    torch.testing.assert_close(y.float(), ref, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(m.weight.grad, x.sum(0).expand(48, 64), rtol=3e-2, atol=3e-1)
+
+
 def test_linear_long_k_split(native, dev):
     """ToyModel's net1: Linear(10000, 10) + ReLU on [20, 10000] (split-K path)."""
     from pytorch_distributed_training_tutorials_amd.ops.linear import linear

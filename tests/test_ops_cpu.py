@@ -128,3 +128,17 @@ def test_checkpoint_roundtrip_with_module_prefix(tmp_path):
 def test_native_extension_importable_on_cpu():
     C = native()
     assert C.ARCH == "gfx950"
+
+
+def test_persistent_engine_selection():
+    """Host-side dispatch: Linear(Din, Dout) with B <= 64 and an instantiated
+    (features per lane, Dout) pair runs the single-wave engine; anything else the
+    workgroup engine."""
+    C = native()
+    ce_soft, ce_index = 0, 1
+    assert C.persistent_engine(32, 20, 0, 1, ce_soft, 2048, 1) == "wave"        # flagship toy
+    assert C.persistent_engine(32, 20, 0, 1, ce_soft, 256, 8) == "wave"         # 8 ranks
+    assert C.persistent_engine(32, 20, 64, 10, ce_index, 2048, 1) == "workgroup"  # hidden layer
+    assert C.persistent_engine(128, 20, 0, 1, ce_soft, 2048, 1) == "workgroup"  # B > 64
+    assert C.persistent_engine(32, 20, 0, 10, ce_index, 2048, 1) == "workgroup"  # Dout 10 not instantiated
+    assert C.persistent_engine(32, 20, 0, 1, ce_soft, 2048, 1, 1) == "workgroup"  # forced

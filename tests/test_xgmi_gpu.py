@@ -105,10 +105,72 @@ def test_persistent_engine_world1_equals_per_step(dev):
         torch.testing.assert_close(res[0], res[1], rtol=1e-6, atol=1e-6)
 
 
-def test_persistent_engine_two_ranks_one_gpu(tmp_path):
+@pytest.mark.parametrize("kind", ["mlp", "linear"])
+def test_persistent_engine_two_ranks_one_gpu(tmp_path, kind):
     world = 2
-    spawn(_workers.persistent_two_procs_one_gpu, args=(world, free_port(), str(tmp_path)), nprocs=world)
+    spawn(_workers.persistent_two_procs_one_gpu, args=(world, free_port(), str(tmp_path), kind), nprocs=world)
     res = [torch.load(os.path.join(tmp_path, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    assert res[0]["engine"] == ("workgroup" if kind == "mlp" else "wave")
     assert torch.equal(res[0]["persistent"], res[1]["persistent"])  # replicas in sync
-    torch.testing.assert_close(res[0]["persistent"], res[0]["per_step"], rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(res[0]["persistent"], res[0]["per_step"], rtol=1e-5, atol=1e-5)
     assert res[0]["cursor"].tolist() == [23 // 10, 23 % 10]  # 150 samples/rank / 16 -> 10 steps per epoch
+
+
+@pytest.mark.parametrize("cfg", [
+    # (Din, Dout, loss, momentum, dataset rows, batch): flagship toy, partial last batch + momentum,
+    # MSE, CE with ignore_index rows, B=64 (one lane per row), B=8 (8 lanes per row)
+    (20, 1, "ce_soft", 0.0, 2048, 32),
+    (20, 2, "ce_index", 0.9, 500, 32),
+    (13, 1, "mse", 0.9, 300, 32),
+    (20, 2, "ce_index_ignore", 0.0, 400, 32),
+    (16, 1, "ce_soft", 0.9, 1000, 64),
+    (30, 4, "mse", 0.5, 200, 8),
+])
+def test_wave_engine_matches_workgroup_engine(dev, cfg):
+    """The single-wave register engine (linear_wave.hip) against the LDS workgroup
+    engine and the per-step kernel on the same sampler stream (fp32, summation
+    order differs only)."""
+    from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+
+    from ._workers import _per_step_reference
+
+    Din, Dout, loss, mom, N, B = cfg
+    g = torch.Generator().manual_seed(11)
+    X = torch.randn(N, Din, generator=g).to(dev)
+    kw = {}
+    if loss.startswith("ce_index"):
+        Y = torch.randint(0, Dout, (N,), generator=g)
+        if loss.endswith("ignore"):
+            Y[::5] = -100
+            kw["ignore_index"] = -100
+        Y = Y.to(dev)
+        loss = "ce_index"
+    else:
+        Y = torch.rand(N, Dout, generator=g).to(dev)
+    n_steps = 3 * -(-N // B) + 5  # several epoch transitions, mid-epoch stop
+    res = {}
+    for mode in ("wave", "workgroup", "per_step"):
+        torch.manual_seed(7)
+        eng = FusedMLPStep(torch.nn.Linear(Din, Dout).to(dev), loss=loss, lr=0.05, momentum=mom, **kw)
+        sampler = DeviceDistributedSampler(N, 1, 0, seed=2, device=dev)
+        if mode == "per_step":
+            _per_step_reference(eng, X, Y, sampler, n_steps, B, dev)
+        else:
+            assert eng.persistent_engine(B, sampler, mode) == mode
+            cursor = torch.zeros(2, dtype=torch.int32, device=dev)
+            losses = torch.zeros(n_steps, device=dev)
+            # two launches: the second resumes from the cursor mid-epoch
+            eng.run_persistent(X, Y, n_steps - 7, B, sampler, cursor, losses, variant=mode)
+            eng.run_persistent(X, Y, 7, B, sampler, cursor, losses[n_steps - 7:], variant=mode)
+            torch.cuda.synchronize()
+            S = -(-N // B)
+            assert cursor.tolist() == [n_steps // S, n_steps % S]
+            res[mode + "_loss"] = losses.clone()
+            res[mode + "_G"] = eng.G.clone()
+        torch.cuda.synchronize()
+        res[mode] = eng.P.clone()
+    torch.testing.assert_close(res["wave"], res["workgroup"], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(res["wave"], res["per_step"], rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(res["wave_loss"], res["workgroup_loss"], rtol=1e-4, atol=1e-5, equal_nan=True)
+    torch.testing.assert_close(res["wave_G"], res["workgroup_G"], rtol=1e-4, atol=1e-6)
