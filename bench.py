@@ -204,7 +204,7 @@ def run_persistent(args, rank, world, dev, comm):
         eng.run_persistent(X, Y, args.steps, args.batch_size, sampler, cursor, losses, chunk, stamps=st,
                            variant=variant)
         v = st.tolist()
-        names = (["fetch", "forward", "loss", "backward", "allreduce", "sgd_loss_report"] if which == "wave" else
+        names = (["fetch", "forward", "loss", "backward", "allreduce", "sgd_loss_report"] if which.startswith("wave") else
                  ["prefetch_issue", "forward", "loss", "backward", "allreduce", "sgd_land", "epoch_indices"])
         clk = v[7] / (v[8] * 10e-9) if v[8] else 0.0
         phase = {"cycles_per_step": {n: round(v[k] / args.steps, 1) for k, n in enumerate(names)},
@@ -216,7 +216,7 @@ def run_persistent(args, rank, world, dev, comm):
              "persistent_engine": which,
              "kernels": ("persistent DDP step engine, single-wave variant: batch/weights/momentum/grads in VGPRs, "
                          "DPP row/column reductions, in-kernel xGMI all-reduce + SGD per step, sampler shard "
-                         "rebuilt each epoch by helper waves" if which == "wave" else
+                         "rebuilt each epoch by helper waves" if which.startswith("wave") else
                          "persistent DDP step engine: per step gather+fwd+loss+bwd+all-reduce+SGD in one resident "
                          "workgroup; sampler shard recomputed in-kernel each epoch")}
     if phase:

@@ -187,7 +187,8 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
   hip_check(fused_mlp_persistent(a, pa, cur_stream(X)), "fused_mlp_persistent");
 }
 
-// Which persistent engine fused_mlp_persistent would run for this configuration.
+// Which persistent engine fused_mlp_persistent would run for this configuration
+// ("workgroup", or "wave:L<lanes per row>R<rows per lane group>K<features per lane>").
 std::string persistent_engine(int64_t B, int64_t Din, int64_t H, int64_t Dout, int64_t loss_kind, int64_t num_samples,
                               int64_t world, int64_t variant) {
   FusedMlpArgs a{};
@@ -195,7 +196,11 @@ std::string persistent_engine(int64_t B, int64_t Din, int64_t H, int64_t Dout, i
   a.ar.world = (int)world;
   PersistArgs pa{};
   pa.num_samples = (int)num_samples;
-  if (variant != kPersistWorkgroup && linear_wave_supported(a, pa)) return "wave";
+  if (variant != kPersistWorkgroup && linear_wave_supported(a, pa)) {
+    int L = 0, R = 0, kp = 0;
+    linear_wave_layout(a, pa, &L, &R, &kp);
+    return "wave:L" + std::to_string(L) + "R" + std::to_string(R) + "K" + std::to_string(kp);
+  }
   return "workgroup";
 }
 

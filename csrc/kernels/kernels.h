@@ -79,6 +79,8 @@ struct PersistArgs {
 enum PersistVariant : int { kPersistAuto = 0, kPersistWorkgroup = 1, kPersistWave = 2 };
 hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s);
 bool linear_wave_supported(const FusedMlpArgs& a, const PersistArgs& p);
+// lane layout the wave engine picks: L lanes per row, R rows per lane group, kp features per lane
+void linear_wave_layout(const FusedMlpArgs& a, const PersistArgs& p, int* L, int* R, int* kp);
 hipError_t linear_wave_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s);
 size_t fused_mlp_persistent_lds_bytes(int B, int Din, int H, int Dout, int num_samples, int world);
 // LDS bytes the step needs (host check against the 160 KiB per-CU budget).

@@ -4,9 +4,10 @@
 
 namespace ptdt {
 
-const void* linear_wave_pick_ce_soft(int L, int kp, int dout, bool ar);
-const void* linear_wave_pick_ce_index(int L, int kp, int dout, bool ar);
-const void* linear_wave_pick_mse(int L, int kp, int dout, bool ar);
+#define PTDT_LW_DECL(tag) const void* linear_wave_pick_##tag(int L, int R, int kp, int dout);
+PTDT_LW_DECL(ce_soft) PTDT_LW_DECL(ce_soft_ar) PTDT_LW_DECL(ce_index) PTDT_LW_DECL(ce_index_ar)
+PTDT_LW_DECL(mse) PTDT_LW_DECL(mse_ar)
+#undef PTDT_LW_DECL
 
 namespace {
 
@@ -16,40 +17,85 @@ size_t lds_bytes(const PersistArgs& p) {  // two epoch index lists + 8 phase-tim
   return (size_t)2 * al4(p.num_samples) * sizeof(int) + 8 * sizeof(unsigned long long);
 }
 
-int lanes_per_row(int B) {
-  int rows = 1;
-  while (rows < B) rows <<= 1;
-  return 64 / rows;
-}
-
-int pick_kp_value(int Din, int L) {
-  const int need = (Din + L - 1) / L;
-  for (int kp : {4, 8, 10, 16})
-    if (kp >= need) return kp;
-  return -1;
-}
-
-const void* linear_wave_fn(const FusedMlpArgs& a, const PersistArgs& p) {
-  if (a.H != 0 || a.B <= 0 || a.B > 64 || a.Dout <= 0) return nullptr;
-  if (a.ar.world > kXgmiMaxRanks) return nullptr;
-  if (lds_bytes(p) > 160 * 1024) return nullptr;
-  const int L = lanes_per_row(a.B);
-  if (L > 8) return nullptr;
-  const int kp = pick_kp_value(a.Din, L);
-  if (kp < 0) return nullptr;
-  const bool ar = a.ar.world > 1;
-  switch (a.loss_kind) {
-    case kLossCEIndex: return linear_wave_pick_ce_index(L, kp, a.Dout, ar);
-    case kLossMSE: return linear_wave_pick_mse(L, kp, a.Dout, ar);
-    default: return linear_wave_pick_ce_soft(L, kp, a.Dout, ar);
+const void* pick(int loss, bool ar, int L, int R, int kp, int dout) {
+  switch (loss) {
+    case kLossCEIndex: return ar ? linear_wave_pick_ce_index_ar(L, R, kp, dout) : linear_wave_pick_ce_index(L, R, kp, dout);
+    case kLossMSE: return ar ? linear_wave_pick_mse_ar(L, R, kp, dout) : linear_wave_pick_mse(L, R, kp, dout);
+    default: return ar ? linear_wave_pick_ce_soft_ar(L, R, kp, dout) : linear_wave_pick_ce_soft(L, R, kp, dout);
   }
 }
 
+int log2i(int v) {
+  int r = 0;
+  while ((1 << r) < v) ++r;
+  return r;
+}
+
+// Cycle model of one step on one wave, from tools/microbench_isa.hip issue costs
+// (FMA ~5, DPP add ~5.6, permlane swap + add ~30 cycles, a row's CE ~70): picks
+// the lane layout (L lanes per row, R rows per lane group) for a shape.
+double model_cycles(int L, int R, int kp, int dout) {
+  const bool split = R > 1 && (L == 2 || L == 4) && R <= L;
+  const int loss_rows = split ? 1 : R;
+  const double fwd = R * kp * dout * 5.0 + R * dout * log2i(L) * 5.6;
+  const double loss = loss_rows * (30.0 + 40.0 * dout) + (split ? R * dout * 5.6 : 0.0);
+  const double bwd = R * kp * dout * 5.0 + (kp + 1) * dout * ((L <= 16 ? log2i(16 / L) : 0) * 5.6 + 2 * 30.0);
+  const double sgd = (kp + 1) * dout * 10.0;
+  const double fetch = R * kp * 3.0;
+  return fwd + loss + bwd + sgd + fetch;
+}
+
+struct Choice {
+  const void* fn = nullptr;
+  int L = 0, R = 0, kp = 0;
+};
+
+Choice choose(const FusedMlpArgs& a, const PersistArgs& p) {
+  Choice best;
+  if (a.H != 0 || a.B <= 0 || a.B > 64 || a.Dout <= 0) return best;
+  if (a.ar.world > kXgmiMaxRanks) return best;
+  if (lds_bytes(p) > 160 * 1024) return best;
+  const bool ar = a.ar.world > 1;
+  static const int kLR[][2] = {{1, 1}, {2, 1}, {4, 1}, {8, 1}, {2, 2}, {4, 2}};
+  double best_cost = 1e30;
+  for (const auto& lr : kLR) {
+    const int L = lr[0], R = lr[1];
+    if ((64 / L) * R < a.B) continue;                // rows must fit one pass
+    if (ar && 64 / L < a.ar.world) continue;         // one row group per rank
+    const int need = (a.Din + L - 1) / L;
+    int kp = -1;
+    for (int c : {4, 5, 8, 10, 16})
+      if (c >= need) {
+        kp = c;
+        break;
+      }
+    if (kp < 0) continue;
+    const void* fn = pick(a.loss_kind, ar, L, R, kp, a.Dout);
+    if (fn == nullptr) continue;
+    const double cost = model_cycles(L, R, kp, a.Dout);
+    if (cost < best_cost) {
+      best_cost = cost;
+      best.fn = fn;
+      best.L = L;
+      best.R = R;
+      best.kp = kp;
+    }
+  }
+  return best;
+}
+
 }  // namespace
-bool linear_wave_supported(const FusedMlpArgs& a, const PersistArgs& p) { return linear_wave_fn(a, p) != nullptr; }
+bool linear_wave_supported(const FusedMlpArgs& a, const PersistArgs& p) { return choose(a, p).fn != nullptr; }
+
+void linear_wave_layout(const FusedMlpArgs& a, const PersistArgs& p, int* L, int* R, int* kp) {
+  const Choice c = choose(a, p);
+  *L = c.L;
+  *R = c.R;
+  *kp = c.kp;
+}
 
 hipError_t linear_wave_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s) {
-  const void* fn = linear_wave_fn(a, p);
+  const void* fn = choose(a, p).fn;
   if (fn == nullptr) return hipErrorInvalidValue;
   const size_t lds = lds_bytes(p);
   if (lds > 64 * 1024)

@@ -1,7 +1,10 @@
-// Single-wave engine instantiations for one loss (split per loss so the
-// instantiation table compiles in parallel). See linear_wave_impl.h.
+// Single-wave engine instantiations: ce_index, without the in-kernel all-reduce.
+// One translation unit per (loss, all-reduce) so the table compiles in parallel.
+// See linear_wave_impl.h.
 #include "linear_wave_impl.h"
 
 namespace ptdt {
-const void* linear_wave_pick_ce_index(int L, int kp, int dout, bool ar) { return lw::pick<kLossCEIndex>(L, kp, dout, ar); }
+const void* linear_wave_pick_ce_index(int L, int R, int kp, int dout) {
+  return lw::pick<kLossCEIndex, false>(L, R, kp, dout);
+}
 }  // namespace ptdt

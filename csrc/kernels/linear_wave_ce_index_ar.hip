@@ -1,0 +1,10 @@
+// Single-wave engine instantiations: ce_index, with the in-kernel all-reduce.
+// One translation unit per (loss, all-reduce) so the table compiles in parallel.
+// See linear_wave_impl.h.
+#include "linear_wave_impl.h"
+
+namespace ptdt {
+const void* linear_wave_pick_ce_index_ar(int L, int R, int kp, int dout) {
+  return lw::pick<kLossCEIndex, true>(L, R, kp, dout);
+}
+}  // namespace ptdt

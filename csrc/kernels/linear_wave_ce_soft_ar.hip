@@ -1,0 +1,10 @@
+// Single-wave engine instantiations: ce_soft, with the in-kernel all-reduce.
+// One translation unit per (loss, all-reduce) so the table compiles in parallel.
+// See linear_wave_impl.h.
+#include "linear_wave_impl.h"
+
+namespace ptdt {
+const void* linear_wave_pick_ce_soft_ar(int L, int R, int kp, int dout) {
+  return lw::pick<kLossCESoft, true>(L, R, kp, dout);
+}
+}  // namespace ptdt

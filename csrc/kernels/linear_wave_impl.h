@@ -6,14 +6,19 @@
 // (fused_mlp.hip) keeps everything in LDS but still pays a chain of
 // LDS round trips and s_barriers per phase. This engine removes both:
 //
-//   * ONE wave trains. Lane (r, p) owns batch row r (r < 64 / L) and feature
-//     chunk p (KP consecutive features, L = lanes per row), so the batch, the
-//     weights, the momentum and the gradients all live in VGPRs.
-//   * forward  : KP FMAs + a DPP row-group sum over the L lanes of a row;
-//   * loss     : computed redundantly by the L lanes of a row (no exchange);
-//   * backward : g * x per lane, then a rotation/permlane column sum over the
-//     rows -- every lane ends with the full-batch gradient of ITS chunk, with
-//     the same bits in every lane (each butterfly stage adds a+b / b+a);
+//   * ONE wave trains. Lane (j, p) owns row group j (j < 64 / L) and feature
+//     chunk p (KP consecutive features, L = lanes per row); the group holds R
+//     batch rows (row j + rho * 64/L), so the batch, the weights, the momentum
+//     and the gradients all live in VGPRs.
+//   * forward  : R*KP FMAs + a DPP row-group sum over the L lanes of a row;
+//   * loss     : with R > 1 each of the first R lanes of a group computes one
+//     row's loss and DPP broadcasts dL/dz to the group; with R == 1 the L
+//     lanes of a row compute it redundantly (no exchange);
+//   * backward : sum over the lane's R rows of g * x, then a rotation/permlane
+//     column sum over the row groups -- every lane ends with the full-batch
+//     gradient of ITS chunk, with the same bits in every lane (each butterfly
+//     stage adds a+b / b+a). Cross-DPP-row permlane swaps cost ~4x a DPP add
+//     (tools/microbench_isa.hip), so R > 1 trades them for local FMAs;
 //   * all-reduce (world > 1): lanes of row q push the chunk to peer q and poll
 //     peer q's contribution (xGMI one-shot, LL words, csrc/comm/xgmi.h), then
 //     the same column sum adds the ranks -- identical on every rank;
@@ -24,9 +29,11 @@
 //   Waves 1-3 build the next epoch's sampler index list (Feistel permutation,
 //   sampler.h) in LDS while wave 0 trains; the two meet at one s_barrier per
 //   epoch.
-// Configurations: KP (features per lane, zero padded), DOUT and the loss are
-// template parameters; anything else runs the workgroup engine.
+// Configurations: L, R, KP (features per lane, zero padded), DOUT, the loss and
+// whether an all-reduce exists are template parameters; anything else runs the
+// workgroup engine.
 #pragma once
+#include <type_traits>
 #include "common.h"
 #include "kernels.h"
 #include "sampler.h"
@@ -100,17 +107,27 @@ struct Ticks {
   }
 };
 
-template <int KP, int DOUT>
+template <int R, int KP, int DOUT, int RY>
 struct Batch {
-  float x[KP];
-  float y[DOUT];
-  int yi;
+  float x[R][KP];
+  float y[RY][DOUT];
+  int yi[RY];
   int nb;  // rows in this batch (last batch of an epoch may be short)
 };
 
-template <int L, int KP, int DOUT, int LOSS, bool AR>
+// quad_perm broadcast of lane `src` of each aligned group of L (2 or 4) lanes
+template <int L, int SRC>
+constexpr int bcast_ctrl() {
+  return L == 4 ? SRC * 0x55 : (SRC | (SRC << 2) | ((2 + SRC) << 4) | ((2 + SRC) << 6));
+}
+
+template <int L, int R, int KP, int DOUT, int LOSS, bool AR>
 __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, PersistArgs pa) {
-  extern __shared__ int elist[];  // [2][estride] sampler index lists (epoch parity)
+  // R > 1: the first R lanes of each group each compute one row's loss
+  constexpr bool SPLIT = R > 1 && (L == 2 || L == 4) && R <= L;
+  constexpr int RY = SPLIT ? 1 : R;  // target rows each lane loads
+  constexpr int RG = 64 / L;         // row groups
+  extern __shared__ int elist[];     // [2][estride] sampler index lists (epoch parity)
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int B = a.B, Din = a.Din;
   const int estride = al4(pa.num_samples);
@@ -141,8 +158,9 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
 
   // ------------------------------------------------------------------ trainer wave
   const int lane = (int)threadIdx.x;
-  const int r = lane / L, p = lane % L;    // batch row, feature chunk (L lanes per row, 64 / L >= B)
+  const int j = lane / L, p = lane % L;    // row group, feature chunk
   const int k0 = p * KP;
+  const int rho_y = SPLIT ? min(p, R - 1) : 0;  // the row whose loss this lane computes (SPLIT)
   const bool hb = a.has_bias != 0;
   const bool use_mom = a.mom != nullptr && a.momentum != 0.f;
   const float lr = a.lr, mu = a.momentum, damp = a.dampening, wd = a.weight_decay;
@@ -168,13 +186,13 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
   int opt_step = a.opt_step ? *a.opt_step : 0;
   const XgmiArgs& ar = a.ar;
   const int world = AR ? ar.world : 1;  // AR == false: single rank, no all-reduce code at all
-  // this lane's push target (row q pushes to rank q) and poll source, selected
-  // once with uniform compares: indexing peers[] by a lane value would spill
-  // the argument array to scratch
+  // this lane's push target (row group q pushes to rank q) and poll source,
+  // selected once with uniform compares: indexing peers[] by a lane value would
+  // spill the argument array to scratch
   uint64_t PTDT_GLOBAL* push_dst = nullptr;
 #pragma unroll
   for (int q = 0; q < kXgmiMaxRanks; ++q)
-    if (r == q && q < world) push_dst = (uint64_t PTDT_GLOBAL*)ar.peers[q];
+    if (j == q && q < world) push_dst = (uint64_t PTDT_GLOBAL*)ar.peers[q];
   uint64_t PTDT_GLOBAL* const poll_src = (uint64_t PTDT_GLOBAL*)ar.local;
   const int my_rank = ar.rank, max_elems = ar.max_elems;
   float PTDT_GLOBAL* const losses = gptr_w(pa.losses);
@@ -187,41 +205,53 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
   float kmask[KP];
 #pragma unroll
   for (int k = 0; k < KP; ++k) kmask[k] = k0 + k < Din ? 1.f : 0.f;
-  // index lookahead: the dataset row of position `ipos` is read from LDS one
-  // fetch before the gather that uses it
+  // index lookahead: the dataset rows of the next batch are read from LDS one
+  // fetch before the gather that uses them
   int ie = e0, ij = j0, barriers = 0;
-  int sel_next = 0, nb_next = 0;
+  int sel_next[R], nb_next = 0;
   auto read_index = [&]() {
     if (ij == 0 && ie != e0) {  // entering a new epoch: its list must be ready, the old one is free
       __syncthreads();
       ++barriers;
     }
     nb_next = min(B, pa.num_samples - ij * B);
-    sel_next = list(ie)[ij * B + min(r, nb_next - 1)];  // rows past the batch re-read its last row
+#pragma unroll
+    for (int rho = 0; rho < R; ++rho)  // rows past the batch re-read its last row
+      sel_next[rho] = list(ie)[ij * B + min(rho * RG + j, nb_next - 1)];
     if (++ij == S) {
       ij = 0;
       ++ie;
     }
   };
   int fetched = 0;
-  auto fetch = [&](Batch<KP, DOUT>& f) {
+  auto fetch = [&](Batch<R, KP, DOUT, RY>& f) {
     // Unconditional loads from clamped addresses (no exec-mask branches): rows
     // past the batch get g = 0 in train(), padded features are masked there.
-    const int sel = sel_next;
     f.nb = nb_next;
-    const auto xr = X + (int64_t)sel * Din + k0;
-    if (!padded) {  // immediate offsets from one address
 #pragma unroll
-      for (int k = 0; k < KP; ++k) f.x[k] = xr[k];
-    } else {
+    for (int rho = 0; rho < R; ++rho) {
+      const auto xr = X + (int64_t)sel_next[rho] * Din + k0;
+      if (!padded) {  // immediate offsets from one address
 #pragma unroll
-      for (int k = 0; k < KP; ++k) f.x[k] = xr[min(k, Din - 1 - k0)];
+        for (int k = 0; k < KP; ++k) f.x[rho][k] = xr[k];
+      } else {
+#pragma unroll
+        for (int k = 0; k < KP; ++k) f.x[rho][k] = xr[min(k, Din - 1 - k0)];
+      }
     }
-    if constexpr (LOSS == kLossCEIndex) {
-      f.yi = (int)gptr(a.Yi)[sel];
-    } else {
 #pragma unroll
-      for (int c = 0; c < DOUT; ++c) f.y[c] = gptr(a.Yf)[(int64_t)sel * DOUT + c];
+    for (int ry = 0; ry < RY; ++ry) {
+      int sel = sel_next[ry];
+      if constexpr (SPLIT) {
+#pragma unroll
+        for (int rho = 1; rho < R; ++rho) sel = rho_y == rho ? sel_next[rho] : sel;
+      }
+      if constexpr (LOSS == kLossCEIndex) {
+        f.yi[ry] = (int)gptr(a.Yi)[sel];
+      } else {
+#pragma unroll
+        for (int c = 0; c < DOUT; ++c) f.y[ry][c] = gptr(a.Yf)[(int64_t)sel * DOUT + c];
+      }
     }
     ++fetched;
     if (fetched < n) read_index();
@@ -233,37 +263,17 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
   if (tk.on && lane == 0)
     for (int k = 0; k < 8; ++k) tk.acc[k] = 0ull;
   const float inv_full = 1.f / (float)((LOSS == kLossMSE) ? B * DOUT : B);
-  const float coef_full = a.grad_scale * inv_full;
   const int64_t t_begin = tk.on ? (int64_t)__builtin_amdgcn_s_memtime() : 0;
   const int64_t r_begin = tk.on ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
 
-
-  auto train = [&](Batch<KP, DOUT>& f, int step) {
-    const int nb = f.nb;
-    const bool valid = r < nb;
-    if (padded) {
-#pragma unroll
-      for (int k = 0; k < KP; ++k) f.x[k] *= kmask[k];
-    }
-    // ---- forward
-    float z[DOUT];
-#pragma unroll
-    for (int c = 0; c < DOUT; ++c) {
-      float acc0 = 0.f, acc1 = 0.f;
-#pragma unroll
-      for (int k = 0; k < KP; k += 2) {
-        acc0 = fmaf(f.x[k], W[c][k], acc0);
-        if (k + 1 < KP) acc1 = fmaf(f.x[k + 1], W[c][k + 1], acc1);
-      }
-      z[c] = row_sum<L>(acc0 + acc1) + Wb[c];
-    }
-    tk.tick(1);
-    // ---- loss and dL/dz (the L lanes of a row compute the same values)
-    float g[DOUT], l = 0.f, cnt = 0.f;
+  // loss and dL/dz of one row: l (summed loss), cnt (CE index: 1 if counted)
+  auto row_loss = [&](const float* z, const float* y, int yi, bool valid, float* g, float& l, float& cnt) {
+    l = 0.f;
+    cnt = 0.f;
     if constexpr (LOSS == kLossMSE) {
 #pragma unroll
       for (int c = 0; c < DOUT; ++c) {
-        const float df = z[c] - f.y[c];
+        const float df = z[c] - y[c];
         l = fmaf(df, df, l);
         g[c] = 2.f * df;
       }
@@ -279,18 +289,18 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
         float tsum = 0.f;
 #pragma unroll
         for (int c = 0; c < DOUT; ++c) {
-          tsum += f.y[c];
-          l -= f.y[c] * (z[c] - lse);
+          tsum += y[c];
+          l -= y[c] * (z[c] - lse);
         }
 #pragma unroll
-        for (int c = 0; c < DOUT; ++c) g[c] = __expf(z[c] - lse) * tsum - f.y[c];
+        for (int c = 0; c < DOUT; ++c) g[c] = __expf(z[c] - lse) * tsum - y[c];
       } else {
-        const bool use = f.yi != a.ignore_index;
+        const bool use = yi != a.ignore_index;
         float zy = 0.f;
 #pragma unroll
         for (int c = 0; c < DOUT; ++c) {
-          zy = c == f.yi ? z[c] : zy;
-          g[c] = use ? __expf(z[c] - lse) - (c == f.yi ? 1.f : 0.f) : 0.f;
+          zy = c == yi ? z[c] : zy;
+          g[c] = use ? __expf(z[c] - lse) - (c == yi ? 1.f : 0.f) : 0.f;
         }
         l = use ? lse - zy : 0.f;
         cnt = use ? 1.f : 0.f;
@@ -302,10 +312,71 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
       l = 0.f;
       cnt = 0.f;
     }
+  };
+
+  auto train = [&](Batch<R, KP, DOUT, RY>& f, int step) {
+    const int nb = f.nb;
+    if (padded) {
+#pragma unroll
+      for (int rho = 0; rho < R; ++rho)
+#pragma unroll
+        for (int k = 0; k < KP; ++k) f.x[rho][k] *= kmask[k];
+    }
+    // ---- forward
+    float z[R][DOUT];
+#pragma unroll
+    for (int rho = 0; rho < R; ++rho) {
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) {
+        float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < KP; k += 2) {
+          acc0 = fmaf(f.x[rho][k], W[c][k], acc0);
+          if (k + 1 < KP) acc1 = fmaf(f.x[rho][k + 1], W[c][k + 1], acc1);
+        }
+        z[rho][c] = row_sum<L>(acc0 + acc1) + Wb[c];
+      }
+    }
+    tk.tick(1);
+    // ---- loss and dL/dz
+    float g[R][DOUT], lsum = 0.f, csum = 0.f;
+    if constexpr (SPLIT) {
+      float zs[DOUT];
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) {
+        zs[c] = z[0][c];
+#pragma unroll
+        for (int rho = 1; rho < R; ++rho) zs[c] = rho_y == rho ? z[rho][c] : zs[c];
+      }
+      float gs[DOUT], l, cnt;
+      row_loss(zs, f.y[0], f.yi[0], rho_y * RG + j < nb, gs, l, cnt);
+      const bool owner = p < R;  // lanes p >= R duplicated row R-1: not counted
+      lsum = owner ? l : 0.f;
+      csum = owner ? cnt : 0.f;
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) {
+        g[0][c] = dpp_f<bcast_ctrl<L, 0>()>(gs[c]);
+        if constexpr (R > 1) g[1][c] = dpp_f<bcast_ctrl<L, 1>()>(gs[c]);
+        if constexpr (R > 2) g[2][c] = dpp_f<bcast_ctrl<L, 2>()>(gs[c]);
+        if constexpr (R > 3) g[3][c] = dpp_f<bcast_ctrl<L, 3>()>(gs[c]);
+      }
+    } else {
+#pragma unroll
+      for (int rho = 0; rho < R; ++rho) {
+        float l, cnt;
+        row_loss(z[rho], f.y[rho], f.yi[rho], rho * RG + j < nb, g[rho], l, cnt);
+        lsum += l;
+        csum += cnt;
+      }
+      if (p != 0) {  // the L lanes of a row computed the same loss: count it once
+        lsum = 0.f;
+        csum = 0.f;
+      }
+    }
     float inv_denom;
     if constexpr (LOSS == kLossCEIndex) {
-      cnt = wave_sum(p == 0 ? cnt : 0.f);  // the one data-dependent denominator
-      inv_denom = 1.f / (cnt > 0.f ? cnt : 1.f);
+      csum = wave_sum(csum);  // the one data-dependent denominator
+      inv_denom = 1.f / (csum > 0.f ? csum : 1.f);
     } else {  // division only for a short last batch
       inv_denom = nb == B ? inv_full : 1.f / (float)((LOSS == kLossMSE) ? nb * DOUT : nb);
     }
@@ -316,18 +387,26 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
 #pragma unroll
     for (int c = 0; c < DOUT; ++c) {
 #pragma unroll
-      for (int k = 0; k < KP; ++k) gW[c][k] = col_sum<L>(g[c] * f.x[k]) * coef;
-      gb[c] = col_sum<L>(g[c]) * coef;
+      for (int k = 0; k < KP; ++k) {
+        float t = g[0][c] * f.x[0][k];
+#pragma unroll
+        for (int rho = 1; rho < R; ++rho) t = fmaf(g[rho][c], f.x[rho][k], t);
+        gW[c][k] = col_sum<L>(t) * coef;
+      }
+      float tb = g[0][c];
+#pragma unroll
+      for (int rho = 1; rho < R; ++rho) tb += g[rho][c];
+      gb[c] = col_sum<L>(tb) * coef;
     }
     tk.tick(3);
-    // ---- all-reduce over ranks (average): row q <-> rank q
+    // ---- all-reduce over ranks (average): row group q <-> rank q
     if (AR && !failed) {
       seq += 1u;
       const int parity = (int)(seq & 1u);
       auto slot = [&](uint64_t PTDT_GLOBAL* base, int src, int i) {
         return base + ((int64_t)(parity * world + src) * max_elems + i);
       };
-      if (r < world && r != my_rank) {
+      if (j < world && j != my_rank) {
         uint64_t PTDT_GLOBAL* dst = push_dst;
 #pragma unroll
         for (int c = 0; c < DOUT; ++c) {
@@ -345,11 +424,11 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
       float v[DOUT][KP], vb[DOUT];
 #pragma unroll
       for (int c = 0; c < DOUT; ++c) {
-        vb[c] = r == my_rank ? gb[c] : 0.f;
+        vb[c] = j == my_rank ? gb[c] : 0.f;
 #pragma unroll
-        for (int k = 0; k < KP; ++k) v[c][k] = r == my_rank ? gW[c][k] : 0.f;
+        for (int k = 0; k < KP; ++k) v[c][k] = j == my_rank ? gW[c][k] : 0.f;
       }
-      if (r < world && r != my_rank) {
+      if (j < world && j != my_rank) {
         // all slots of the chunk in flight together; re-poll until every seq matches
         uint32_t polls = 0;
         while (true) {
@@ -359,7 +438,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
 #pragma unroll
             for (int k = 0; k < KP; ++k) {
               if (k0 + k < Din) {
-                const uint64_t w = __hip_atomic_load(slot(poll_src, r, c * Din + k0 + k), __ATOMIC_RELAXED,
+                const uint64_t w = __hip_atomic_load(slot(poll_src, j, c * Din + k0 + k), __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_SYSTEM);
                 all &= (uint32_t)(w >> 32) == seq;
                 v[c][k] = __uint_as_float((uint32_t)w);
@@ -367,7 +446,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
             }
             if (hb) {
               const uint64_t w =
-                  __hip_atomic_load(slot(poll_src, r, nW + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                  __hip_atomic_load(slot(poll_src, j, nW + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
               all &= (uint32_t)(w >> 32) == seq;
               vb[c] = __uint_as_float((uint32_t)w);
             }
@@ -390,32 +469,32 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
       }
     }
     tk.tick(4);
-    // ---- SGD (torch.optim.SGD semantics) on this lane's chunk
+    // ---- SGD (torch.optim.SGD semantics) on this lane's chunk; unswitched on
+    // momentum so the unrolled body has no per-element branches
     const bool first = opt_step == 0;
-#pragma unroll
-    for (int c = 0; c < DOUT; ++c) {
-#pragma unroll
-      for (int k = 0; k < KP; ++k) {
-        float d = fmaf(wd, W[c][k], gW[c][k]);
-        if (use_mom) {
-          const float buf = first ? d : fmaf(mu, M[c][k], (1.f - damp) * d);
-          M[c][k] = buf;
+    auto sgd_all = [&](auto mom_tag) {
+      constexpr bool MOM = decltype(mom_tag)::value;
+      auto upd = [&](float& w, float& m, float gr) {
+        float d = fmaf(wd, w, gr);
+        if constexpr (MOM) {
+          const float buf = first ? d : fmaf(mu, m, (1.f - damp) * d);
+          m = buf;
           d = nesterov ? fmaf(mu, buf, d) : buf;
         }
-        W[c][k] = fmaf(-lr, d, W[c][k]);
+        w = fmaf(-lr, d, w);
+      };
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+        for (int k = 0; k < KP; ++k) upd(W[c][k], M[c][k], gW[c][k]);
+        upd(Wb[c], Mb[c], gb[c]);
+        Wb[c] = hb ? Wb[c] : 0.f;  // no bias: stays 0 (select, not a branch)
       }
-      if (hb) {
-        float d = fmaf(wd, Wb[c], gb[c]);
-        if (use_mom) {
-          const float buf = first ? d : fmaf(mu, Mb[c], (1.f - damp) * d);
-          Mb[c] = buf;
-          d = nesterov ? fmaf(mu, buf, d) : buf;
-        }
-        Wb[c] = fmaf(-lr, d, Wb[c]);
-      }
-    }
+    };
+    if (use_mom) sgd_all(std::true_type{});
+    else sgd_all(std::false_type{});
     ++opt_step;
-    if (step == n - 1 && r == 0) {  // the DDP bucket keeps the last step's averaged gradients
+    if (step == n - 1 && j == 0) {  // the DDP bucket keeps the last step's averaged gradients
       const auto Gw = gptr_w(a.G);
 #pragma unroll
       for (int c = 0; c < DOUT; ++c) {
@@ -425,15 +504,15 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
         if (hb && p == 0) Gw[nW + c] = gb[c];
       }
     }
-    // ---- loss report (off the critical path: nothing waits on it)
-    const float ls = wave_sum(p == 0 ? l : 0.f);
-    // every lane stores the same value to the same address: no exec-mask branch
-    if constexpr (LOSS == kLossCEIndex) losses[step] = cnt > 0.f ? ls * inv_denom : NAN;
+    // ---- loss report (off the critical path: nothing waits on it); every lane
+    // stores the same value to the same address: no exec-mask branch
+    const float ls = wave_sum(lsum);
+    if constexpr (LOSS == kLossCEIndex) losses[step] = csum > 0.f ? ls * inv_denom : NAN;
     else losses[step] = ls * inv_denom;
     tk.tick(5);
   };
 
-  Batch<KP, DOUT> buf[kNB];
+  Batch<R, KP, DOUT, RY> buf[kNB];
   tk.start();
   read_index();
 #pragma unroll
@@ -459,8 +538,8 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
     ++barriers;
   }
 
-  // ---- write back resident state (lanes of row 0 hold every chunk)
-  if (r == 0) {
+  // ---- write back resident state (lanes of row group 0 hold every chunk)
+  if (j == 0) {
     const auto Pw = gptr_w(a.P);
 #pragma unroll
     for (int c = 0; c < DOUT; ++c) {
@@ -493,19 +572,19 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
   }
 }
 
-// Instantiation table of one loss: (L, KP, DOUT) combinations whose register
-// footprint fits (no scratch). Returns nullptr for anything else.
-template <int LOSS>
-const void* pick(int L, int kp, int dout, bool ar) {
-#define PTDT_LW(LL, KP, DO) \
-  if (L == LL && kp == KP && dout == DO)  \
-    return ar ? (const void*)linear_wave_kernel<LL, KP, DO, LOSS, true> \
-              : (const void*)linear_wave_kernel<LL, KP, DO, LOSS, false>;
-#define PTDT_LW_L(LL) \
-  PTDT_LW(LL, 4, 1) PTDT_LW(LL, 8, 1) PTDT_LW(LL, 10, 1) PTDT_LW(LL, 16, 1) \
-  PTDT_LW(LL, 4, 2) PTDT_LW(LL, 8, 2) PTDT_LW(LL, 10, 2) PTDT_LW(LL, 4, 4)
-  PTDT_LW_L(1) PTDT_LW_L(2) PTDT_LW_L(4) PTDT_LW_L(8)
-#undef PTDT_LW_L
+// Instantiation table of one loss and all-reduce flag: (L, R, KP, DOUT)
+// combinations whose register footprint fits (no scratch). nullptr otherwise.
+// Keep in sync with kWaveConfigs in linear_wave.hip.
+template <int LOSS, bool AR>
+const void* pick(int L, int R, int kp, int dout) {
+#define PTDT_LW(LL, RR, KP, DO) \
+  if (L == LL && R == RR && kp == KP && dout == DO) return (const void*)linear_wave_kernel<LL, RR, KP, DO, LOSS, AR>;
+#define PTDT_LW_LR(LL, RR)                                                                    \
+  PTDT_LW(LL, RR, 4, 1) PTDT_LW(LL, RR, 5, 1) PTDT_LW(LL, RR, 8, 1) PTDT_LW(LL, RR, 10, 1)    \
+  PTDT_LW(LL, RR, 16, 1) PTDT_LW(LL, RR, 4, 2) PTDT_LW(LL, RR, 5, 2) PTDT_LW(LL, RR, 8, 2)    \
+  PTDT_LW(LL, RR, 10, 2) PTDT_LW(LL, RR, 4, 4)
+  PTDT_LW_LR(1, 1) PTDT_LW_LR(2, 1) PTDT_LW_LR(4, 1) PTDT_LW_LR(8, 1) PTDT_LW_LR(2, 2) PTDT_LW_LR(4, 2)
+#undef PTDT_LW_LR
 #undef PTDT_LW
   return nullptr;
 }

@@ -173,7 +173,8 @@ class FusedMLPStep:
         self._pending = False
 
     def persistent_engine(self, batch_size: int, sampler, variant: str | None = None) -> str:
-        """Which persistent engine :meth:`run_persistent` runs: "wave" or "workgroup"."""
+        """Which persistent engine :meth:`run_persistent` runs: "workgroup" or
+        "wave:L<l>R<r>K<k>" (lanes per row, rows per lane group, features per lane)."""
         return self._C.persistent_engine(batch_size, self.Din, self.H, self.Dout, self.loss_kind,
                                          sampler.num_samples, sampler.num_replicas, _variant_id(variant))
 
