@@ -118,12 +118,13 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
                              double lr, double momentum, double dampening, double weight_decay, bool nesterov,
                              std::shared_ptr<XgmiComm> ar, int64_t n_steps, int64_t W, int64_t rank,
                              int64_t num_samples, bool shuffle, int64_t seed, Tensor cursor, Tensor losses,
-                             c10::optional<Tensor> stamps, int64_t variant) {
-  check_gpu(X, "X");
+                             c10::optional<Tensor> stamps, int64_t variant, bool x_zero_padded) {
+  TORCH_CHECK(X.is_cuda(), "X must be a GPU tensor");  // rows may be padded: checked below
   check_gpu(P, "P");
   check_gpu(G, "G");
   TORCH_CHECK(X.scalar_type() == at::kFloat && P.scalar_type() == at::kFloat && G.scalar_type() == at::kFloat);
-  TORCH_CHECK(X.dim() == 2 && X.size(1) == Din, "persistent: X must be [N, Din]");
+  TORCH_CHECK(X.dim() == 2 && X.size(1) == Din && X.stride(1) == 1 && X.stride(0) >= Din,
+              "persistent: X must be [N, Din] with unit column stride (rows may be padded)");
   const int64_t N = X.size(0);
   const int64_t Dh = H > 0 ? H : Din;
   const int64_t np = (H > 0 ? H * Din + (has_bias ? H : 0) : 0) + Dout * Dh + (has_bias ? Dout : 0);
@@ -149,6 +150,8 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
   a.mom = ptr_or_null<float>(mom);
   a.opt_step = ptr_or_null<int32_t>(opt_step);
   a.B = (int)B; a.Din = (int)Din; a.H = (int)H; a.Dout = (int)Dout;
+  a.ldx = (int)X.stride(0);
+  a.x_padded = x_zero_padded ? 1 : 0;
   a.loss_kind = (int)loss_kind;
   a.ignore_index = (int)ignore_index;
   a.has_bias = has_bias ? 1 : 0;
@@ -194,6 +197,8 @@ std::string persistent_engine(int64_t B, int64_t Din, int64_t H, int64_t Dout, i
   FusedMlpArgs a{};
   a.B = (int)B; a.Din = (int)Din; a.H = (int)H; a.Dout = (int)Dout; a.loss_kind = (int)loss_kind;
   a.ar.world = (int)world;
+  a.ldx = 1 << 20;  // the caller zero-pads X rows to the layout's width when needed
+  a.x_padded = 1;
   PersistArgs pa{};
   pa.num_samples = (int)num_samples;
   if (variant != kPersistWorkgroup && linear_wave_supported(a, pa)) {
@@ -568,7 +573,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"), py::arg("nesterov"), py::arg("ar"),
         py::arg("n_steps"), py::arg("W"), py::arg("rank"), py::arg("num_samples"), py::arg("shuffle"),
         py::arg("seed"), py::arg("cursor"), py::arg("losses"), py::arg("stamps") = py::none(),
-        py::arg("variant") = 0);
+        py::arg("variant") = 0, py::arg("x_zero_padded") = false);
   m.def("persistent_engine", &persistent_engine, py::arg("B"), py::arg("Din"), py::arg("H"), py::arg("Dout"),
         py::arg("loss_kind"), py::arg("num_samples"), py::arg("world"), py::arg("variant") = 0);
   m.def("fused_mlp_lds_bytes", [](int B, int Din, int H, int Dout) { return fused_mlp_lds_bytes(B, Din, H, Dout); });

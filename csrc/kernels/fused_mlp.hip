@@ -88,9 +88,10 @@ template <int LOSS>
 __device__ __forceinline__ void gather_batch(const FusedMlpArgs& a, const Dims& d, const int* sel, const Scratch& s,
                                              int tid, int NT) {
   const auto X = gptr(a.X);
+  const int ldx = a.ldx > 0 ? a.ldx : d.Din;
   for (int e = tid; e < d.B * d.Din; e += NT) {
     const int b = e / d.Din, k = e - b * d.Din;
-    s.xs[e] = X[(int64_t)sel[b] * d.Din + k];
+    s.xs[e] = X[(int64_t)sel[b] * ldx + k];
   }
   if constexpr (LOSS != kLossCEIndex) {
     const auto Yf = gptr(a.Yf);
@@ -449,12 +450,13 @@ struct Prefetch {
   __device__ __forceinline__ void issue(const FusedMlpArgs& a, const int* sel, int B, int Din, int Dout, int tid,
                                         int NT) {
     const auto X = gptr(a.X);
+    const int ldx = a.ldx > 0 ? a.ldx : Din;
 #pragma unroll
     for (int q = 0; q < kPf; ++q) {
       const int e = tid + q * NT;
       if (e < B * Din) {
         const int b = e / Din;
-        x[q] = X[(int64_t)sel[b] * Din + (e - b * Din)];
+        x[q] = X[(int64_t)sel[b] * ldx + (e - b * Din)];
       }
       if constexpr (LOSS != kLossCEIndex) {
         if (e < B * Dout) {

@@ -38,6 +38,8 @@ struct FusedMlpArgs {
   int32_t* opt_step;     // device step counter for momentum init (may be nullptr)
   float* loss_out;       // [1] mean loss of this step
   int B, Din, H, Dout;
+  int ldx;               // row stride of X in elements (0: Din)
+  int x_padded;          // columns [Din, ldx) of X are zero (lets the wave engine read whole lane chunks)
   int loss_kind;
   int ignore_index;      // CE index: rows with this label are skipped (torch default -100)
   int has_bias;

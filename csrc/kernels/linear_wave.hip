@@ -63,9 +63,10 @@ Choice choose(const FusedMlpArgs& a, const PersistArgs& p) {
     if ((64 / L) * R < a.B) continue;                // rows must fit one pass
     if (ar && 64 / L < a.ar.world) continue;         // one row group per rank
     const int need = (a.Din + L - 1) / L;
+    const int ldx = a.ldx > 0 ? a.ldx : a.Din;
     int kp = -1;
     for (int c : {4, 5, 8, 10, 16})
-      if (c >= need) {
+      if (c >= need && (L * c == a.Din || (a.x_padded && L * c <= ldx))) {  // lane chunks read zero padding
         kp = c;
         break;
       }

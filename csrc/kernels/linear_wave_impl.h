@@ -200,44 +200,42 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
   bool failed = AR && *ar.err != 0;  // a peer already timed out earlier: do not wait again
   const float inv_w = 1.f / (float)world;
 
-  // padded feature slots (L * KP > Din): x masked to 0 so W stays 0 there
-  const bool padded = L * KP != Din;
-  float kmask[KP];
-#pragma unroll
-  for (int k = 0; k < KP; ++k) kmask[k] = k0 + k < Din ? 1.f : 0.f;
+  // Feature slots past Din (L * KP > Din) read the zero padding of X (the host
+  // guarantees ldx >= L * KP and zeros there): their gradient is 0, W stays 0.
+  const int ldx = a.ldx > 0 ? a.ldx : Din;
   // index lookahead: the dataset rows of the next batch are read from LDS one
   // fetch before the gather that uses them
   int ie = e0, ij = j0, barriers = 0;
   int sel_next[R], nb_next = 0;
+  // Always called (also for the kNB positions past this launch, whose lists may
+  // be stale): no conditional loads in the loop, so the waitcnt pass can count
+  // the outstanding prefetches exactly instead of falling back to vmcnt(0).
+  const uint32_t N = (uint32_t)pa.N;
   auto read_index = [&]() {
-    if (ij == 0 && ie != e0) {  // entering a new epoch: its list must be ready, the old one is free
+    if (ij == 0 && ie != e0 && barriers < T) {  // new epoch: its list is ready, the old one free
       __syncthreads();
       ++barriers;
     }
     nb_next = min(B, pa.num_samples - ij * B);
 #pragma unroll
-    for (int rho = 0; rho < R; ++rho)  // rows past the batch re-read its last row
-      sel_next[rho] = list(ie)[ij * B + min(rho * RG + j, nb_next - 1)];
+    for (int rho = 0; rho < R; ++rho) {  // rows past the batch re-read its last row
+      const int sel = list(ie)[ij * B + min(rho * RG + j, nb_next - 1)];
+      sel_next[rho] = (uint32_t)sel < N ? sel : 0;
+    }
     if (++ij == S) {
       ij = 0;
       ++ie;
     }
   };
-  int fetched = 0;
   auto fetch = [&](Batch<R, KP, DOUT, RY>& f) {
-    // Unconditional loads from clamped addresses (no exec-mask branches): rows
-    // past the batch get g = 0 in train(), padded features are masked there.
+    // Unconditional loads (no exec-mask branches), immediate offsets from one
+    // address per row: rows past the batch re-read a valid row and get g = 0.
     f.nb = nb_next;
 #pragma unroll
     for (int rho = 0; rho < R; ++rho) {
-      const auto xr = X + (int64_t)sel_next[rho] * Din + k0;
-      if (!padded) {  // immediate offsets from one address
+      const auto xr = X + (int64_t)sel_next[rho] * ldx + k0;
 #pragma unroll
-        for (int k = 0; k < KP; ++k) f.x[rho][k] = xr[k];
-      } else {
-#pragma unroll
-        for (int k = 0; k < KP; ++k) f.x[rho][k] = xr[min(k, Din - 1 - k0)];
-      }
+      for (int k = 0; k < KP; ++k) f.x[rho][k] = xr[k];
     }
 #pragma unroll
     for (int ry = 0; ry < RY; ++ry) {
@@ -253,8 +251,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
         for (int c = 0; c < DOUT; ++c) f.y[ry][c] = gptr(a.Yf)[(int64_t)sel * DOUT + c];
       }
     }
-    ++fetched;
-    if (fetched < n) read_index();
+    read_index();
   };
 
   Ticks tk;
@@ -277,6 +274,18 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
         l = fmaf(df, df, l);
         g[c] = 2.f * df;
       }
+    } else if constexpr (DOUT == 1) {
+      // one class: log_softmax(z) = z - z (0, or NaN for a non-finite z) -- no exp/log
+      const float ls0 = z[0] - z[0];
+      if constexpr (LOSS == kLossCESoft) {
+        l = -y[0] * ls0;
+        g[0] = (ls0 + 1.f) * y[0] - y[0];
+      } else {
+        const bool use = yi != a.ignore_index;
+        g[0] = use ? (ls0 + 1.f) - (yi == 0 ? 1.f : 0.f) : 0.f;
+        l = use ? -(yi == 0 ? ls0 : 0.f) : 0.f;
+        cnt = use ? 1.f : 0.f;
+      }
     } else {
       float m = z[0];
 #pragma unroll
@@ -284,7 +293,8 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
       float se = 0.f;
 #pragma unroll
       for (int c = 0; c < DOUT; ++c) se += __expf(z[c] - m);
-      const float lse = m + __logf(se);
+      // se >= 1 (the max term is exp(0)): the hardware log2 needs no denormal fix-up
+      const float lse = m + __builtin_amdgcn_logf(se) * 0.6931471805599453f;
       if constexpr (LOSS == kLossCESoft) {
         float tsum = 0.f;
 #pragma unroll
@@ -316,12 +326,6 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
 
   auto train = [&](Batch<R, KP, DOUT, RY>& f, int step) {
     const int nb = f.nb;
-    if (padded) {
-#pragma unroll
-      for (int rho = 0; rho < R; ++rho)
-#pragma unroll
-        for (int k = 0; k < KP; ++k) f.x[rho][k] *= kmask[k];
-    }
     // ---- forward
     float z[R][DOUT];
 #pragma unroll
@@ -516,20 +520,26 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
   tk.start();
   read_index();
 #pragma unroll
-  for (int u = 0; u < kNB; ++u)
-    if (u < n) fetch(buf[u]);
+  for (int u = 0; u < kNB; ++u) fetch(buf[u]);
   tk.tick(0);
+  // main loop: whole groups of kNB steps, straight-line body (every fetch
+  // unconditional); then the < kNB tail steps
   int done = 0;
-  for (int base = 0; base < n && !failed; base += kNB) {
+  const int nfull = n - n % kNB;
+  while (done < nfull && !failed) {
 #pragma unroll
     for (int u = 0; u < kNB; ++u) {
-      const int step = base + u;
-      if (step < n && !failed) {
-        train(buf[u], step);
-        if (step + kNB < n) fetch(buf[u]);
-        tk.tick(0);
-        done = step + 1;
-      }
+      train(buf[u], done + u);
+      fetch(buf[u]);
+      tk.tick(0);
+    }
+    done += kNB;
+  }
+#pragma unroll
+  for (int u = 0; u < kNB - 1; ++u) {
+    if (done < n && !failed) {
+      train(buf[u], done);
+      ++done;
     }
   }
   // a failed all-reduce stops training early: still meet the producers at every barrier

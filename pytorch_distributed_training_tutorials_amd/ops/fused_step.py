@@ -160,6 +160,7 @@ class FusedMLPStep:
             raise RuntimeError("the persistent engine needs the xGMI all-reduce for world > 1")
         ce_index = self.loss_kind == LOSS_KINDS["ce_index"]
         vid = _variant_id(variant)
+        X, padded = self._wave_input(X, batch_size, sampler, vid)
         done = 0
         while done < n_steps:
             n = min(max_steps_per_launch, n_steps - done)
@@ -168,9 +169,29 @@ class FusedMLPStep:
                 batch_size, self.Din, self.H, self.Dout, self.loss_kind, self.ignore_index, self.has_bias,
                 self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
                 self.xgmi.handle if self.xgmi is not None else None, n, sampler.num_replicas, sampler.rank,
-                sampler.num_samples, sampler.shuffle, sampler.seed, cursor, losses, stamps, vid)
+                sampler.num_samples, sampler.shuffle, sampler.seed, cursor, losses, stamps, vid, padded)
             done += n
         self._pending = False
+
+    def _wave_input(self, X, batch_size, sampler, vid):
+        """The wave engine reads whole lane chunks (L lanes x K features per row):
+        when L*K > Din, hand it a zero-padded copy of X (cached per tensor version)."""
+        eng = self._C.persistent_engine(batch_size, self.Din, self.H, self.Dout, self.loss_kind,
+                                        sampler.num_samples, sampler.num_replicas, vid)
+        if not eng.startswith("wave"):
+            return X, False
+        lanes, kp = int(eng.split("L")[1].split("R")[0]), int(eng.split("K")[1])
+        width = lanes * kp
+        if width <= self.Din:
+            return X, False
+        key = (X.data_ptr(), X._version, tuple(X.shape), width)
+        cached = getattr(self, "_xpad", None)
+        if cached is None or cached[0] != key:
+            xp = torch.zeros(X.shape[0], width, device=X.device, dtype=X.dtype)
+            xp[:, :self.Din].copy_(X)
+            cached = (key, xp[:, :self.Din])
+            self._xpad = cached
+        return cached[1], True
 
     def persistent_engine(self, batch_size: int, sampler, variant: str | None = None) -> str:
         """Which persistent engine :meth:`run_persistent` runs: "workgroup" or
