@@ -38,6 +38,15 @@ void check_gpu(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
 
+// Elementwise optimizer operands: any dense memory order (channels_last conv
+// weights), as long as every operand of one parameter shares it.
+void check_dense_like(const Tensor& p, const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_non_overlapping_and_dense(), name, " must be dense (non-overlapping)");
+  TORCH_CHECK(t.numel() == p.numel() && (t.strides() == p.strides() || (t.is_contiguous() && p.is_contiguous())),
+              name, " must have the parameter's memory layout");
+}
+
 template <typename T>
 T* ptr_or_null(const c10::optional<Tensor>& t) {
   return (t.has_value() && t->defined()) ? static_cast<T*>(t->data_ptr()) : nullptr;
@@ -250,8 +259,9 @@ void sgd_multi_(std::vector<Tensor> ps, std::vector<Tensor> gs, std::vector<Tens
     TensorList tl{};
     tl.n = (int)(b - a);
     for (size_t i = a; i < b; ++i) {
-      check_gpu(ps[i], "param");
-      check_gpu(gs[i], "grad");
+      check_dense_like(ps[i], ps[i], "param");
+      check_dense_like(ps[i], gs[i], "grad");
+      if (!moms.empty()) check_dense_like(ps[i], moms[i], "momentum buffer");
       TORCH_CHECK(dt_of(ps[i]) == dt && gs[i].scalar_type() == ps[i].scalar_type() && gs[i].numel() == ps[i].numel());
       tl.numel[i - a] = ps[i].numel();
       tl.p[i - a] = ps[i].data_ptr();
@@ -276,8 +286,10 @@ void adam_multi_(std::vector<Tensor> ps, std::vector<Tensor> gs, std::vector<Ten
     TensorList tl{};
     tl.n = (int)(b - a);
     for (size_t i = a; i < b; ++i) {
-      check_gpu(ps[i], "param");
-      check_gpu(gs[i], "grad");
+      check_dense_like(ps[i], ps[i], "param");
+      check_dense_like(ps[i], gs[i], "grad");
+      check_dense_like(ps[i], ms[i], "exp_avg");
+      check_dense_like(ps[i], vs[i], "exp_avg_sq");
       TORCH_CHECK(dt_of(ps[i]) == dt && gs[i].numel() == ps[i].numel());
       TORCH_CHECK(ms[i].scalar_type() == at::kFloat && vs[i].scalar_type() == at::kFloat);
       tl.numel[i - a] = ps[i].numel();

@@ -109,7 +109,7 @@ void Reducer::build(std::vector<std::vector<int64_t>> plan, bool copy_old) {
     b.flat = at::zeros({off}, p0.options().requires_grad(false));
     for (size_t k = 0; k < b.params.size(); ++k) {
       const int64_t i = b.params[k];
-      auto view = b.flat.narrow(0, b.offsets[k], params_[i].numel()).view(params_[i].sizes());
+      auto view = bucket_view(b, k, i);
       const auto& old = params_[i].grad();
       if (copy_old && old.defined()) view.copy_(old);
       param_bucket_[i] = (int64_t)bi;
@@ -156,12 +156,23 @@ void Reducer::prepare_for_backward(bool sync) {
   if (record_order_) ready_order_.clear();
 }
 
+// The grad view of params_[i] inside its bucket. It keeps the parameter's
+// strides when the parameter is dense (e.g. channels_last conv weights), so
+// grad and param share one memory order ("gradient layout contract") and the
+// flat multi-tensor optimizers can treat both as plain arrays.
+at::Tensor Reducer::bucket_view(const Bucket& b, size_t k, int64_t i) const {
+  const auto& p = params_[i];
+  auto flat = b.flat.narrow(0, b.offsets[k], p.numel());
+  if (p.is_non_overlapping_and_dense() && !p.is_contiguous()) return flat.as_strided(p.sizes(), p.strides());
+  return flat.view(p.sizes());
+}
+
 // Make params_[i].grad the bucket view again (a user may have set grads to
 // None, or autograd may have assigned a fresh tensor on the first accumulation).
 void Reducer::ensure_view(int64_t i) {
   auto& b = buckets_[param_bucket_[i]];
   const int64_t k = param_slot_[i];
-  auto view = b.flat.narrow(0, b.offsets[k], params_[i].numel()).view(params_[i].sizes());
+  auto view = bucket_view(b, k, i);
   auto& g = params_[i].mutable_grad();
   if (!g.defined()) {
     view.zero_();

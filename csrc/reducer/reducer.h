@@ -82,6 +82,7 @@ class Reducer {
   void build(std::vector<std::vector<int64_t>> buckets, bool copy_old);
   void launch(size_t b);
   void ensure_view(int64_t i);
+  at::Tensor bucket_view(const Bucket& b, size_t k, int64_t i) const;
 
   std::vector<at::Tensor> params_;
   std::vector<Bucket> buckets_;

@@ -65,12 +65,14 @@ class FlatParameters:
 
 
 def contiguous_span(tensors) -> torch.Tensor | None:
-    """If ``tensors`` are back-to-back views of one storage (in order), return the
-    1-D view covering all of them, else None."""
+    """If ``tensors`` are back-to-back dense blocks of one storage (in order; any
+    dense memory order, e.g. channels_last), return the 1-D view covering all
+    of them, else None. Elementwise use of two spans is only valid when the
+    tensors pair up with equal strides (:func:`same_layout`)."""
     if not tensors:
         return None
     t0 = tensors[0]
-    if not all(t.is_contiguous() for t in tensors):
+    if not all(is_dense(t) for t in tensors):
         return None
     st = t0.untyped_storage().data_ptr()
     esz = t0.element_size()
@@ -83,3 +85,28 @@ def contiguous_span(tensors) -> torch.Tensor | None:
     base = torch.empty(0, dtype=t0.dtype, device=t0.device).set_(
         t0.untyped_storage(), t0.storage_offset(), (total,), (1,))
     return base
+
+
+def is_dense(t: torch.Tensor) -> bool:
+    """Non-overlapping and dense: the elements fill exactly numel() consecutive
+    slots starting at data_ptr() (any dimension order, positive strides)."""
+    if t.is_contiguous():
+        return True
+    expect = 1
+    for stride, size in sorted((st, sz) for st, sz in zip(t.stride(), t.shape) if sz != 1):
+        if stride != expect:
+            return False
+        expect *= size
+    return True
+
+
+def same_layout(xs, ys) -> bool:
+    """Pairwise equal shapes and memory orders (strides)."""
+    return len(xs) == len(ys) and all(a.shape == b.shape and a.stride() == b.stride() for a, b in zip(xs, ys))
+
+
+def dense_like(buf: torch.Tensor, p: torch.Tensor) -> torch.Tensor:
+    """View ``buf`` (1-D, p.numel() elements) with ``p``'s shape and memory order."""
+    if p.is_contiguous() or not is_dense(p):
+        return buf.view(p.shape)
+    return buf.as_strided(p.shape, p.stride())

@@ -20,7 +20,7 @@ import torch
 from torch.optim import Optimizer
 
 from .._ext import native
-from .flat import contiguous_span
+from .flat import contiguous_span, dense_like, same_layout
 
 
 def _split_by_device(params):
@@ -64,7 +64,7 @@ class FusedSGD(Optimizer):
         flat = torch.zeros(total, device=ps[0].device, dtype=torch.float32)
         out, off = [], 0
         for p in ps:
-            v = flat[off:off + p.numel()].view_as(p)
+            v = dense_like(flat[off:off + p.numel()], p)
             old = self.state[p].get("momentum_buffer")
             if old is not None:
                 v.copy_(old)
@@ -94,7 +94,10 @@ class FusedSGD(Optimizer):
                 pflat = contiguous_span([p.data for p in ps])
                 gflat = contiguous_span(grads)
                 mflat = contiguous_span(moms) if moms else None
-                if dtype == torch.float32 and pflat is not None and gflat is not None and (not moms or mflat is not None):
+                pdata = [p.data for p in ps]
+                aligned = same_layout(pdata, grads) and (not moms or same_layout(pdata, moms))
+                if (dtype == torch.float32 and aligned and pflat is not None and gflat is not None
+                        and (not moms or mflat is not None)):
                     # one launch for the whole group (also increments the device counter)
                     C.sgd_flat_(pflat, gflat, mflat, step, lr, mu, damp, wd, nest, gscale)
                 else:
@@ -136,8 +139,8 @@ class FusedAdam(Optimizer):
             fv = torch.zeros(total, device=need[0].device, dtype=torch.float32)
             off = 0
             for p in need:
-                self.state[p]["exp_avg"] = fm[off:off + p.numel()].view(p.shape)
-                self.state[p]["exp_avg_sq"] = fv[off:off + p.numel()].view(p.shape)
+                self.state[p]["exp_avg"] = dense_like(fm[off:off + p.numel()], p)
+                self.state[p]["exp_avg_sq"] = dense_like(fv[off:off + p.numel()], p)
                 off += p.numel()
         return [self.state[p]["exp_avg"] for p in ps], [self.state[p]["exp_avg_sq"] for p in ps]
 
@@ -164,7 +167,9 @@ class FusedAdam(Optimizer):
                 grads = [p.grad for p in ps]
                 pflat, gflat = contiguous_span([p.data for p in ps]), contiguous_span(grads)
                 mflat, vflat = contiguous_span(ms), contiguous_span(vs)
-                if dtype == torch.float32 and None not in (pflat, gflat, mflat, vflat):
+                pdata = [p.data for p in ps]
+                aligned = same_layout(pdata, grads) and same_layout(pdata, ms) and same_layout(pdata, vs)
+                if dtype == torch.float32 and aligned and None not in (pflat, gflat, mflat, vflat):
                     C.adam_flat_(pflat, gflat, mflat, vflat, step, group["lr"], b1, b2, group["eps"],
                                  group["weight_decay"], group["decoupled_weight_decay"], gscale)
                 else:

@@ -361,3 +361,25 @@ def test_bn_relu(native, dev):
     sc, sh = torch.randn(6, device=dev), torch.randn(6, device=dev)
     y = native.bn_relu(x, sc, sh, True)
     torch.testing.assert_close(y, F.relu(x * sc[None, :, None, None] + sh[None, :, None, None]))
+
+
+def test_fused_optimizers_channels_last(native, dev):
+    """channels_last conv weights: grads/state keep the parameter's memory order and
+    the native SGD/Adam match torch.optim (ResNet-50 DDP bench path)."""
+    from pytorch_distributed_training_tutorials_amd.ops.optim import FusedAdam, FusedSGD
+
+    for opt_cls, ref_cls, kw in ((FusedSGD, torch.optim.SGD, dict(lr=0.1, momentum=0.9, weight_decay=1e-4)),
+                                 (FusedAdam, torch.optim.Adam, dict(lr=1e-2))):
+        torch.manual_seed(0)
+        conv = torch.nn.Conv2d(8, 16, 3).to(dev).to(memory_format=torch.channels_last)
+        ref = torch.nn.Conv2d(8, 16, 3).to(dev).to(memory_format=torch.channels_last)
+        ref.load_state_dict(conv.state_dict())
+        o1, o2 = opt_cls(conv.parameters(), **kw), ref_cls(ref.parameters(), **kw)
+        x = torch.randn(4, 8, 10, 10, device=dev).to(memory_format=torch.channels_last)
+        for _ in range(3):
+            for m, o in ((conv, o1), (ref, o2)):
+                o.zero_grad()
+                m(x).square().mean().backward()
+                o.step()
+        assert not conv.weight.is_contiguous()  # stayed channels_last
+        torch.testing.assert_close(conv.weight, ref.weight, rtol=1e-5, atol=1e-6)

@@ -131,3 +131,25 @@ def test_trainer_autograd_engine_mlp_learns(pg, dev):
     t.train(5)
     l1 = float(cross_entropy(model(x), y))
     assert l1 < l0
+
+
+def test_ddp_channels_last_grads_keep_param_layout(pg, dev):
+    """Native DDP reducer: bucket views of channels_last weights use the parameter's
+    strides (no layout-contract copies) and FusedSGD steps them in place."""
+    from pytorch_distributed_training_tutorials_amd.ops.optim import FusedSGD
+    from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
+    from pytorch_distributed_training_tutorials_amd.parallel.ddp import DistributedDataParallel
+
+    torch.manual_seed(1)
+    model = torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3), torch.nn.ReLU(), torch.nn.Conv2d(8, 4, 3))
+    model = model.to(dev).to(memory_format=torch.channels_last)
+    ddp = DistributedDataParallel(model, device_ids=[dev.index], comm=comm_mod.get_default(dev))
+    opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9)
+    x = torch.randn(2, 3, 12, 12, device=dev).to(memory_format=torch.channels_last)
+    ddp.zero_grad()
+    ddp(x).sum().backward()
+    w = model[0].weight
+    assert w.grad.stride() == w.stride()
+    before = w.detach().clone()
+    opt.step()
+    torch.testing.assert_close(w.detach(), before - 0.1 * w.grad, rtol=1e-6, atol=1e-7)
