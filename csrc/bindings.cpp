@@ -192,7 +192,7 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
   }
   pa.variant = (int)variant;
   const bool wave = variant != kPersistWorkgroup && linear_wave_supported(a, pa);
-  TORCH_CHECK(wave || variant != kPersistWave, "persistent: the wave engine does not support this configuration");
+  TORCH_CHECK(wave || variant < kPersistWave, "persistent: the wave engine does not support this configuration");
   TORCH_CHECK(wave || fused_mlp_persistent_lds_bytes((int)B, (int)Din, (int)H, (int)Dout, (int)num_samples,
                                                      world) <= 160 * 1024,
               "persistent: model + epoch index list do not fit one workgroup's LDS");
@@ -210,6 +210,7 @@ std::string persistent_engine(int64_t B, int64_t Din, int64_t H, int64_t Dout, i
   a.x_padded = 1;
   PersistArgs pa{};
   pa.num_samples = (int)num_samples;
+  pa.variant = (int)variant;
   if (variant != kPersistWorkgroup && linear_wave_supported(a, pa)) {
     int L = 0, R = 0, kp = 0;
     linear_wave_layout(a, pa, &L, &R, &kp);

@@ -703,7 +703,7 @@ hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hip
   if (a.ar.world > 1 && (num_params(a) > a.ar.max_elems || a.ar.world != p.W || a.ar.rank != p.rank))
     return hipErrorInvalidValue;
   if (p.variant != kPersistWorkgroup && linear_wave_supported(a, p)) return linear_wave_persistent(a, p, s);
-  if (p.variant == kPersistWave) return hipErrorInvalidValue;
+  if (p.variant >= kPersistWave) return hipErrorInvalidValue;
   const size_t lds = fused_mlp_persistent_lds_bytes(a.B, a.Din, a.H, a.Dout, p.num_samples, a.ar.world);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const void* fn = a.H > 0 ? pick_persist<true>(a.loss_kind) : pick_persist<false>(a.loss_kind);

@@ -78,7 +78,11 @@ struct PersistArgs {
 // Linear(Din, Dout) models with B <= 64 and small Dout; everything else runs the
 // LDS workgroup engine (fused_mlp.hip). kPersistAuto picks the wave engine when
 // it supports the configuration.
-enum PersistVariant : int { kPersistAuto = 0, kPersistWorkgroup = 1, kPersistWave = 2 };
+// kPersistWaveRows / kPersistWaveF restrict the wave engine to one lane-layout
+// family (row groups across DPP rows / feature groups across DPP rows).
+enum PersistVariant : int {
+  kPersistAuto = 0, kPersistWorkgroup = 1, kPersistWave = 2, kPersistWaveRows = 3, kPersistWaveF = 4
+};
 hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s);
 bool linear_wave_supported(const FusedMlpArgs& a, const PersistArgs& p);
 // lane layout the wave engine picks: L lanes per row, R rows per lane group, kp features per lane

@@ -35,6 +35,13 @@ int log2i(int v) {
 // (FMA ~5, DPP add ~5.6, permlane swap + add ~30 cycles, a row's CE ~70): picks
 // the lane layout (L lanes per row, R rows per lane group) for a shape.
 double model_cycles(int L, int R, int kp, int dout) {
+  if (L == 0) {  // layout F: features across DPP rows, rows across the 16 lanes of a DPP row
+    const bool scatter = dout == 1 && R > 1;
+    const double fwd = R * kp * dout * 5.0 + (scatter ? (R == 2 ? 2 : 3) * 25.0 : R * dout * 2 * 30.0);
+    const double loss = (scatter ? 1 : R) * (30.0 + 40.0 * dout) + (scatter ? (R == 2 ? 1 : 3) * 25.0 : 0.0);
+    const double bwd = R * kp * dout * 5.0 + (kp + 1) * dout * 4 * 5.6;
+    return fwd + loss + bwd + (kp + 1) * dout * 10.0 + R * kp * 3.0;
+  }
   const bool split = R > 1 && (L == 2 || L == 4) && R <= L;
   const int loss_rows = split ? 1 : R;
   const double fwd = R * kp * dout * 5.0 + R * dout * log2i(L) * 5.6;
@@ -56,17 +63,20 @@ Choice choose(const FusedMlpArgs& a, const PersistArgs& p) {
   if (a.ar.world > kXgmiMaxRanks) return best;
   if (lds_bytes(p) > 160 * 1024) return best;
   const bool ar = a.ar.world > 1;
-  static const int kLR[][2] = {{1, 1}, {2, 1}, {4, 1}, {8, 1}, {2, 2}, {4, 2}};
+  static const int kLR[][2] = {{1, 1}, {2, 1}, {4, 1}, {8, 1}, {2, 2}, {4, 2}, {0, 1}, {0, 2}, {0, 4}};
   double best_cost = 1e30;
+  const int ldx = a.ldx > 0 ? a.ldx : a.Din;
   for (const auto& lr : kLR) {
     const int L = lr[0], R = lr[1];
-    if ((64 / L) * R < a.B) continue;                // rows must fit one pass
-    if (ar && 64 / L < a.ar.world) continue;         // one row group per rank
-    const int need = (a.Din + L - 1) / L;
-    const int ldx = a.ldx > 0 ? a.ldx : a.Din;
+    if ((p.variant == kPersistWaveRows && L == 0) || (p.variant == kPersistWaveF && L != 0)) continue;
+    const int lanes = L == 0 ? 4 : L;            // feature chunks per row
+    const int groups = L == 0 ? 16 : 64 / L;     // row slots
+    if (groups * R < a.B) continue;              // rows must fit one pass
+    if (ar && groups < a.ar.world) continue;     // one row slot per rank
+    const int need = (a.Din + lanes - 1) / lanes;
     int kp = -1;
     for (int c : {4, 5, 8, 10, 16})
-      if (c >= need && (L * c == a.Din || (a.x_padded && L * c <= ldx))) {  // lane chunks read zero padding
+      if (c >= need && (lanes * c == a.Din || (a.x_padded && lanes * c <= ldx))) {  // chunks read zero padding
         kp = c;
         break;
       }

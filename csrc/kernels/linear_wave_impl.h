@@ -91,15 +91,21 @@ __device__ __forceinline__ float col_sum(float v) {
 // Optional per-phase s_memtime accounting (PersistArgs::stamps). Accumulators
 // live in LDS, not SGPRs: the untimed build of the loop must not pay register
 // pressure for diagnostics.
+// Per-phase timers are compiled in only with -DPTDT_WAVE_STAMPS=1 (diagnostic
+// builds): in the production build a tick is nothing, not even a branch --
+// each skipped tick cost a taken branch plus an lgkmcnt(0) join per step.
+#ifndef PTDT_WAVE_STAMPS
+#define PTDT_WAVE_STAMPS 0
+#endif
 struct Ticks {
   bool on = false;
   int64_t prev = 0;
   unsigned long long* acc = nullptr;  // LDS [8]
   __device__ __forceinline__ void start() {
-    if (on) prev = (int64_t)__builtin_amdgcn_s_memtime();
+    if (PTDT_WAVE_STAMPS && on) prev = (int64_t)__builtin_amdgcn_s_memtime();
   }
   __device__ __forceinline__ void tick(int k) {
-    if (on) {
+    if (PTDT_WAVE_STAMPS && on) {
       const int64_t t = (int64_t)__builtin_amdgcn_s_memtime();
       if (threadIdx.x == 0) acc[k] += (unsigned long long)(t - prev);
       prev = t;
@@ -206,7 +212,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
   // index lookahead: the dataset rows of the next batch are read from LDS one
   // fetch before the gather that uses them
   int ie = e0, ij = j0, barriers = 0;
-  int sel_next[R], nb_next = 0;
+  int sel_next[R], sel_y_next = 0, nb_next = 0;
   // Always called (also for the kNB positions past this launch, whose lists may
   // be stale): no conditional loads in the loop, so the waitcnt pass can count
   // the outstanding prefetches exactly instead of falling back to vmcnt(0).
@@ -221,6 +227,10 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
     for (int rho = 0; rho < R; ++rho) {  // rows past the batch re-read its last row
       const int sel = list(ie)[ij * B + min(rho * RG + j, nb_next - 1)];
       sel_next[rho] = (uint32_t)sel < N ? sel : 0;
+    }
+    if constexpr (SPLIT) {  // own row's index read directly (selecting by a lane value spills)
+      const int sel = list(ie)[ij * B + min(rho_y * RG + j, nb_next - 1)];
+      sel_y_next = (uint32_t)sel < N ? sel : 0;
     }
     if (++ij == S) {
       ij = 0;
@@ -239,11 +249,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
     }
 #pragma unroll
     for (int ry = 0; ry < RY; ++ry) {
-      int sel = sel_next[ry];
-      if constexpr (SPLIT) {
-#pragma unroll
-        for (int rho = 1; rho < R; ++rho) sel = rho_y == rho ? sel_next[rho] : sel;
-      }
+      const int sel = SPLIT ? sel_y_next : sel_next[ry];
       if constexpr (LOSS == kLossCEIndex) {
         f.yi[ry] = (int)gptr(a.Yi)[sel];
       } else {
@@ -582,11 +588,534 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
   }
 }
 
+// ============================================================================
+// Layout F ("features across DPP rows"): lane (q, i) = (lane / 16, lane % 16).
+// DPP row q owns feature group q (KP consecutive features, 4 * KP >= Din);
+// row slot i holds batch rows i + 16 * rho, rho < R (B <= 16 R).
+//   forward : the 4 feature-group partial logits of a row meet with permlane
+//             swaps; with DOUT == 1 the R rows are reduce-scattered in pairs
+//             (one swap per pair and stage, no register copies), so each lane
+//             ends with ONE row's logit and computes that row's loss;
+//   dL/dz   : all-gathered back with the same swaps;
+//   backward: the column sum over the 16 row slots of a DPP row is 4 row_ror
+//             DPP adds -- no permlane at all (vs 2 per gradient element when
+//             rows span DPP rows). Measured issue costs (tools/microbench_isa):
+//             DPP add ~5.6 cycles, permlane swap ~20.
+// All reductions pair lanes symmetrically (a+b / b+a): every lane that holds
+// a value holds the same bits.
+
+struct F2 {
+  float a, b;
+};
+// permlane16_swap(A, B): A' = rows [A0, B0, A2, B2], B' = rows [A1, B1, A3, B3]
+__device__ __forceinline__ F2 pl16(float a, float b) {
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(a), __float_as_int(b), false, false);
+  return {__int_as_float(p[0]), __int_as_float(p[1])};
+}
+// permlane32_swap(A, B): A' = rows [A0, A1, B0, B1], B' = rows [A2, A3, B2, B3]
+__device__ __forceinline__ F2 pl32(float a, float b) {
+  auto p = __builtin_amdgcn_permlane32_swap(__float_as_int(a), __float_as_int(b), false, false);
+  return {__int_as_float(p[0]), __int_as_float(p[1])};
+}
+// stage-16 reduce-scatter of a pair: rows [a0+a1, b0+b1, a2+a3, b2+b3]
+__device__ __forceinline__ float rs16(float a, float b) {
+#pragma clang fp contract(off)
+  const F2 r = pl16(a, b);
+  return r.a + r.b;
+}
+// stage-32 reduce-scatter of a pair: rows [a0+a2, a1+a3, b0+b2, b1+b3]
+__device__ __forceinline__ float rs32(float a, float b) {
+#pragma clang fp contract(off)
+  const F2 r = pl32(a, b);
+  return r.a + r.b;
+}
+// full sum over the 4 DPP rows, in every lane
+__device__ __forceinline__ float allrows(float v) {
+  const float s = rs16(v, v);
+  return rs32(s, s);
+}
+// sum over the 16 lanes of a DPP row (row_ror 8, 4, 2, 1), in every lane of the row
+__device__ __forceinline__ float row16_sum(float v) {
+#pragma clang fp contract(off)
+  v += dpp_f<kDppRor8>(v);
+  v += dpp_f<kDppRor4>(v);
+  v += dpp_f<kDppRor2>(v);
+  v += dpp_f<kDppRor1>(v);
+  return v;
+}
+
+template <int R, int KP, int DOUT, int LOSS, bool AR>
+__global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a, PersistArgs pa) {
+  static_assert(R == 1 || R == 2 || R == 4, "rows per lane: 1, 2 or 4");
+  // DOUT == 1: reduce-scatter, one row per lane (rows q & (R-1)); else every lane all rows
+  constexpr bool SCATTER = DOUT == 1 && R > 1;
+  constexpr int RY = SCATTER ? 1 : R;  // target rows a lane loads / computes the loss of
+  extern __shared__ int elist[];
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int B = a.B, Din = a.Din;
+  const int estride = al4(pa.num_samples);
+  const int S = (pa.num_samples + B - 1) / B;
+  const int e0 = pa.cursor[0], j0 = pa.cursor[1];
+  const int64_t pos0 = (int64_t)e0 * S + j0;
+  const int n = pa.n_steps;
+  const int T = (int)((pos0 + n - 1) / S - pos0 / S);
+  auto list = [&](int e) { return elist + (e & 1) * estride; };
+
+  rank_epoch_indices(list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
+                     (int)threadIdx.x, kThreads);
+  if (T > 0)
+    rank_epoch_indices(list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1, pa.shuffle,
+                       (int)threadIdx.x, kThreads);
+  __syncthreads();
+  if (wave != 0) {
+    for (int i = 1; i <= T; ++i) {
+      __syncthreads();
+      if (i < T)
+        rank_epoch_indices(list(e0 + i + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + i + 1,
+                           pa.shuffle, (int)threadIdx.x - 64, kThreads - 64);
+    }
+    return;
+  }
+
+  const int lane = (int)threadIdx.x;
+  const int q = lane >> 4, i = lane & 15;  // feature group, row slot
+  const int k0 = q * KP;
+  const int rho_own = SCATTER ? (q & (R - 1)) : 0;  // the row whose loss this lane computes
+  const bool hb = a.has_bias != 0;
+  const bool use_mom = a.mom != nullptr && a.momentum != 0.f;
+  const float lr = a.lr, mu = a.momentum, damp = a.dampening, wd = a.weight_decay;
+  const int nesterov = a.nesterov;
+  const auto X = gptr(a.X);
+  const int nW = DOUT * Din;
+  const int ldx = a.ldx > 0 ? a.ldx : Din;  // feature slots past Din read X's zero padding
+
+  float W[DOUT][KP], M[DOUT][KP], Wb[DOUT], Mb[DOUT];
+  {
+    const auto P = gptr(a.P);
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        const bool in = k0 + k < Din;
+        W[c][k] = in ? P[c * Din + k0 + k] : 0.f;
+        M[c][k] = (in && use_mom) ? gptr(a.mom)[c * Din + k0 + k] : 0.f;
+      }
+      Wb[c] = hb ? P[nW + c] : 0.f;
+      Mb[c] = (hb && use_mom) ? gptr(a.mom)[nW + c] : 0.f;
+    }
+  }
+  int opt_step = a.opt_step ? *a.opt_step : 0;
+  const XgmiArgs& ar = a.ar;
+  const int world = AR ? ar.world : 1;
+  uint64_t PTDT_GLOBAL* push_dst = nullptr;  // row slot i pushes to rank i
+#pragma unroll
+  for (int r = 0; r < kXgmiMaxRanks; ++r)
+    if (i == r && r < world) push_dst = (uint64_t PTDT_GLOBAL*)ar.peers[r];
+  uint64_t PTDT_GLOBAL* const poll_src = (uint64_t PTDT_GLOBAL*)ar.local;
+  const int my_rank = ar.rank, max_elems = ar.max_elems;
+  float PTDT_GLOBAL* const losses = gptr_w(pa.losses);
+  uint32_t seq = AR ? *ar.seq : 0u;
+  bool failed = AR && *ar.err != 0;
+  const float inv_w = 1.f / (float)world;
+
+  const uint32_t N = (uint32_t)pa.N;
+  int ie = e0, ij = j0, barriers = 0;
+  int sel_next[R], sel_y_next = 0, nb_next = 0;
+  auto read_index = [&]() {
+    if (ij == 0 && ie != e0 && barriers < T) {
+      __syncthreads();
+      ++barriers;
+    }
+    nb_next = min(B, pa.num_samples - ij * B);
+#pragma unroll
+    for (int rho = 0; rho < R; ++rho) {
+      const int sel = list(ie)[ij * B + min(rho * 16 + i, nb_next - 1)];
+      sel_next[rho] = (uint32_t)sel < N ? sel : 0;
+    }
+    if constexpr (SCATTER) {  // own row's index read directly: selecting from sel_next[] by a lane
+      const int sel = list(ie)[ij * B + min(rho_own * 16 + i, nb_next - 1)];  // value spills it
+      sel_y_next = (uint32_t)sel < N ? sel : 0;
+    }
+    if (++ij == S) {
+      ij = 0;
+      ++ie;
+    }
+  };
+  auto fetch = [&](Batch<R, KP, DOUT, RY>& f) {
+    f.nb = nb_next;
+#pragma unroll
+    for (int rho = 0; rho < R; ++rho) {
+      const auto xr = X + (int64_t)sel_next[rho] * ldx + k0;
+#pragma unroll
+      for (int k = 0; k < KP; ++k) f.x[rho][k] = xr[k];
+    }
+#pragma unroll
+    for (int ry = 0; ry < RY; ++ry) {
+      const int sel = SCATTER ? sel_y_next : sel_next[ry];
+      if constexpr (LOSS == kLossCEIndex) {
+        f.yi[ry] = (int)gptr(a.Yi)[sel];
+      } else {
+#pragma unroll
+        for (int c = 0; c < DOUT; ++c) f.y[ry][c] = gptr(a.Yf)[(int64_t)sel * DOUT + c];
+      }
+    }
+    read_index();
+  };
+
+  Ticks tk;
+  tk.on = pa.stamps != nullptr;
+  tk.acc = reinterpret_cast<unsigned long long*>(elist + 2 * estride);
+  if (tk.on && lane == 0)
+    for (int k = 0; k < 8; ++k) tk.acc[k] = 0ull;
+  const int nb_last = pa.num_samples - (S - 1) * B;  // the one short batch size (== B if none)
+  const float inv_full = 1.f / (float)((LOSS == kLossMSE) ? B * DOUT : B);
+  const float inv_last = 1.f / (float)((LOSS == kLossMSE) ? nb_last * DOUT : nb_last);
+  const int64_t t_begin = tk.on ? (int64_t)__builtin_amdgcn_s_memtime() : 0;
+  const int64_t r_begin = tk.on ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+
+  auto row_loss = [&](const float* z, const float* y, int yi, bool valid, float* g, float& l, float& cnt) {
+    l = 0.f;
+    cnt = 0.f;
+    if constexpr (LOSS == kLossMSE) {
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) {
+        const float df = z[c] - y[c];
+        l = fmaf(df, df, l);
+        g[c] = 2.f * df;
+      }
+    } else if constexpr (DOUT == 1) {
+      const float ls0 = z[0] - z[0];  // log_softmax of one class: 0 (NaN if z is not finite)
+      if constexpr (LOSS == kLossCESoft) {
+        l = -y[0] * ls0;
+        g[0] = (ls0 + 1.f) * y[0] - y[0];
+      } else {
+        const bool use = yi != a.ignore_index;
+        g[0] = use ? (ls0 + 1.f) - (yi == 0 ? 1.f : 0.f) : 0.f;
+        l = use ? -(yi == 0 ? ls0 : 0.f) : 0.f;
+        cnt = use ? 1.f : 0.f;
+      }
+    } else {
+      float m = z[0];
+#pragma unroll
+      for (int c = 1; c < DOUT; ++c) m = fmaxf(m, z[c]);
+      float se = 0.f;
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) se += __expf(z[c] - m);
+      const float lse = m + __builtin_amdgcn_logf(se) * 0.6931471805599453f;
+      if constexpr (LOSS == kLossCESoft) {
+        float tsum = 0.f;
+#pragma unroll
+        for (int c = 0; c < DOUT; ++c) {
+          tsum += y[c];
+          l -= y[c] * (z[c] - lse);
+        }
+#pragma unroll
+        for (int c = 0; c < DOUT; ++c) g[c] = __expf(z[c] - lse) * tsum - y[c];
+      } else {
+        const bool use = yi != a.ignore_index;
+        float zy = 0.f;
+#pragma unroll
+        for (int c = 0; c < DOUT; ++c) {
+          zy = c == yi ? z[c] : zy;
+          g[c] = use ? __expf(z[c] - lse) - (c == yi ? 1.f : 0.f) : 0.f;
+        }
+        l = use ? lse - zy : 0.f;
+        cnt = use ? 1.f : 0.f;
+      }
+    }
+    if (!valid) {
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) g[c] = 0.f;
+      l = 0.f;
+      cnt = 0.f;
+    }
+  };
+
+  float Gk[DOUT][KP], Gbk[DOUT];
+#pragma unroll
+  for (int c = 0; c < DOUT; ++c) {
+    Gbk[c] = 0.f;
+#pragma unroll
+    for (int k = 0; k < KP; ++k) Gk[c][k] = 0.f;
+  }
+  auto train = [&](Batch<R, KP, DOUT, RY>& f, int step, auto mom_tag) {
+    constexpr bool MOM = decltype(mom_tag)::value;
+    const int nb = f.nb;
+    // ---- forward: partial logits of this feature group
+    float zp[R][DOUT];
+#pragma unroll
+    for (int rho = 0; rho < R; ++rho) {
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) {
+        float acc0 = 0.f, acc1 = 0.f;
+#pragma unroll
+        for (int k = 0; k < KP; k += 2) {
+          acc0 = fmaf(f.x[rho][k], W[c][k], acc0);
+          if (k + 1 < KP) acc1 = fmaf(f.x[rho][k + 1], W[c][k + 1], acc1);
+        }
+        zp[rho][c] = acc0 + acc1;
+      }
+    }
+    tk.tick(1);
+    // ---- logits -> loss -> dL/dz (g[rho][c] in every lane)
+    float g[R][DOUT], lsum, csum;
+    if constexpr (SCATTER) {
+      float z;
+      if constexpr (R == 2) {
+        const float s = rs16(zp[0][0], zp[1][0]);
+        z = rs32(s, s);  // DPP rows {0,2}: batch row 0, {1,3}: batch row 1
+      } else {
+        z = rs32(rs16(zp[0][0], zp[1][0]), rs16(zp[2][0], zp[3][0]));  // DPP row q: batch row q
+      }
+      z += Wb[0];
+      float gz, l, cnt;
+      row_loss(&z, f.y[0], f.yi[0], rho_own * 16 + i < nb, &gz, l, cnt);
+      // each batch row counted once: R == 2 has every row in two DPP rows
+      const bool owner = R == 4 || q < 2;
+      lsum = owner ? l : 0.f;
+      csum = owner ? cnt : 0.f;
+      if constexpr (R == 2) {
+        const F2 r = pl16(gz, gz);  // rows [g0, g0, g0, g0], [g1, g1, g1, g1]
+        g[0][0] = r.a;
+        g[1][0] = r.b;
+      } else {
+        const F2 h = pl32(gz, gz);   // [g0, g1, g0, g1], [g2, g3, g2, g3]
+        const F2 r01 = pl16(h.a, h.a);
+        const F2 r23 = pl16(h.b, h.b);
+        g[0][0] = r01.a;
+        g[1][0] = r01.b;
+        g[2][0] = r23.a;
+        g[3][0] = r23.b;
+      }
+    } else {
+      lsum = 0.f;
+      csum = 0.f;
+#pragma unroll
+      for (int rho = 0; rho < R; ++rho) {
+        float z[DOUT];
+#pragma unroll
+        for (int c = 0; c < DOUT; ++c) z[c] = allrows(zp[rho][c]) + Wb[c];
+        float l, cnt;
+        row_loss(z, f.y[rho], f.yi[rho], rho * 16 + i < nb, g[rho], l, cnt);
+        lsum += l;
+        csum += cnt;
+      }
+      if (q != 0) {  // the 4 DPP rows computed the same rows: count them once
+        lsum = 0.f;
+        csum = 0.f;
+      }
+    }
+    float inv_denom;
+    if constexpr (LOSS == kLossCEIndex) {
+      csum = wave_sum(csum);
+      inv_denom = 1.f / (csum > 0.f ? csum : 1.f);
+    } else {
+      inv_denom = nb == B ? inv_full : inv_last;
+    }
+    const float coef = a.grad_scale * inv_denom;
+    tk.tick(2);
+    // ---- backward: column sums over the 16 row slots of this DPP row
+    float gW[DOUT][KP], gb[DOUT];
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        float t = g[0][c] * f.x[0][k];
+#pragma unroll
+        for (int rho = 1; rho < R; ++rho) t = fmaf(g[rho][c], f.x[rho][k], t);
+        gW[c][k] = row16_sum(t) * coef;
+      }
+      float tb = g[0][c];
+#pragma unroll
+      for (int rho = 1; rho < R; ++rho) tb += g[rho][c];
+      gb[c] = row16_sum(tb) * coef;
+    }
+    tk.tick(3);
+    // ---- all-reduce over ranks: row slot r <-> rank r, summed with the same DPP tree
+    if (AR && !failed) {
+      seq += 1u;
+      const int parity = (int)(seq & 1u);
+      auto slot = [&](uint64_t PTDT_GLOBAL* base, int src, int e) {
+        return base + ((int64_t)(parity * world + src) * max_elems + e);
+      };
+      if (i < world && i != my_rank) {
+#pragma unroll
+        for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+          for (int k = 0; k < KP; ++k)
+            if (k0 + k < Din)
+              __hip_atomic_store(slot(push_dst, my_rank, c * Din + k0 + k),
+                                 ((uint64_t)seq << 32) | (uint64_t)__float_as_uint(gW[c][k]), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+          if (hb && q == 0)
+            __hip_atomic_store(slot(push_dst, my_rank, nW + c),
+                               ((uint64_t)seq << 32) | (uint64_t)__float_as_uint(gb[c]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+      float v[DOUT][KP], vb[DOUT];
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) {
+        vb[c] = i == my_rank ? gb[c] : 0.f;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) v[c][k] = i == my_rank ? gW[c][k] : 0.f;
+      }
+      if (i < world && i != my_rank) {
+        uint32_t polls = 0;
+        while (true) {
+          bool all = true;
+#pragma unroll
+          for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+            for (int k = 0; k < KP; ++k) {
+              if (k0 + k < Din) {
+                const uint64_t w = __hip_atomic_load(slot(poll_src, i, c * Din + k0 + k), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_SYSTEM);
+                all &= (uint32_t)(w >> 32) == seq;
+                v[c][k] = __uint_as_float((uint32_t)w);
+              }
+            }
+            if (hb) {
+              const uint64_t w =
+                  __hip_atomic_load(slot(poll_src, i, nW + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              all &= (uint32_t)(w >> 32) == seq;
+              vb[c] = __uint_as_float((uint32_t)w);
+            }
+          }
+          if (all) break;
+          if (++polls > kXgmiMaxPolls) {
+            __hip_atomic_store((int PTDT_GLOBAL*)ar.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            failed = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      failed = __any(failed);
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+        for (int k = 0; k < KP; ++k) gW[c][k] = row16_sum(v[c][k]) * inv_w;
+        gb[c] = row16_sum(vb[c]) * inv_w;
+      }
+    }
+    tk.tick(4);
+    // ---- SGD on this lane's feature group (MOM: momentum on; the caller
+    // instantiates the whole step loop per value, so no per-step branch)
+    const bool first = opt_step == 0;
+    auto upd = [&](float& w, float& m, float gr) {
+      float d = fmaf(wd, w, gr);
+      if constexpr (MOM) {
+        const float buf = first ? d : fmaf(mu, m, (1.f - damp) * d);
+        m = buf;
+        d = nesterov ? fmaf(mu, buf, d) : buf;
+      }
+      w = fmaf(-lr, d, w);
+    };
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) upd(W[c][k], M[c][k], gW[c][k]);
+      upd(Wb[c], Mb[c], gb[c]);
+      Wb[c] = hb ? Wb[c] : 0.f;
+    }
+    ++opt_step;
+    // the DDP bucket (a.G) keeps the last step's averaged gradients: register
+    // copies here (the unrolled loop keeps only the last), one store at the end
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) Gk[c][k] = gW[c][k];
+      Gbk[c] = gb[c];
+    }
+    // ---- loss report: row sums by DPP, the 4 DPP rows by two swaps
+    const float ls = allrows(row16_sum(lsum));
+    if constexpr (LOSS == kLossCEIndex) losses[step] = csum > 0.f ? ls * inv_denom : NAN;
+    else losses[step] = ls * inv_denom;
+    tk.tick(5);
+  };
+
+  Batch<R, KP, DOUT, RY> buf[kNB];
+  tk.start();
+  read_index();
+#pragma unroll
+  for (int u = 0; u < kNB; ++u) fetch(buf[u]);
+  tk.tick(0);
+  int done = 0;
+  const int nfull = n - n % kNB;
+  auto run = [&](auto mom_tag) {
+    while (done < nfull && !failed) {
+#pragma unroll
+      for (int u = 0; u < kNB; ++u) {
+        train(buf[u], done + u, mom_tag);
+        fetch(buf[u]);
+        tk.tick(0);
+      }
+      done += kNB;
+    }
+#pragma unroll
+    for (int u = 0; u < kNB - 1; ++u) {
+      if (done < n && !failed) {
+        train(buf[u], done, mom_tag);
+        ++done;
+      }
+    }
+  };
+  if (use_mom) run(std::true_type{});
+  else run(std::false_type{});
+  while (barriers < T) {
+    __syncthreads();
+    ++barriers;
+  }
+
+  if (i == 0) {
+    const auto Pw = gptr_w(a.P);
+    const auto Gw = gptr_w(a.G);
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        if (k0 + k < Din) {
+          Pw[c * Din + k0 + k] = W[c][k];
+          if (done > 0) Gw[c * Din + k0 + k] = Gk[c][k];
+          if (use_mom) a.mom[c * Din + k0 + k] = M[c][k];
+        }
+      }
+      if (hb && q == 0) {
+        Pw[nW + c] = Wb[c];
+        if (done > 0) Gw[nW + c] = Gbk[c];
+        if (use_mom) a.mom[nW + c] = Mb[c];
+      }
+    }
+  }
+  if (lane == 0) {
+    const int64_t pos = pos0 + done;
+    pa.cursor[0] = (int)(pos / S);
+    pa.cursor[1] = (int)(pos % S);
+    if (a.opt_step) *a.opt_step = opt_step;
+    if (AR) *ar.seq = seq;
+    if (tk.on) {
+      for (int k = 0; k < 6; ++k) pa.stamps[k] += (int64_t)tk.acc[k];
+      pa.stamps[7] += (int64_t)__builtin_amdgcn_s_memtime() - t_begin;
+      pa.stamps[8] += (int64_t)__builtin_amdgcn_s_memrealtime() - r_begin;
+    }
+  }
+}
+
 // Instantiation table of one loss and all-reduce flag: (L, R, KP, DOUT)
 // combinations whose register footprint fits (no scratch). nullptr otherwise.
 // Keep in sync with kWaveConfigs in linear_wave.hip.
+// L == 0 selects layout F (linear_wave_f_kernel), R in {1, 2, 4}.
 template <int LOSS, bool AR>
 const void* pick(int L, int R, int kp, int dout) {
+#define PTDT_LWF(RR, KP, DO) \
+  if (L == 0 && R == RR && kp == KP && dout == DO) return (const void*)linear_wave_f_kernel<RR, KP, DO, LOSS, AR>;
+#define PTDT_LWF_R(RR)                                                                             \
+  PTDT_LWF(RR, 4, 1) PTDT_LWF(RR, 5, 1) PTDT_LWF(RR, 8, 1) PTDT_LWF(RR, 10, 1) PTDT_LWF(RR, 16, 1) \
+  PTDT_LWF(RR, 4, 2) PTDT_LWF(RR, 5, 2) PTDT_LWF(RR, 8, 2)
+  PTDT_LWF_R(1) PTDT_LWF_R(2) PTDT_LWF_R(4)
+#undef PTDT_LWF_R
+#undef PTDT_LWF
 #define PTDT_LW(LL, RR, KP, DO) \
   if (L == LL && R == RR && kp == KP && dout == DO) return (const void*)linear_wave_kernel<LL, RR, KP, DO, LOSS, AR>;
 #define PTDT_LW_LR(LL, RR)                                                                    \

@@ -92,7 +92,10 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         obj = BUILD / (src.stem + ".o")
         objs.append(obj)
         if force or _newer(src, obj, hdrs):
-            todo.append([hipcc, *common, "-c", str(src), "-o", str(obj)])
+            # single-wave engine: no SLP vectorisation -- it splits DPP adds into
+            # v_mov_dpp + v_pk_add pairs (plus zero-inits), ~50 extra VALU per step
+            extra = ["-fno-slp-vectorize"] if src.stem.startswith("linear_wave") else []
+            todo.append([hipcc, *common, *extra, "-c", str(src), "-o", str(obj)])
     for src in hosts:
         obj = BUILD / (src.stem + ".host.o")
         objs.append(obj)

@@ -46,7 +46,7 @@ def _linears(model: nn.Module):
     raise ValueError("FusedMLPStep supports Linear or Linear-ReLU-Linear models; use the autograd engine otherwise")
 
 
-_VARIANTS = {"auto": 0, "workgroup": 1, "wave": 2}
+_VARIANTS = {"auto": 0, "workgroup": 1, "wave": 2, "wave_rows": 3, "wave_f": 4}
 
 
 def _variant_id(variant: str | None) -> int:
@@ -181,7 +181,7 @@ class FusedMLPStep:
         if not eng.startswith("wave"):
             return X, False
         lanes, kp = int(eng.split("L")[1].split("R")[0]), int(eng.split("K")[1])
-        width = lanes * kp
+        width = (lanes or 4) * kp  # L0: layout F, 4 feature groups
         if width <= self.Din:
             return X, False
         key = (X.data_ptr(), X._version, tuple(X.shape), width)

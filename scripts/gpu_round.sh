@@ -41,6 +41,8 @@ for s in $STAGES; do
            step prof_fused_rccl 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_fused_rccl -o run -- python3 bench.py --engine fused --steps 500 --warmup 64 --allreduce rccl
            step prof_mlp 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_mlp -o run -- python3 bench.py --model mlp --steps 500 --warmup 64
            step prof_reference 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_reference -o run -- python3 bench.py --engine reference --steps 200 --warmup 20 ;;
+    pmc)   step pmc_list 120 rocprofv3 -L
+           step pmc_wave 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAIT_INST_ANY SQ_BUSY_CYCLES --kernel-trace --stats --output-format csv -d gpurun_out/pmc_wave -o run -- python3 bench.py --steps 8192 --warmup 64 ;;
   esac
 done
 echo "=== done"

@@ -247,13 +247,15 @@ def persistent_two_procs_one_gpu(rank, world, port, out_dir, kind="mlp"):
         # instantiated, so use Linear(20, 2))
         model = ToyMLP(20, 16, 4) if kind == "mlp" else torch.nn.Linear(20, 2)
         eng = FusedMLPStep(model.to(dev), loss="ce_index", lr=0.05, momentum=0.9, xgmi=xg)
+        variant = "wave_rows" if kind == "linear_rows" else None
         if mode == "persistent":
-            out["engine"] = eng.persistent_engine(16, DeviceDistributedSampler(300, world, rank, seed=3, device=dev))
+            out["engine"] = eng.persistent_engine(16, DeviceDistributedSampler(300, world, rank, seed=3, device=dev),
+                                                  variant)
         sampler = DeviceDistributedSampler(300, world, rank, seed=3, device=dev)
         if mode == "persistent":
             cursor = torch.zeros(2, dtype=torch.int32, device=dev)
             losses = torch.zeros(7, device=dev)
-            eng.run_persistent(X, Y, 23, 16, sampler, cursor, losses, max_steps_per_launch=7)
+            eng.run_persistent(X, Y, 23, 16, sampler, cursor, losses, max_steps_per_launch=7, variant=variant)
             torch.cuda.synchronize()
             out["cursor"] = cursor.cpu()
         else:

@@ -136,8 +136,9 @@ def test_persistent_engine_selection():
     workgroup engine."""
     C = native()
     ce_soft, ce_index = 0, 1
-    # flagship toy: 4 lanes per row, 2 rows per lane group, 5 features per lane (cost model)
-    assert C.persistent_engine(32, 20, 0, 1, ce_soft, 2048, 1) == "wave:L4R2K5"
+    # flagship toy: layout F (4 feature groups x 16 row slots), 2 rows per slot, 5 features per lane
+    assert C.persistent_engine(32, 20, 0, 1, ce_soft, 2048, 1) == "wave:L0R2K5"
+    assert C.persistent_engine(32, 20, 0, 1, ce_soft, 2048, 1, 3) == "wave:L4R2K5"  # row-group layouts only
     assert C.persistent_engine(32, 20, 0, 1, ce_soft, 256, 8).startswith("wave")  # 8 ranks
     assert C.persistent_engine(64, 16, 0, 1, ce_soft, 1000, 1).startswith("wave")
     assert C.persistent_engine(32, 20, 64, 10, ce_index, 2048, 1) == "workgroup"  # hidden layer
