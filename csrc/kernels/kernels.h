@@ -72,7 +72,8 @@ struct PersistArgs {
   float* losses;         // [n_steps] per-step mean loss
   int64_t* stamps;       // optional [9] diagnostic phase timers (s_memtime cycles, thread 0): prefetch issue,
                          // forward, loss, backward, all-reduce, sgd+land, epoch indices, total, realtime (100 MHz)
-  int variant;           // kPersistAuto / kPersistWorkgroup / kPersistWave
+  int variant;           // kPersistAuto / kPersistWorkgroup / kPersistWave...
+  int loss_ring;         // set by the launcher: the wave engine reduces losses in helper waves
 };
 // Engine choice: the register-resident single-wave engine (linear_wave.hip) runs
 // Linear(Din, Dout) models with B <= 64 and small Dout; everything else runs the
@@ -80,6 +81,7 @@ struct PersistArgs {
 // it supports the configuration.
 // kPersistWaveRows / kPersistWaveF restrict the wave engine to one lane-layout
 // family (row groups across DPP rows / feature groups across DPP rows).
+constexpr int kWavePrefetch = 3;  // batches in flight in the wave engine (register buffers)
 enum PersistVariant : int {
   kPersistAuto = 0, kPersistWorkgroup = 1, kPersistWave = 2, kPersistWaveRows = 3, kPersistWaveF = 4
 };

@@ -16,6 +16,11 @@ constexpr int kThreads = 256;  // wave 0 trains, waves 1-3 build index lists
 size_t lds_bytes(const PersistArgs& p) {  // two epoch index lists + 8 phase-timer slots
   return (size_t)2 * al4(p.num_samples) * sizeof(int) + 8 * sizeof(unsigned long long);
 }
+// loss ring of layout F: (2 epochs + prefetch depth) steps x 64 lane shares
+size_t ring_bytes(const FusedMlpArgs& a, const PersistArgs& p) {
+  const int S = (p.num_samples + a.B - 1) / a.B;
+  return (size_t)(2 * S + kWavePrefetch) * 64 * sizeof(float);
+}
 
 const void* pick(int loss, bool ar, int L, int R, int kp, int dout) {
   switch (loss) {
@@ -72,6 +77,7 @@ Choice choose(const FusedMlpArgs& a, const PersistArgs& p) {
     const int lanes = L == 0 ? 4 : L;            // feature chunks per row
     const int groups = L == 0 ? 16 : 64 / L;     // row slots
     if (groups * R < a.B) continue;              // rows must fit one pass
+    if (L == 0 && (int64_t)p.N * ldx >= (1ll << 32)) continue;  // layout F gathers with 32-bit offsets
     if (ar && groups < a.ar.world) continue;     // one row slot per rank
     const int need = (a.Din + lanes - 1) / lanes;
     int kp = -1;
@@ -106,12 +112,19 @@ void linear_wave_layout(const FusedMlpArgs& a, const PersistArgs& p, int* L, int
 }
 
 hipError_t linear_wave_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s) {
-  const void* fn = choose(a, p).fn;
+  const Choice c = choose(a, p);
+  const void* fn = c.fn;
   if (fn == nullptr) return hipErrorInvalidValue;
-  const size_t lds = lds_bytes(p);
+  PersistArgs pr = p;
+  size_t lds = lds_bytes(p);
+  pr.loss_ring = 0;
+  if (c.L == 0 && lds + ring_bytes(a, p) <= 160 * 1024) {
+    pr.loss_ring = 1;
+    lds += ring_bytes(a, p);
+  }
   if (lds > 64 * 1024)
     PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  void* args[] = {const_cast<FusedMlpArgs*>(&a), const_cast<PersistArgs*>(&p)};
+  void* args[] = {const_cast<FusedMlpArgs*>(&a), &pr};
   return hipLaunchKernel(fn, dim3(1), dim3(kThreads), args, lds, s);
 }
 

@@ -41,7 +41,7 @@
 namespace ptdt {
 namespace lw {
 
-constexpr int kNB = 3;           // batches in flight (register buffers)
+constexpr int kNB = kWavePrefetch;  // batches in flight (register buffers)
 constexpr int kThreads = 256;    // wave 0 trains, waves 1-3 build index lists
 
 __device__ __forceinline__ float swap16_add(float v) {
@@ -661,18 +661,42 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   const int T = (int)((pos0 + n - 1) / S - pos0 / S);
   auto list = [&](int e) { return elist + (e & 1) * estride; };
 
+  // Both lists are built even when the launch stays in one epoch: the trainer
+  // reads (stale but valid) indices for the kNB positions past its last step,
+  // so every list entry it can touch is a valid dataset row (no clamp per load).
   rank_epoch_indices(list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
                      (int)threadIdx.x, kThreads);
-  if (T > 0)
-    rank_epoch_indices(list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1, pa.shuffle,
-                       (int)threadIdx.x, kThreads);
+  rank_epoch_indices(list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1, pa.shuffle,
+                     (int)threadIdx.x, kThreads);
+  // Loss ring (pa.loss_ring): the trainer stores each lane's scaled loss share
+  // per step (one ds_write), the helper waves add the 64 shares and write
+  // losses[] -- the per-step cross-lane loss reduction leaves the critical path.
+  const int ring = pa.loss_ring ? 2 * S + kNB : 0;  // slots; 2 epochs + prefetch depth never overwrite unread
+  float* const lring = reinterpret_cast<float*>(elist + 2 * estride + 16);  // after the 8 u64 timer slots
   __syncthreads();
   if (wave != 0) {
+    const int ht = (int)threadIdx.x - 64, hn = kThreads - 64;
+    int64_t lo = pos0;
+    auto reduce_losses = [&](int64_t hi) {  // positions [lo, hi): sum the 64 shares in lane order
+      for (int64_t P = lo + ht; P < hi; P += hn) {
+        const float* sh = lring + (int)((P - pos0) % ring) * 64;
+        float acc = 0.f;
+        for (int l = 0; l < 64; ++l) acc += sh[l];
+        pa.losses[P - pos0] = acc;
+      }
+      lo = hi > lo ? hi : lo;
+    };
     for (int i = 1; i <= T; ++i) {
       __syncthreads();
       if (i < T)
         rank_epoch_indices(list(e0 + i + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + i + 1,
-                           pa.shuffle, (int)threadIdx.x - 64, kThreads - 64);
+                           pa.shuffle, ht, hn);
+      // at barrier i the trainer has trained every position before (e0+i)*S - kNB
+      if (ring) reduce_losses(min((int64_t)(e0 + i) * S - kNB, pos0 + n));
+    }
+    if (ring) {
+      __syncthreads();  // the trainer's final barrier: every step done
+      reduce_losses(pos0 + n);
     }
     return;
   }
@@ -718,7 +742,6 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   bool failed = AR && *ar.err != 0;
   const float inv_w = 1.f / (float)world;
 
-  const uint32_t N = (uint32_t)pa.N;
   int ie = e0, ij = j0, barriers = 0;
   int sel_next[R], sel_y_next = 0, nb_next = 0;
   auto read_index = [&]() {
@@ -728,14 +751,9 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     }
     nb_next = min(B, pa.num_samples - ij * B);
 #pragma unroll
-    for (int rho = 0; rho < R; ++rho) {
-      const int sel = list(ie)[ij * B + min(rho * 16 + i, nb_next - 1)];
-      sel_next[rho] = (uint32_t)sel < N ? sel : 0;
-    }
-    if constexpr (SCATTER) {  // own row's index read directly: selecting from sel_next[] by a lane
-      const int sel = list(ie)[ij * B + min(rho_own * 16 + i, nb_next - 1)];  // value spills it
-      sel_y_next = (uint32_t)sel < N ? sel : 0;
-    }
+    for (int rho = 0; rho < R; ++rho) sel_next[rho] = list(ie)[ij * B + min(rho * 16 + i, nb_next - 1)];
+    if constexpr (SCATTER)  // own row's index read directly: selecting from sel_next[] by a lane value spills it
+      sel_y_next = list(ie)[ij * B + min(rho_own * 16 + i, nb_next - 1)];
     if (++ij == S) {
       ij = 0;
       ++ie;
@@ -745,7 +763,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     f.nb = nb_next;
 #pragma unroll
     for (int rho = 0; rho < R; ++rho) {
-      const auto xr = X + (int64_t)sel_next[rho] * ldx + k0;
+      const auto xr = X + ((uint32_t)sel_next[rho] * (uint32_t)ldx + (uint32_t)k0);  // 32-bit offset (host-checked)
 #pragma unroll
       for (int k = 0; k < KP; ++k) f.x[rho][k] = xr[k];
     }
@@ -838,8 +856,10 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
 #pragma unroll
     for (int k = 0; k < KP; ++k) Gk[c][k] = 0.f;
   }
-  auto train = [&](Batch<R, KP, DOUT, RY>& f, int step, auto mom_tag) {
+  int rslot = 0;  // loss ring slot of the next step
+  auto train = [&](Batch<R, KP, DOUT, RY>& f, int step, auto mom_tag, auto ring_tag) {
     constexpr bool MOM = decltype(mom_tag)::value;
+    constexpr bool RING = decltype(ring_tag)::value;
     const int nb = f.nb;
     // ---- forward: partial logits of this feature group
     float zp[R][DOUT];
@@ -874,6 +894,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
       const bool owner = R == 4 || q < 2;
       lsum = owner ? l : 0.f;
       csum = owner ? cnt : 0.f;
+      if constexpr (LOSS != kLossCEIndex) gz *= a.grad_scale * (nb == B ? inv_full : inv_last);  // 1/B once
       if constexpr (R == 2) {
         const F2 r = pl16(gz, gz);  // rows [g0, g0, g0, g0], [g1, g1, g1, g1]
         g[0][0] = r.a;
@@ -912,7 +933,8 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     } else {
       inv_denom = nb == B ? inv_full : inv_last;
     }
-    const float coef = a.grad_scale * inv_denom;
+    // SCATTER already applied the scale to dL/dz before the all-gather
+    const float coef = (SCATTER && LOSS != kLossCEIndex) ? 1.f : a.grad_scale * inv_denom;
     tk.tick(2);
     // ---- backward: column sums over the 16 row slots of this DPP row
     float gW[DOUT][KP], gb[DOUT];
@@ -923,12 +945,12 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
         float t = g[0][c] * f.x[0][k];
 #pragma unroll
         for (int rho = 1; rho < R; ++rho) t = fmaf(g[rho][c], f.x[rho][k], t);
-        gW[c][k] = row16_sum(t) * coef;
+        gW[c][k] = (SCATTER && LOSS != kLossCEIndex) ? row16_sum(t) : row16_sum(t) * coef;
       }
       float tb = g[0][c];
 #pragma unroll
       for (int rho = 1; rho < R; ++rho) tb += g[rho][c];
-      gb[c] = row16_sum(tb) * coef;
+      gb[c] = (SCATTER && LOSS != kLossCEIndex) ? row16_sum(tb) : row16_sum(tb) * coef;
     }
     tk.tick(3);
     // ---- all-reduce over ranks: row slot r <-> rank r, summed with the same DPP tree
@@ -1028,10 +1050,16 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
       for (int k = 0; k < KP; ++k) Gk[c][k] = gW[c][k];
       Gbk[c] = gb[c];
     }
-    // ---- loss report: row sums by DPP, the 4 DPP rows by two swaps
-    const float ls = allrows(row16_sum(lsum));
-    if constexpr (LOSS == kLossCEIndex) losses[step] = csum > 0.f ? ls * inv_denom : NAN;
-    else losses[step] = ls * inv_denom;
+    // ---- loss report
+    if constexpr (RING) {  // this lane's share; the helper waves add the 64 shares
+      const float share = (LOSS == kLossCEIndex && !(csum > 0.f)) ? NAN : lsum * inv_denom;
+      lring[rslot * 64 + lane] = share;
+      rslot = rslot + 1 == ring ? 0 : rslot + 1;
+    } else {  // row sums by DPP, the 4 DPP rows by two swaps
+      const float ls = allrows(row16_sum(lsum));
+      if constexpr (LOSS == kLossCEIndex) losses[step] = csum > 0.f ? ls * inv_denom : NAN;
+      else losses[step] = ls * inv_denom;
+    }
     tk.tick(5);
   };
 
@@ -1043,11 +1071,11 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   tk.tick(0);
   int done = 0;
   const int nfull = n - n % kNB;
-  auto run = [&](auto mom_tag) {
+  auto run = [&](auto mom_tag, auto ring_tag) {
     while (done < nfull && !failed) {
 #pragma unroll
       for (int u = 0; u < kNB; ++u) {
-        train(buf[u], done + u, mom_tag);
+        train(buf[u], done + u, mom_tag, ring_tag);
         fetch(buf[u]);
         tk.tick(0);
       }
@@ -1056,17 +1084,24 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
 #pragma unroll
     for (int u = 0; u < kNB - 1; ++u) {
       if (done < n && !failed) {
-        train(buf[u], done, mom_tag);
+        train(buf[u], done, mom_tag, ring_tag);
         ++done;
       }
     }
   };
-  if (use_mom) run(std::true_type{});
-  else run(std::false_type{});
+  // one loop instantiation per (momentum, loss ring): no per-step branch on either
+  if (use_mom) {
+    if (ring) run(std::true_type{}, std::true_type{});
+    else run(std::true_type{}, std::false_type{});
+  } else {
+    if (ring) run(std::false_type{}, std::true_type{});
+    else run(std::false_type{}, std::false_type{});
+  }
   while (barriers < T) {
     __syncthreads();
     ++barriers;
   }
+  if (ring) __syncthreads();  // final barrier: the helpers reduce the remaining losses
 
   if (i == 0) {
     const auto Pw = gptr_w(a.P);
