@@ -18,7 +18,9 @@ STAGES=${STAGES:-"tests smoke bench prof"}
 for s in $STAGES; do
   case $s in
     tests) step pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
-    micro) step microbench 120 tools/bin/microbench_launch ;;
+    micro) step microbench 120 tools/bin/microbench_launch
+           step microbench_isa 120 tools/bin/microbench_isa ;;
+    xgmi)  step xgmi_latency 300 python benchmarks/xgmi_step_latency.py --steps 20000 ;;
     quick) step bench_persistent 300 python bench.py --steps 20000 --warmup 2000 --stamps
            step bench_persistent_wg 300 python bench.py --steps 20000 --warmup 2000 --stamps --persist workgroup
            step bench_mlp 300 python bench.py --model mlp --steps 20000 --warmup 2000 --stamps
