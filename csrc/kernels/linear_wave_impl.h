@@ -113,6 +113,69 @@ struct Ticks {
   }
 };
 
+// One-shot LL exchange of one lane's gradient chunk (csrc/comm/xgmi.h protocol):
+// push the chunk to rank `peer` (when `active`), then poll rank `peer`'s chunk in
+// this rank's buffer. Chunk elements: c*Din + k0 + k (k < KP, real when
+// k0 + k < Din) and the biases nW + c. Every poll load is unconditional (padded
+// slots re-read a real slot and are zeroed afterwards): loads under per-slot exec
+// masks were issued one round trip at a time. Returns false after a poll timeout.
+template <int KP, int DOUT>
+__device__ __forceinline__ bool ll_exchange(bool active, uint64_t PTDT_GLOBAL* push_base,
+                                            uint64_t PTDT_GLOBAL* poll_base, int my_rank, int peer, int world,
+                                            int max_elems, uint32_t seq, int k0, int Din, bool hb, bool bias_lane,
+                                            bool padded, const float (&gW)[DOUT][KP], const float (&gb)[DOUT],
+                                            float (&v)[DOUT][KP], float (&vb)[DOUT], int* err) {
+  const int parity = (int)(seq & 1u);
+  const int nW = DOUT * Din;
+  const uint64_t hi = (uint64_t)seq << 32;
+  if (!active) return true;
+  uint64_t PTDT_GLOBAL* const dst = push_base + (int64_t)(parity * world + my_rank) * max_elems;
+  uint64_t PTDT_GLOBAL* const src = poll_base + (int64_t)(parity * world + peer) * max_elems;
+  if (!padded) {
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c)
+#pragma unroll
+      for (int k = 0; k < KP; ++k)
+        __hip_atomic_store(dst + c * Din + k0 + k, hi | __float_as_uint(gW[c][k]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c)
+#pragma unroll
+      for (int k = 0; k < KP; ++k)
+        if (k0 + k < Din)
+          __hip_atomic_store(dst + c * Din + k0 + k, hi | __float_as_uint(gW[c][k]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (hb && bias_lane)
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c)
+      __hip_atomic_store(dst + nW + c, hi | __float_as_uint(gb[c]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (uint32_t polls = 0;; ++polls) {
+    bool all = true;
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        const int e = c * Din + min(k0 + k, Din - 1);
+        const uint64_t w = __hip_atomic_load(src + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        all &= (uint32_t)(w >> 32) == seq;
+        v[c][k] = k0 + k < Din ? __uint_as_float((uint32_t)w) : 0.f;
+      }
+      // no bias: re-read element 0 (a real slot of this exchange) instead of branching
+      const uint64_t w = __hip_atomic_load(src + (hb ? nW + c : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      all &= (uint32_t)(w >> 32) == seq;
+      vb[c] = hb ? __uint_as_float((uint32_t)w) : 0.f;
+    }
+    if (all) return true;
+    if (polls >= kXgmiMaxPolls) {  // a peer is gone: fail loudly, never hang
+      __hip_atomic_store((int PTDT_GLOBAL*)err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
 template <int R, int KP, int DOUT, int RY>
 struct Batch {
   float x[R][KP];
@@ -412,64 +475,17 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
     // ---- all-reduce over ranks (average): row group q <-> rank q
     if (AR && !failed) {
       seq += 1u;
-      const int parity = (int)(seq & 1u);
-      auto slot = [&](uint64_t PTDT_GLOBAL* base, int src, int i) {
-        return base + ((int64_t)(parity * world + src) * max_elems + i);
-      };
-      if (j < world && j != my_rank) {
-        uint64_t PTDT_GLOBAL* dst = push_dst;
-#pragma unroll
-        for (int c = 0; c < DOUT; ++c) {
-#pragma unroll
-          for (int k = 0; k < KP; ++k)
-            if (k0 + k < Din)
-              __hip_atomic_store(slot(dst, my_rank, c * Din + k0 + k),
-                                 ((uint64_t)seq << 32) | (uint64_t)__float_as_uint(gW[c][k]), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_SYSTEM);
-          if (hb && p == 0)
-            __hip_atomic_store(slot(dst, my_rank, nW + c), ((uint64_t)seq << 32) | (uint64_t)__float_as_uint(gb[c]),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
       float v[DOUT][KP], vb[DOUT];
 #pragma unroll
-      for (int c = 0; c < DOUT; ++c) {
+      for (int c = 0; c < DOUT; ++c) {  // own contribution from registers, rows >= world add 0
         vb[c] = j == my_rank ? gb[c] : 0.f;
 #pragma unroll
         for (int k = 0; k < KP; ++k) v[c][k] = j == my_rank ? gW[c][k] : 0.f;
       }
-      if (j < world && j != my_rank) {
-        // all slots of the chunk in flight together; re-poll until every seq matches
-        uint32_t polls = 0;
-        while (true) {
-          bool all = true;
-#pragma unroll
-          for (int c = 0; c < DOUT; ++c) {
-#pragma unroll
-            for (int k = 0; k < KP; ++k) {
-              if (k0 + k < Din) {
-                const uint64_t w = __hip_atomic_load(slot(poll_src, j, c * Din + k0 + k), __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_SYSTEM);
-                all &= (uint32_t)(w >> 32) == seq;
-                v[c][k] = __uint_as_float((uint32_t)w);
-              }
-            }
-            if (hb) {
-              const uint64_t w =
-                  __hip_atomic_load(slot(poll_src, j, nW + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              all &= (uint32_t)(w >> 32) == seq;
-              vb[c] = __uint_as_float((uint32_t)w);
-            }
-          }
-          if (all) break;
-          if (++polls > kXgmiMaxPolls) {  // a peer is gone: fail loudly, never hang
-            __hip_atomic_store((int PTDT_GLOBAL*)ar.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            failed = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
+      const bool ok = ll_exchange<KP, DOUT>(j < world && j != my_rank, push_dst, poll_src, my_rank, j, world,
+                                            max_elems, seq, k0, Din, hb, p == 0, L * KP != Din, gW, gb, v, vb,
+                                            ar.err);
+      failed = !ok;
       failed = __any(failed);
 #pragma unroll
       for (int c = 0; c < DOUT; ++c) {
@@ -956,63 +972,17 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     // ---- all-reduce over ranks: row slot r <-> rank r, summed with the same DPP tree
     if (AR && !failed) {
       seq += 1u;
-      const int parity = (int)(seq & 1u);
-      auto slot = [&](uint64_t PTDT_GLOBAL* base, int src, int e) {
-        return base + ((int64_t)(parity * world + src) * max_elems + e);
-      };
-      if (i < world && i != my_rank) {
-#pragma unroll
-        for (int c = 0; c < DOUT; ++c) {
-#pragma unroll
-          for (int k = 0; k < KP; ++k)
-            if (k0 + k < Din)
-              __hip_atomic_store(slot(push_dst, my_rank, c * Din + k0 + k),
-                                 ((uint64_t)seq << 32) | (uint64_t)__float_as_uint(gW[c][k]), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_SYSTEM);
-          if (hb && q == 0)
-            __hip_atomic_store(slot(push_dst, my_rank, nW + c),
-                               ((uint64_t)seq << 32) | (uint64_t)__float_as_uint(gb[c]), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      }
       float v[DOUT][KP], vb[DOUT];
 #pragma unroll
-      for (int c = 0; c < DOUT; ++c) {
+      for (int c = 0; c < DOUT; ++c) {  // own contribution from registers, slots >= world add 0
         vb[c] = i == my_rank ? gb[c] : 0.f;
 #pragma unroll
         for (int k = 0; k < KP; ++k) v[c][k] = i == my_rank ? gW[c][k] : 0.f;
       }
-      if (i < world && i != my_rank) {
-        uint32_t polls = 0;
-        while (true) {
-          bool all = true;
-#pragma unroll
-          for (int c = 0; c < DOUT; ++c) {
-#pragma unroll
-            for (int k = 0; k < KP; ++k) {
-              if (k0 + k < Din) {
-                const uint64_t w = __hip_atomic_load(slot(poll_src, i, c * Din + k0 + k), __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_SYSTEM);
-                all &= (uint32_t)(w >> 32) == seq;
-                v[c][k] = __uint_as_float((uint32_t)w);
-              }
-            }
-            if (hb) {
-              const uint64_t w =
-                  __hip_atomic_load(slot(poll_src, i, nW + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              all &= (uint32_t)(w >> 32) == seq;
-              vb[c] = __uint_as_float((uint32_t)w);
-            }
-          }
-          if (all) break;
-          if (++polls > kXgmiMaxPolls) {
-            __hip_atomic_store((int PTDT_GLOBAL*)ar.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            failed = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
+      const bool ok = ll_exchange<KP, DOUT>(i < world && i != my_rank, push_dst, poll_src, my_rank, i, world,
+                                            max_elems, seq, k0, Din, hb, q == 0, 4 * KP != Din, gW, gb, v, vb,
+                                            ar.err);
+      failed = !ok;
       failed = __any(failed);
 #pragma unroll
       for (int c = 0; c < DOUT; ++c) {

@@ -96,6 +96,29 @@ __global__ void __launch_bounds__(64) k_chase(const int* tab, int* out, long lon
   if (threadIdx.x == 0) cyc[0] = t1 - t0;
 }
 
+// dependent system-scope (L2-bypassing) loads, as the all-reduce polls issue them
+__global__ void __launch_bounds__(64) k_chase_sys(int* tab, int* out, long long* cyc, int iters) {
+  int i = threadIdx.x;
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  for (int t = 0; t < iters; ++t) i = __hip_atomic_load(tab + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  out[threadIdx.x] = i;
+  if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+
+// store a new value, spin until a system-scope load returns it
+__global__ void __launch_bounds__(64) k_store_visible(int* buf, long long* cyc, int iters) {
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  for (int t = 1; t <= iters; ++t) {
+    __hip_atomic_store(buf + threadIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    int spins = 0;
+    while (__hip_atomic_load(buf + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != t && ++spins < 100000) {
+    }
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  if (threadIdx.x == 0) cyc[0] = t1 - t0;
+}
+
 template <int OP>
 int run_op(float* out, long long* dcyc) {
   const int iters = 1024;
@@ -146,6 +169,32 @@ int main() {
     CK(hipMemcpy(&c, dcyc, 8, hipMemcpyDeviceToHost));
   }
   std::printf("%-32s latency %6.2f cycles\n", "global_load (L2 hit, 1 MiB walk)", (double)c / 4096);
+  // polling memory of the one-shot all-reduce: uncached and fine-grained allocations
+  // (64-entry table, so a cacheable allocation would hit L1)
+  for (int kind = 0; kind < 2; ++kind) {
+    int* t2;
+    CK(hipExtMallocWithFlags((void**)&t2, 64 * sizeof(int),
+                             kind == 0 ? hipDeviceMallocUncached : hipDeviceMallocFinegrained));
+    CK(hipMemcpy(t2, h, sizeof(h), hipMemcpyHostToDevice));
+    for (int rep = 0; rep < 2; ++rep) {
+      hipLaunchKernelGGL(k_chase_sys, dim3(1), dim3(64), 0, 0, t2, iout, dcyc, 1024);
+      CK(hipMemcpy(&c, dcyc, 8, hipMemcpyDeviceToHost));
+    }
+    std::printf("%-32s latency %6.2f cycles\n", kind == 0 ? "system-scope load, uncached mem" : "system-scope load, fine-grained",
+                (double)c / 1024);
+    CK(hipFree(t2));
+  }
+  {  // store -> visible to a system-scope load of the same wave (write round trip on uncached memory)
+    int* t3;
+    CK(hipExtMallocWithFlags((void**)&t3, 64 * sizeof(int), hipDeviceMallocUncached));
+    CK(hipMemset(t3, 0, 64 * sizeof(int)));
+    for (int rep = 0; rep < 2; ++rep) {
+      hipLaunchKernelGGL(k_store_visible, dim3(1), dim3(64), 0, 0, t3, dcyc, 1024);
+      CK(hipMemcpy(&c, dcyc, 8, hipMemcpyDeviceToHost));
+    }
+    std::printf("%-32s latency %6.2f cycles\n", "store->load seen, uncached mem", (double)c / 1024);
+    CK(hipFree(t3));
+  }
   CK(hipDeviceSynchronize());
   return 0;
 }
