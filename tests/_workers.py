@@ -288,3 +288,22 @@ def fingerprint_check(rank, world, port, out_dir, diverge):
         res["msg"] = str(e)
     torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
     destroy_process_group()
+
+
+def bucket_all_reduce(rank, world, port, out_dir, numel):
+    _init(rank, world, port)
+    from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+
+    c = comm_mod.get_default()
+    t = torch.full((numel,), float(rank + 1))
+    t[-1] = rank * 2.0
+    c.all_reduce(t, "avg")
+    expect = sum(range(1, world + 1)) / world
+    b = torch.full((numel,), float(rank))
+    c.broadcast(b, world - 1)
+    res = {"avg_ok": bool(torch.allclose(t[:-1], torch.full((numel - 1,), expect))) and
+           abs(float(t[-1]) - sum(2.0 * r for r in range(world)) / world) < 1e-6,
+           "avg0": float(t[0]), "bcast_ok": bool((b == world - 1).all())}
+    torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
+    destroy_process_group()

@@ -86,3 +86,15 @@ def test_collective_fingerprint_check(tmp_path, diverge):
         assert not any(r["ok"] for r in res) and "all_reduce.min" in res[0]["msg"]
     else:
         assert all(r["ok"] and r["n"] == 2 for r in res)
+
+
+@pytest.mark.parametrize("numel", [21, 1 << 18, 1 << 21])  # the toy's 84 B bucket, 1 MiB, 8 MiB
+def test_bucket_sized_all_reduce_world4(tmp_path, numel):
+    """tiny and bucket-sized messages over 4 ranks (gloo)."""
+    world = 4
+    spawn(_workers.bucket_all_reduce, args=(world, free_port(), str(tmp_path), numel), nprocs=world)
+    res = _load(tmp_path, world)
+    expect = sum(range(1, world + 1)) / world
+    for r in res:
+        assert r["avg_ok"] and r["bcast_ok"]
+        assert abs(r["avg0"] - expect) < 1e-6
