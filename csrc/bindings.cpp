@@ -127,7 +127,8 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
                              double lr, double momentum, double dampening, double weight_decay, bool nesterov,
                              std::shared_ptr<XgmiComm> ar, int64_t n_steps, int64_t W, int64_t rank,
                              int64_t num_samples, bool shuffle, int64_t seed, Tensor cursor, Tensor losses,
-                             c10::optional<Tensor> stamps, int64_t variant, bool x_zero_padded) {
+                             c10::optional<Tensor> stamps, int64_t variant, bool x_zero_padded,
+                             c10::optional<Tensor> idx, int64_t cursor_j) {
   TORCH_CHECK(X.is_cuda(), "X must be a GPU tensor");  // rows may be padded: checked below
   check_gpu(P, "P");
   check_gpu(G, "G");
@@ -191,6 +192,15 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
     pa.stamps = stamps->data_ptr<int64_t>();
   }
   pa.variant = (int)variant;
+  pa.cursor_host_j = -1;
+  if (idx.has_value() && idx->defined()) {
+    TORCH_CHECK(idx->is_cuda() && idx->scalar_type() == at::kInt && idx->is_contiguous() && idx->numel() >= num_samples,
+                "persistent: idx must be a contiguous int32 GPU tensor of num_samples indices");
+    TORCH_CHECK(cursor_j >= 0 && cursor_j + n_steps <= (num_samples + B - 1) / B,
+                "persistent: with an explicit index list a launch must stay inside the epoch (pass cursor_j)");
+    pa.idx = idx->data_ptr<int32_t>();
+    pa.cursor_host_j = (int)cursor_j;
+  }
   const bool wave = variant != kPersistWorkgroup && linear_wave_supported(a, pa);
   TORCH_CHECK(wave || variant < kPersistWave, "persistent: the wave engine does not support this configuration");
   TORCH_CHECK(wave || fused_mlp_persistent_lds_bytes((int)B, (int)Din, (int)H, (int)Dout, (int)num_samples,
@@ -586,7 +596,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("momentum"), py::arg("dampening"), py::arg("weight_decay"), py::arg("nesterov"), py::arg("ar"),
         py::arg("n_steps"), py::arg("W"), py::arg("rank"), py::arg("num_samples"), py::arg("shuffle"),
         py::arg("seed"), py::arg("cursor"), py::arg("losses"), py::arg("stamps") = py::none(),
-        py::arg("variant") = 0, py::arg("x_zero_padded") = false);
+        py::arg("variant") = 0, py::arg("x_zero_padded") = false, py::arg("idx") = py::none(),
+        py::arg("cursor_j") = -1);
   m.def("persistent_engine", &persistent_engine, py::arg("B"), py::arg("Din"), py::arg("H"), py::arg("Dout"),
         py::arg("loss_kind"), py::arg("num_samples"), py::arg("world"), py::arg("variant") = 0);
   m.def("fused_mlp_lds_bytes", [](int B, int Din, int H, int Dout) { return fused_mlp_lds_bytes(B, Din, H, Dout); });

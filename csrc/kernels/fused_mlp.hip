@@ -522,9 +522,9 @@ __global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs
   const int steps_per_epoch = (pa.num_samples + B - 1) / B;
   int opt_step = a.opt_step ? *a.opt_step : 0;
   uint32_t seq = a.ar.world > 1 ? *a.ar.seq : 0u;
-  rank_epoch_indices(ebuf(epoch), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch, pa.shuffle,
+  rank_epoch_indices_or(pa.idx, ebuf(epoch), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch, pa.shuffle,
                      tid, NT);
-  rank_epoch_indices(ebuf(epoch + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
+  rank_epoch_indices_or(pa.idx, ebuf(epoch + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
                      pa.shuffle, tid, NT);
   __syncthreads();
   const bool pf_ok = B * full.Din <= kPf * NT && B * (FY ? full.Dout : 1) <= kPf * NT;
@@ -553,7 +553,7 @@ __global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs
       ++ne;
     }
     if (j == 0 && step > 0) {
-      rank_epoch_indices(ebuf(epoch + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
+      rank_epoch_indices_or(pa.idx, ebuf(epoch + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
                          pa.shuffle, tid, NT);
       __syncthreads();
     }
@@ -702,6 +702,9 @@ hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hip
     return hipErrorInvalidValue;
   if (a.ar.world > 1 && (num_params(a) > a.ar.max_elems || a.ar.world != p.W || a.ar.rank != p.rank))
     return hipErrorInvalidValue;
+  if (p.idx != nullptr && p.cursor_host_j >= 0 &&
+      p.cursor_host_j + p.n_steps > (p.num_samples + a.B - 1) / a.B)
+    return hipErrorInvalidValue;  // an explicit index list covers one epoch only
   if (p.variant != kPersistWorkgroup && linear_wave_supported(a, p)) return linear_wave_persistent(a, p, s);
   if (p.variant >= kPersistWave) return hipErrorInvalidValue;
   const size_t lds = fused_mlp_persistent_lds_bytes(a.B, a.Din, a.H, a.Dout, p.num_samples, a.ar.world);

@@ -74,6 +74,9 @@ struct PersistArgs {
                          // forward, loss, backward, all-reduce, sgd+land, epoch indices, total, realtime (100 MHz)
   int variant;           // kPersistAuto / kPersistWorkgroup / kPersistWave...
   int loss_ring;         // set by the launcher: the wave engine reduces losses in helper waves
+  const int32_t* idx;    // optional [num_samples] index list of the cursor's epoch (replaces the in-kernel
+                         // Feistel permutation; the launch must then stay inside that epoch)
+  int cursor_host_j;     // the caller's view of cursor[1] (checked against n_steps when idx is set), or -1
 };
 // Engine choice: the register-resident single-wave engine (linear_wave.hip) runs
 // Linear(Din, Dout) models with B <= 64 and small Dout; everything else runs the

@@ -207,10 +207,10 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
   const int T = (int)((pos0 + n - 1) / S - pos0 / S);  // epoch transitions inside this launch
   auto list = [&](int e) { return elist + (e & 1) * estride; };
 
-  rank_epoch_indices(list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
+  rank_epoch_indices_or(pa.idx, list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
                      (int)threadIdx.x, kThreads);
   if (T > 0)
-    rank_epoch_indices(list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1, pa.shuffle,
+    rank_epoch_indices_or(pa.idx, list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1, pa.shuffle,
                        (int)threadIdx.x, kThreads);
   __syncthreads();
   if (wave != 0) {
@@ -219,7 +219,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
     for (int i = 1; i <= T; ++i) {
       __syncthreads();
       if (i < T)
-        rank_epoch_indices(list(e0 + i + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + i + 1,
+        rank_epoch_indices_or(pa.idx, list(e0 + i + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + i + 1,
                            pa.shuffle, (int)threadIdx.x - 64, kThreads - 64);
     }
     return;
@@ -680,9 +680,9 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   // Both lists are built even when the launch stays in one epoch: the trainer
   // reads (stale but valid) indices for the kNB positions past its last step,
   // so every list entry it can touch is a valid dataset row (no clamp per load).
-  rank_epoch_indices(list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
+  rank_epoch_indices_or(pa.idx, list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
                      (int)threadIdx.x, kThreads);
-  rank_epoch_indices(list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1, pa.shuffle,
+  rank_epoch_indices_or(pa.idx, list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1, pa.shuffle,
                      (int)threadIdx.x, kThreads);
   // Loss ring (pa.loss_ring): the trainer stores each lane's scaled loss share
   // per step (one ds_write), the helper waves add the 64 shares and write
@@ -705,7 +705,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     for (int i = 1; i <= T; ++i) {
       __syncthreads();
       if (i < T)
-        rank_epoch_indices(list(e0 + i + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + i + 1,
+        rank_epoch_indices_or(pa.idx, list(e0 + i + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + i + 1,
                            pa.shuffle, ht, hn);
       // at barrier i the trainer has trained every position before (e0+i)*S - kNB
       if (ring) reduce_losses(min((int64_t)(e0 + i) * S - kNB, pos0 + n));

@@ -62,4 +62,16 @@ __device__ __forceinline__ void rank_epoch_indices(int32_t* out, uint32_t N, int
   }
 }
 
+// The epoch's list from a caller-provided index array (e.g. the host's torch-
+// identical DistributedSampler order) when `given` is set, else the Feistel one.
+__device__ __forceinline__ void rank_epoch_indices_or(const int32_t* given, int32_t* out, uint32_t N, int W, int rank,
+                                                      int num_samples, uint64_t seed, int epoch, int shuffle, int tid,
+                                                      int nt) {
+  if (given != nullptr) {
+    for (int i = tid; i < num_samples; i += nt) out[i] = given[i];
+  } else {
+    rank_epoch_indices(out, N, W, rank, num_samples, seed, epoch, shuffle, tid, nt);
+  }
+}
+
 }  // namespace ptdt

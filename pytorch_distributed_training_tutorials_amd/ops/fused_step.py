@@ -145,7 +145,7 @@ class FusedMLPStep:
     # ------------------------------------------------------------ persistent engine
     def run_persistent(self, X, Y, n_steps: int, batch_size: int, sampler, cursor: torch.Tensor,
                        losses: torch.Tensor, max_steps_per_launch: int = 8192, stamps: torch.Tensor | None = None,
-                       variant: str | None = None):
+                       variant: str | None = None, idx: torch.Tensor | None = None, cursor_j: int = 0):
         """Run ``n_steps`` DDP steps in persistent launches: each step = gather ->
         fwd/loss/bwd -> all-reduce (in-kernel xGMI one-shot; identity at world 1)
         -> SGD. Two engines (``variant``, default ``$PTDT_PERSIST`` or "auto"):
@@ -155,7 +155,11 @@ class FusedMLPStep:
         "auto" picks the wave engine when it supports the configuration. ``sampler`` is a DeviceDistributedSampler
         (sharding/permutation parameters); ``cursor`` an int32[2] device tensor
         ``[epoch, step_in_epoch]`` advanced by the kernel; ``losses[i]`` receives
-        step i's mean loss (``losses`` must hold ``min(n_steps, max_steps_per_launch)``)."""
+        step i's mean loss (``losses`` must hold ``min(n_steps, max_steps_per_launch)``).
+        ``idx`` (int32, the epoch's index list, e.g. torch's DistributedSampler
+        order from DeviceDataLoader.device_indices) replaces the in-kernel
+        permutation; the steps must then stay inside that epoch, starting at
+        step ``cursor_j``."""
         if self.xgmi is None and self.comm is not None and self.comm.world > 1:
             raise RuntimeError("the persistent engine needs the xGMI all-reduce for world > 1")
         ce_index = self.loss_kind == LOSS_KINDS["ce_index"]
@@ -169,7 +173,8 @@ class FusedMLPStep:
                 batch_size, self.Din, self.H, self.Dout, self.loss_kind, self.ignore_index, self.has_bias,
                 self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
                 self.xgmi.handle if self.xgmi is not None else None, n, sampler.num_replicas, sampler.rank,
-                sampler.num_samples, sampler.shuffle, sampler.seed, cursor, losses, stamps, vid, padded)
+                sampler.num_samples, sampler.shuffle, sampler.seed, cursor, losses, stamps, vid, padded,
+                idx, cursor_j + done if idx is not None else -1)
             done += n
         self._pending = False
 

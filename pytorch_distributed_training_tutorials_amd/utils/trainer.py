@@ -8,6 +8,12 @@ calls ``sampler.set_epoch(epoch)`` and runs zero_grad -> forward ->
 cross_entropy -> backward -> step per batch.
 
 Engines (same observable result, different execution):
+  * ``persistent`` -- GPU, Linear[-ReLU-Linear] models + SGD, one rank or a
+                    working in-kernel xGMI all-reduce: ONE kernel launch per
+                    epoch runs every DDP step of it (ops/fused_step.py
+                    run_persistent; the single-wave engine for Linear models),
+                    fed the loader's torch-identical DistributedSampler order.
+                    The default whenever available.
   * ``fused``    -- GPU, Linear[-ReLU-Linear] models + SGD: one fused kernel +
                     one RCCL all-reduce per step, a whole epoch captured into a
                     hipGraph and replayed (ops/fused_step.py). The default on GPU
@@ -49,6 +55,14 @@ class _ModuleView(nn.Module):
         return self.module(*a, **k)
 
 
+class _Shard:
+    """Sampler parameters the persistent kernel needs when it is given the index list."""
+
+    def __init__(self, world, rank, num_samples):
+        self.num_replicas, self.rank, self.num_samples = world, rank, num_samples
+        self.shuffle, self.seed = False, 0
+
+
 def _sgd_hparams(opt):
     g = opt.param_groups[0]
     if len(opt.param_groups) != 1 or "momentum" not in g:
@@ -82,16 +96,26 @@ class Trainer:
         self.comm = comm if comm is not None else comm_mod.get_default(self.device if self.device.type == "cuda" else None)
         model = model.to(self.device)
         self.engine_name = self._select_engine(engine, model)
-        if self.engine_name == "fused":
+        xg = None
+        if self.engine_name == "persistent" and self.world_size > 1:
+            from ..parallel.xgmi import maybe_create
+
+            xg = maybe_create(self.comm, self.device)  # collective: every rank takes this branch
+            if xg is None:
+                if engine == "persistent":
+                    raise RuntimeError("persistent engine: the in-kernel xGMI all-reduce is unavailable")
+                self.engine_name = "fused"
+        if self.engine_name in ("fused", "persistent"):
             hp = _sgd_hparams(optimizer)
             loss_kind = self._fused_loss_kind()
-            self.engine = FusedMLPStep(model, loss=loss_kind, comm=self.comm, **hp)
+            self.engine = FusedMLPStep(model, loss=loss_kind, comm=self.comm, xgmi=xg, **hp)
             if self.world_size > 1:  # DDP init semantics: rank 0's parameters everywhere (M4)
                 self.comm.broadcast(self.engine.P, 0)
             self.model = _ModuleView(model)
             self._idx_buf = None
             self._graphs = {}
             self._loss_buf = None
+            self._cursor = None
         else:
             self.engine = None
             self.model = DistributedDataParallel(model, device_ids=[self.gpu_id] if self.device.type == "cuda" else None,
@@ -115,9 +139,9 @@ class Trainer:
 
     def _select_engine(self, engine: str, model) -> str:
         if engine == "auto":
-            return "fused" if self._fusable(model) else "autograd"
-        if engine == "fused" and not self._fusable(model):
-            raise ValueError("fused engine needs: GPU, DeviceDataLoader, SGD, Linear[-ReLU-Linear], CE/MSE loss")
+            return "persistent" if self._fusable(model) else "autograd"
+        if engine in ("fused", "persistent") and not self._fusable(model):
+            raise ValueError(f"{engine} engine needs: GPU, DeviceDataLoader, SGD, Linear[-ReLU-Linear], CE/MSE loss")
         return engine
 
     def _fused_loss_kind(self) -> str:
@@ -155,7 +179,9 @@ class Trainer:
         self.log(f"[GPU: {self.gpu_id} Epoch: {epoch}, Batch size: {b_sz} | Steps {len(self.train_dataloader)}]")
         self._set_epoch(epoch)
         t0 = time.perf_counter()
-        if self.engine_name == "fused":
+        if self.engine_name == "persistent" and not self.faults.armed:
+            self._run_epoch_persistent(epoch)
+        elif self.engine_name in ("fused", "persistent"):
             self._run_epoch_fused()
         else:
             for xs, ys in self.train_dataloader:
@@ -196,6 +222,25 @@ class Trainer:
         else:
             self.engine.run(X, Y, self._idx_buf, list(batches), self._loss_buf)
         self.global_step += len(batches)
+
+    # ------------------------------------------------------------ persistent engine
+    def _run_epoch_persistent(self, epoch: int):
+        dl = self.train_dataloader
+        X, Y = dl.dataset.tensors[0], dl.dataset.tensors[1]
+        n = dl._num_samples()
+        if self._idx_buf is None:
+            self._idx_buf = torch.zeros(n, dtype=torch.int32, device=self.device)
+        dl.device_indices(out=self._idx_buf)  # torch-identical DistributedSampler order
+        steps = len(dl)
+        if self._loss_buf is None or self._loss_buf.numel() < steps:
+            self._loss_buf = torch.zeros(steps, device=self.device)
+        if self._cursor is None:
+            self._cursor = torch.zeros(2, dtype=torch.int32, device=self.device)
+        self._cursor.copy_(torch.tensor([epoch, 0], dtype=torch.int32))
+        shard = _Shard(self.world_size, self.rank, n)
+        self.engine.run_persistent(X, Y, steps, dl.batch_size, shard, self._cursor, self._loss_buf,
+                                   idx=self._idx_buf, cursor_j=0)
+        self.global_step += steps
 
     def last_losses(self) -> torch.Tensor | None:
         return None if self._loss_buf is None else self._loss_buf

@@ -105,13 +105,38 @@ def test_trainer_fused_engine_prints_reference_lines(pg, dev, capsys):
     loader = DeviceDataLoader(ds, batch_size=32, sampler=DistributedSampler(ds, 1, 0))
     model = ddp_toy_model()
     t = Trainer(model, loader, FusedSGD(model.parameters(), lr=1e-2), 0)
-    assert t.engine_name == "fused"
+    assert t.engine_name == "persistent"  # one launch per epoch
     t.train(2)
     out = capsys.readouterr().out
     assert "[GPU: 0 Epoch: 0, Batch size: 32 | Steps 64]" in out
     assert "[GPU: 0 Epoch: 1, Batch size: 32 | Steps 64]" in out
     assert float(t.last_losses().abs().max()) == 0.0  # quirk Q1: zero loss
     assert list(t.model.state_dict()) == ["module.weight", "module.bias"]
+
+
+@pytest.mark.parametrize("model_kind", ["linear", "mlp"])
+def test_trainer_persistent_engine_equals_fused_engine(pg, dev, model_kind):
+    """The per-epoch persistent launch (fed the loader's torch-identical sampler order)
+    reaches the same parameters as the per-step fused kernel over the same batches."""
+    from pytorch_distributed_training_tutorials_amd.data import DeviceDataLoader, DeviceTensorDataset, DistributedSampler
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP
+    from pytorch_distributed_training_tutorials_amd.ops.optim import FusedSGD
+    from pytorch_distributed_training_tutorials_amd.utils.trainer import Trainer
+
+    torch.manual_seed(3)
+    ds = DeviceTensorDataset.synthetic_classification(500, 20, 4, device=dev)  # 16 steps, last one short
+    params = []
+    for engine in ("persistent", "fused"):
+        torch.manual_seed(4)
+        model = torch.nn.Linear(20, 4) if model_kind == "linear" else ToyMLP(20, 32, 4)
+        loader = DeviceDataLoader(ds, batch_size=32, sampler=DistributedSampler(ds, 1, 0, shuffle=True, seed=5))
+        t = Trainer(model, loader, FusedSGD(model.parameters(), lr=0.05, momentum=0.9), 0, engine=engine,
+                    verbose=False)
+        assert t.engine_name == engine
+        t.train(3)
+        torch.cuda.synchronize()
+        params.append(torch.cat([p.detach().reshape(-1) for p in model.parameters()]))
+    torch.testing.assert_close(params[0], params[1], rtol=1e-5, atol=1e-6)
 
 
 def test_trainer_autograd_engine_mlp_learns(pg, dev):
