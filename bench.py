@@ -17,8 +17,10 @@ Every timed step does the full work: batch gather by sampler index, forward,
 loss, backward, RCCL all-reduce of the gradient bucket across all ranks, SGD
 update; the sampler permutation of every epoch is generated on device inside
 the timed region. Engines:
-  fused     (default) fused step kernel + RCCL all-reduce, epochs captured into
-            hipGraphs (ops/fused_step.py)
+  persistent (default) many DDP steps per launch, in-kernel xGMI all-reduce
+            (single-wave engine for Linear(Din, Dout), LDS workgroup engine otherwise)
+  fused     fused step kernel + in-kernel xGMI or RCCL all-reduce, epochs
+            captured into hipGraphs (ops/fused_step.py)
   autograd  native DDP reducer + native Linear/CE/SGD kernels, eager
   reference stock PyTorch-ROCm loop (torch DDP, DataLoader + DistributedSampler,
             nn.Linear, F.cross_entropy, torch.optim.SGD) -- the comparator
@@ -61,6 +63,10 @@ def parse(argv=None):
     ap.add_argument("--stamps", action="store_true",
                     help="persistent engine: diagnostic run with in-kernel phase timers (separate from the timed run)")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
+    ap.add_argument("--share_gpu", action="store_true",
+                    help="REHEARSAL ONLY: every rank on cuda:0 with a gloo control plane (RCCL refuses two ranks "
+                         "per GPU), to exercise the N>1 path (xGMI self-test, in-kernel all-reduce, replica-sync "
+                         "check) on a 1-GPU box; the result is tagged and is not a scaling number")
     return ap.parse_args(argv)
 
 
@@ -70,8 +76,49 @@ def _setup(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    env.init_process_group("nccl")
+    env.init_process_group("gloo" if args.share_gpu else "nccl")
     return env.rank(), env.world_size(), env.local_rank()
+
+
+class _StagedComm:
+    """Control plane for --share_gpu rehearsals: gloo collectives on host copies
+    (RCCL cannot put two ranks on one GPU). Same surface as parallel.comm.Communicator
+    for what the bench uses."""
+
+    def __init__(self, dev):
+        import torch.distributed as dist
+
+        self.dist, self.dev = dist, dev
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+
+    def barrier(self):
+        torch.cuda.synchronize(self.dev)
+        self.dist.barrier()
+
+    def broadcast(self, t, src=0):
+        h = t.detach().cpu()
+        self.dist.broadcast(h, src)
+        t.copy_(h)
+        return t
+
+    def all_reduce(self, t, op="sum"):
+        h = t.detach().cpu()
+        self.dist.all_reduce(h, {"sum": self.dist.ReduceOp.SUM, "max": self.dist.ReduceOp.MAX}[op])
+        t.copy_(h)
+        return t
+
+    def all_gather_object(self, obj):
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+
+def _replicas_in_sync(comm, params: torch.Tensor) -> bool:
+    """DDP invariant after training: every rank holds bit-identical parameters."""
+    if comm.world == 1:
+        return True
+    digest = params.detach().float().cpu().numpy().tobytes()
+    return len(set(comm.all_gather_object(digest))) == 1
 
 
 def _build_model(args, dev):
@@ -156,7 +203,8 @@ def run_fused(args, rank, world, dev, comm):
     t = _timed(comm, dev, lambda: [get_graph(n).replay() for n in timed])
     if xg is not None:
         xg.check()
-    extra = {"steps_per_epoch": S, "steps_per_graph": full, "warmup_steps_run": warm_steps,
+    extra = {"replicas_in_sync": _replicas_in_sync(comm, eng.P),
+             "steps_per_epoch": S, "steps_per_graph": full, "warmup_steps_run": warm_steps,
              "final_loss": float(losses[(args.steps - 1) % S].item()),
              "allreduce": "xgmi-oneshot (in-kernel)" if xg is not None else "rccl",
              "kernels": ("1 launch per step: fused fwd+loss+bwd+xGMI all-reduce+SGD, hipGraph" if xg is not None
@@ -198,6 +246,7 @@ def run_persistent(args, rank, world, dev, comm):
                                                      chunk, variant=variant))
     if xg is not None:
         xg.check()
+    in_sync = _replicas_in_sync(comm, eng.P)
     phase = None
     if args.stamps:  # diagnostic pass AFTER the timed region (timers cost a little)
         st = torch.zeros(9, dtype=torch.int64, device=dev)
@@ -210,7 +259,7 @@ def run_persistent(args, rank, world, dev, comm):
         phase = {"cycles_per_step": {n: round(v[k] / args.steps, 1) for k, n in enumerate(names)},
                  "total_cycles_per_step": round(v[7] / args.steps, 1), "clock_GHz": round(clk / 1e9, 3)}
     last = (args.steps - 1) % chunk
-    extra = {"steps_per_epoch": S, "launches_timed": math.ceil(args.steps / chunk),
+    extra = {"replicas_in_sync": in_sync, "steps_per_epoch": S, "launches_timed": math.ceil(args.steps / chunk),
              "final_loss": float(losses[last].item()),
              "allreduce": "xgmi-oneshot (in-kernel)" if world > 1 else "identity (world 1)",
              "persistent_engine": which,
@@ -323,11 +372,17 @@ def main(argv=None):
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU (MI355X)")
     rank, world, local = _setup(args)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", 0 if args.share_gpu else local)
     from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
     from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
 
-    comm = comm_mod.get_default(dev)
+    if args.share_gpu:
+        if args.engine not in ("persistent", "fused") or args.allreduce == "rccl":
+            raise SystemExit("--share_gpu rehearses the xGMI engines only (RCCL needs one GPU per rank)")
+        torch.cuda.set_device(dev)
+        comm = _StagedComm(dev)
+    else:
+        comm = comm_mod.get_default(dev)
     runner = {"persistent": run_persistent, "fused": run_fused, "autograd": run_autograd,
               "reference": run_reference}[args.engine]
     elapsed, extra = runner(args, rank, world, dev, comm)
@@ -356,6 +411,8 @@ def main(argv=None):
                          "(CPU/gloo, same N); the reference publishes no GPU DDP number",
         **extra,
     }
+    if args.share_gpu:
+        rec["rehearsal"] = f"{world} ranks sharing cuda:0 (no xGMI hop): protocol/correctness check, not a scaling number"
     if rank == 0:
         line = json.dumps(rec)
         print(line, flush=True)
