@@ -1,0 +1,95 @@
+#!/usr/bin/env python3
+"""Throughput of the native bf16 GEMMs vs PyTorch-ROCm's library GEMM (hipBLASLt).
+
+Kernels:
+  big   csrc/kernels/gemm_big.hip  (256x256x64 tile, LDS-DMA double buffer)  C = A . Bt^T
+  tile  csrc/kernels/gemm.hip      (64x64 strided tile, the small-shape path)
+  torch torch.matmul (hipBLASLt), same operands
+
+Operands are uniform [-1, 1) (zero-filled operands read high: DVFS), variants are
+timed in interleaved rounds inside one process (cdna_hip_programming.md §5.4 rules
+24-25) and the median is reported. One JSON line per shape.
+
+    python benchmarks/gemm_bench.py [--shapes 4096x4096x4096,8192x8192x8192] [--rounds 5]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timed(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--shapes", default="4096x4096x4096,8192x8192x8192,8192x8192x1024,4096x11008x4096,"
+                                        "120x1000x2048,2048x2048x2048")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--tile", action="store_true", help="also time the 64x64 strided kernel")
+    ap.add_argument("--extra_sched", type=int, nargs="*", default=[],
+                    help="also time these schedules of the big kernel (0: 8 waves read-then-multiply, "
+                         "1: 8 waves ping-pong (default))")
+    a = ap.parse_args()
+    from pytorch_distributed_training_tutorials_amd import native
+
+    C_ = native()
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    for spec in a.shapes.split(","):
+        M, N, K = (int(v) for v in spec.split("x"))
+        A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        Bt = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
+        Cb = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        Ct = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        flops = 2.0 * M * N * K
+        variants = {"torch": lambda: torch.matmul(A, Bt.t(), out=Ct)}
+        if C_.gemm_big_ok(A, Bt):
+            variants["big"] = lambda: C_.gemm_big_(A, Bt, Cb, sched=1)
+            for sc in a.extra_sched:
+                variants[f"big_sched{sc}"] = (lambda sc=sc: C_.gemm_big_(A, Bt, Cb, sched=sc))
+        if a.tile:
+            variants["tile"] = lambda: C_.gemm_(A, Bt.t(), Cb, None, None, False, 1.0, 0.0, None, 1)
+        # numerics vs fp32 on the same bf16 operands
+        ref = A.float() @ Bt.float().t()
+        err = {}
+        for k, f in variants.items():
+            f()
+            torch.cuda.synchronize()
+            out = Cb if k != "torch" else Ct
+            err[k] = float((out.float() - ref).abs().max() / ref.abs().max())
+        iters = max(3, min(200, int(2e13 / flops)))
+        for f in variants.values():
+            timed(f, 2)
+        res = {k: [] for k in variants}
+        for _ in range(a.rounds):
+            for k, f in variants.items():
+                res[k].append(timed(f, iters))
+        rec = {"metric": "bf16 GEMM TFLOP/s (C = A.Bt^T, uniform[-1,1) operands)", "M": M, "N": N, "K": K,
+               "iters": iters, "rounds": a.rounds}
+        for k, ts in res.items():
+            med = statistics.median(ts)
+            rec[f"{k}_tflops"] = round(flops / med / 1e12, 1)
+            rec[f"{k}_us"] = round(med * 1e6, 2)
+            rec[f"{k}_max_rel_err"] = round(err[k], 5)
+        if "big" in res:
+            rec["big_vs_torch"] = round(rec["big_tflops"] / rec["torch_tflops"], 3)
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

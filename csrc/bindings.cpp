@@ -449,6 +449,44 @@ void gemm_(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> bias, c10::option
   hip_check(gemm(g, cur_stream(A)), "gemm");
 }
 
+// C = alpha*A.Bt^T (+beta C) (+bias) (relu) on the 256x256 LDS-DMA kernel (gemm_big.hip).
+// A [M,K], Bt [N,K]: bf16 with unit K stride; C [M,N] f32/bf16 with unit column stride.
+bool gemm_big_ok(Tensor A, Tensor Bt) {
+  return A.is_cuda() && Bt.is_cuda() && A.dim() == 2 && Bt.dim() == 2 && A.scalar_type() == at::kBFloat16 &&
+         Bt.scalar_type() == at::kBFloat16 && A.stride(1) == 1 && Bt.stride(1) == 1 && A.size(1) == Bt.size(1) &&
+         gemm_bf16_big_supported((int)A.size(0), (int)Bt.size(0), (int)A.size(1), A.stride(0), Bt.stride(0),
+                                 A.data_ptr(), Bt.data_ptr());
+}
+
+void gemm_big_(Tensor A, Tensor Bt, Tensor C, c10::optional<Tensor> bias, bool relu, double alpha, double beta,
+               int64_t sched) {
+  TORCH_CHECK(gemm_big_ok(A, Bt), "gemm_big: needs bf16 A[M,K], Bt[N,K] with unit K stride, K % 64 == 0, "
+              "16-B aligned rows; got ", A.sizes(), A.strides(), " / ", Bt.sizes(), Bt.strides());
+  TORCH_CHECK(C.is_cuda() && C.dim() == 2 && C.size(0) == A.size(0) && C.size(1) == Bt.size(0) && C.stride(1) == 1,
+              "gemm_big: C must be [M,N] with unit column stride");
+  TORCH_CHECK(C.scalar_type() == at::kFloat || C.scalar_type() == at::kBFloat16, "gemm_big: C f32 or bf16");
+  BigGemmArgs g{};
+  g.M = (int)A.size(0);
+  g.N = (int)Bt.size(0);
+  g.K = (int)A.size(1);
+  g.A = A.data_ptr(); g.lda = A.stride(0);
+  g.Bt = Bt.data_ptr(); g.ldb = Bt.stride(0);
+  g.C = C.data_ptr(); g.ldc = C.stride(0);
+  g.out_dtype = dt_of(C);
+  if (bias.has_value() && bias->defined()) {
+    check_gpu(*bias, "bias");
+    TORCH_CHECK(bias->numel() == g.N, "gemm_big: bias must have N entries");
+    g.bias = bias->data_ptr();
+    g.bias_dtype = dt_of(*bias);
+  }
+  g.relu = relu ? 1 : 0;
+  g.alpha = (float)alpha;
+  g.beta = (float)beta;
+  g.sched = sched < 0 ? 1 : (int)sched;
+  c10::hip::HIPGuard guard(A.device().index());
+  hip_check(gemm_bf16_big(g, cur_stream(A)), "gemm_big");
+}
+
 Tensor relu_bwd(Tensor dy, Tensor y) {
   check_gpu(dy, "dy");
   check_gpu(y, "y");
@@ -614,6 +652,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm_", &gemm_, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("bias") = py::none(),
         py::arg("amask") = py::none(), py::arg("relu") = false, py::arg("alpha") = 1.0, py::arg("beta") = 0.0,
         py::arg("colsum") = py::none(), py::arg("split_k") = 1);
+  m.def("gemm_big_ok", &gemm_big_ok);
+  m.def("gemm_big_", &gemm_big_, py::arg("A"), py::arg("Bt"), py::arg("C"), py::arg("bias") = py::none(),
+        py::arg("relu") = false, py::arg("alpha") = 1.0, py::arg("beta") = 0.0, py::arg("sched") = -1);
   m.def("relu_bwd", &relu_bwd);
   m.def("col_sum_", &col_sum_);
   m.def("philox_", &philox_);

@@ -173,6 +173,22 @@ struct GemmArgs {
 };
 hipError_t gemm(const GemmArgs& g, hipStream_t s);
 
+// Large-shape bf16 GEMM (csrc/kernels/gemm_big.hip): C = alpha*A.Bt^T (+beta*C)(+bias)(ReLU),
+// A [M,K] and Bt [N,K] both K-contiguous bf16, C f32 or bf16 with row stride ldc.
+struct BigGemmArgs {
+  int M, N, K;
+  const void* A; int64_t lda;
+  const void* Bt; int64_t ldb;
+  void* C; int64_t ldc;
+  int out_dtype;
+  const void* bias; int bias_dtype;
+  int relu;
+  float alpha, beta;
+  int sched;  // 0: read-then-multiply per K-tile, 1: ping-pong wave pairs (default)
+};
+bool gemm_bf16_big_supported(int M, int N, int K, int64_t lda, int64_t ldb, const void* A, const void* Bt);
+hipError_t gemm_bf16_big(const BigGemmArgs& g, hipStream_t s);
+
 // Elementwise helpers (csrc/kernels/elementwise.hip)
 hipError_t relu_backward(const void* dy, const void* y, void* dx, int dtype, int64_t n, hipStream_t s);
 hipError_t col_sum(const void* x, int dtype, int64_t rows, int64_t cols, float* out, int accumulate,

@@ -12,6 +12,11 @@ Backward : dx = (dy * relu'(y)) W      -- ReLU mask applied while staging dy
 Long-K / tiny-MN shapes (ToyModel's K=10000, M=20, N=10) run split-K over
 workgroups with fp32 atomics so the launch has enough workgroups to fill the
 chip instead of one workgroup walking 10000 columns.
+Large bf16 shapes (K % 64 == 0, >= 2^24 MACs) run the 256x256 LDS-DMA kernel
+(csrc/kernels/gemm_big.hip, ~1.1 PFLOP/s at 4096^3): the forward directly on
+nn.Linear's [out, in] weight, the backward GEMMs on K-contiguous copies (the
+transposes cost a few % of the GEMM), with the ReLU mask and bias gradient as
+separate elementwise / column-sum kernels.
 CPU tensors use ``torch.nn.functional.linear`` (plumbing tests only).
 """
 from __future__ import annotations
@@ -36,6 +41,23 @@ def _split_k(M: int, N: int, K: int, dtype) -> int:
         return 1
     want = max(1, min(ktiles // 4, _CUS // tiles))
     return int(want)
+
+
+_BIG_MIN_MACS = 1 << 24
+
+
+def _big(M: int, N: int, K: int, dtype) -> bool:
+    """Use the 256x256 kernel: bf16, K a multiple of its 64-deep K-tile, enough work."""
+    return dtype == torch.bfloat16 and K >= 64 and K % 64 == 0 and M * N * K >= _BIG_MIN_MACS
+
+
+def gemm_nt_big(A: torch.Tensor, Bt: torch.Tensor, out_dtype, bias=None, relu: bool = False) -> torch.Tensor:
+    """C = A @ Bt^T on the 256x256 kernel (A [M,K], Bt [N,K], both made K-contiguous)."""
+    A = A if A.stride(-1) == 1 and A.stride(0) % 8 == 0 else A.contiguous()
+    Bt = Bt if Bt.stride(-1) == 1 and Bt.stride(0) % 8 == 0 else Bt.contiguous()
+    C = torch.empty((A.shape[0], Bt.shape[0]), device=A.device, dtype=out_dtype)
+    native().gemm_big_(A, Bt, C, bias, relu)
+    return C
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, out: torch.Tensor | None = None, *, bias=None, amask=None,
@@ -73,7 +95,11 @@ class _LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, shape[-1])
         if not x2.is_contiguous():
             x2 = x2.contiguous()
-        y = gemm(x2, weight.t(), bias=bias, relu=relu, out_dtype=x.dtype)
+        M, K = x2.shape
+        if _big(M, weight.shape[0], K, x2.dtype):
+            y = gemm_nt_big(x2, weight, x.dtype, bias=bias, relu=relu)
+        else:
+            y = gemm(x2, weight.t(), bias=bias, relu=relu, out_dtype=x.dtype)
         ctx.relu = relu
         ctx.has_bias = bias is not None
         ctx.bias_dtype = bias.dtype if bias is not None else None
@@ -89,6 +115,19 @@ class _LinearFn(torch.autograd.Function):
             dy2 = dy2.contiguous()
         mask = y if ctx.relu else None
         dx = dw = db = None
+        M, Nout, Kin = dy2.shape[0], weight.shape[0], weight.shape[1]
+        if _big(M, Kin, Nout, dy2.dtype) and _big(Nout, Kin, M, dy2.dtype):
+            C_ = native()
+            g = C_.relu_bwd(dy2, mask) if mask is not None else dy2
+            if ctx.needs_input_grad[0]:
+                dx = gemm_nt_big(g, weight.t(), x2.dtype).reshape(ctx.in_shape)
+            if ctx.needs_input_grad[1]:
+                dw = gemm_nt_big(g.t(), x2.t(), weight.dtype)
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                cs = torch.empty(Nout, device=dy.device, dtype=torch.float32)
+                C_.col_sum_(g, cs, False)
+                db = cs if ctx.bias_dtype == torch.float32 else cs.to(ctx.bias_dtype)
+            return dx, dw, db, None
         if ctx.needs_input_grad[0]:
             dx = gemm(dy2, weight, amask=mask, out_dtype=x2.dtype).reshape(ctx.in_shape)
         if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):

@@ -118,6 +118,45 @@ def test_gemm_layouts(native, dev, dtype, M, N, K, layout):
     torch.testing.assert_close(C, ref, rtol=tol, atol=tol * 4)
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 1024), (300, 200, 128), (120, 1000, 2048),
+                                   (1, 257, 64), (1000, 17, 192)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("sched", [0, 1])
+def test_gemm_big_matches_fp32(native, dev, M, N, K, out_dtype, sched):
+    """256x256 LDS-DMA kernel: C = A.Bt^T (+bias, ReLU, alpha/beta) vs fp32 on the same bf16 operands;
+    asymmetric operands catch a transposed C write, edge shapes the clamped rows."""
+    torch.manual_seed(M * 7 + N + K)
+    A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    Bt = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    assert native.gemm_big_ok(A, Bt)
+    ref = A.float() @ Bt.float().t()
+    C = torch.empty(M, N, device=dev, dtype=out_dtype)
+    native.gemm_big_(A, Bt, C, sched=sched)
+    tol = 1e-4 * math.sqrt(K) if out_dtype == torch.float32 else 1e-2 * math.sqrt(K) / 8
+    torch.testing.assert_close(C.float(), ref, rtol=tol, atol=tol)
+    bias = torch.randn(N, device=dev)
+    C0 = torch.randn(M, N, device=dev).to(out_dtype)
+    C1 = C0.clone()
+    native.gemm_big_(A, Bt, C1, bias, True, 0.5, 2.0, sched)
+    torch.testing.assert_close(C1.float(), F.relu(0.5 * ref + 2.0 * C0.float() + bias), rtol=tol, atol=tol)
+
+
+def test_gemm_big_identity_and_strides(native, dev):
+    """A = I picks rows of Bt exactly; strided (sliced) operands use their row stride."""
+    K = 128
+    eye = torch.eye(K, device=dev, dtype=torch.bfloat16)
+    Bt = torch.arange(300 * K, device=dev, dtype=torch.float32).reshape(300, K).remainder(97).to(torch.bfloat16)
+    C = torch.empty(K, 300, device=dev)
+    native.gemm_big_(eye, Bt, C)
+    torch.testing.assert_close(C, Bt.float().t(), rtol=0, atol=0)
+    big = (torch.rand(200, 3 * K, device=dev) * 2 - 1).to(torch.bfloat16)
+    A = big[:, K:2 * K]  # row stride 3K
+    C2 = torch.empty(200, 300, device=dev)
+    native.gemm_big_(A, Bt, C2)
+    torch.testing.assert_close(C2, A.float() @ Bt.float().t(), rtol=1e-3, atol=1e-2)
+    assert not native.gemm_big_ok(A[:, :100], Bt[:, :100])  # K % 64 != 0 -> strided kernel
+
+
 def test_gemm_epilogues(native, dev):
     torch.manual_seed(0)
     M, N, K = 70, 50, 90
@@ -160,6 +199,31 @@ def test_linear_autograd(native, dev, dtype, relu):
     torch.testing.assert_close(x.grad.float(), xr.grad, rtol=tol, atol=tol)
     torch.testing.assert_close(w.grad.float(), wr.grad, rtol=tol, atol=tol)
     torch.testing.assert_close(b.grad.float(), br.grad, rtol=tol, atol=tol * 4)
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_linear_big_bf16_path(native, dev, relu):
+    """bf16 Linear large enough for the 256x256 kernel (forward, dx, dW, db) vs fp32 autograd."""
+    import importlib
+
+    L = importlib.import_module("pytorch_distributed_training_tutorials_amd.ops.linear")  # module, not the op
+    torch.manual_seed(5)
+    M, K, N = 512, 384, 320
+    assert L._big(M, N, K, torch.bfloat16) and L._big(N, K, M, torch.bfloat16)
+    x = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16).requires_grad_(True)
+    w = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16).requires_grad_(True)
+    b = torch.randn(N, device=dev, dtype=torch.bfloat16, requires_grad=True)
+    y = L.linear(x, w, b, relu)
+    g = (torch.rand_like(y.float()) * 2 - 1).to(torch.bfloat16)
+    y.backward(g)
+    xr, wr, br = (t.detach().float().requires_grad_(True) for t in (x, w, b))
+    yr = F.linear(xr, wr, br)
+    if relu:
+        yr = F.relu(yr)
+    yr.backward(g.float())
+    for got, ref, k in ((y, yr, K), (x.grad, xr.grad, N), (w.grad, wr.grad, M), (b.grad, br.grad, M)):
+        tol = 2e-2 * math.sqrt(k) / 4
+        torch.testing.assert_close(got.float(), ref, rtol=tol, atol=tol)
 
 
 def test_linear_under_autocast(native, dev):
