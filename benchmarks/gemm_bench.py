@@ -2,9 +2,12 @@
 """Throughput of the native bf16 GEMMs vs PyTorch-ROCm's library GEMM (hipBLASLt).
 
 Kernels:
-  big   csrc/kernels/gemm_big.hip  (256x256x64 tile, LDS-DMA double buffer)  C = A . Bt^T
-  tile  csrc/kernels/gemm.hip      (64x64 strided tile, the small-shape path)
-  torch torch.matmul (hipBLASLt), same operands
+  auto      ops.linear.gemm_nt_big: csrc/kernels/gemm_big.hip with plan_big's (tile, split-K)
+  big256    gemm_big.hip, 256x256x64 tile, 8 waves, ping-pong      C = A . Bt^T
+  big128    gemm_big.hip, 128x128x64 tile, 4 waves, 2 workgroups per CU
+  big128_sS big128 with split-K over S slices (f32 atomics + zero fill + bf16 cast, all timed)
+  tile      csrc/kernels/gemm.hip      (64x64 strided tile, the small-shape path)
+  torch     torch.matmul (hipBLASLt), same operands
 
 Operands are uniform [-1, 1) (zero-filled operands read high: DVFS), variants are
 timed in interleaved rounds inside one process (cdna_hip_programming.md §5.4 rules
@@ -38,14 +41,18 @@ def timed(fn, iters):
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--shapes", default="4096x4096x4096,8192x8192x8192,8192x8192x1024,4096x11008x4096,"
-                                        "120x1000x2048,2048x2048x2048")
+                                        "120x1000x2048,2048x2048x2048,"
+                                        "1024x1024x1024,4096x4096x1024,3072x3072x3072,256x4096x4096,"
+                                        "128x2048x8192,120x2048x1024")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--tile", action="store_true", help="also time the 64x64 strided kernel")
     ap.add_argument("--extra_sched", type=int, nargs="*", default=[],
-                    help="also time these schedules of the big kernel (0: 8 waves read-then-multiply, "
+                    help="also time these schedules of the 256 kernel (0: 8 waves read-then-multiply, "
                          "1: 8 waves ping-pong (default))")
+    ap.add_argument("--splits", default="2,4,8,16", help="split-K slice counts to time with the 128 tile")
     a = ap.parse_args()
     from pytorch_distributed_training_tutorials_amd import native
+    from pytorch_distributed_training_tutorials_amd.ops.linear import gemm_nt_big, plan_big
 
     C_ = native()
     dev = torch.device("cuda", 0)
@@ -58,10 +65,22 @@ def main():
         Ct = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         flops = 2.0 * M * N * K
         variants = {"torch": lambda: torch.matmul(A, Bt.t(), out=Ct)}
+        outs = {"torch": Ct}
         if C_.gemm_big_ok(A, Bt):
-            variants["big"] = lambda: C_.gemm_big_(A, Bt, Cb, sched=1)
+            def auto():
+                outs["auto"] = gemm_nt_big(A, Bt, torch.bfloat16)
+            variants["auto"] = auto
+            variants["big256"] = lambda: C_.gemm_big_(A, Bt, Cb, sched=1)
             for sc in a.extra_sched:
-                variants[f"big_sched{sc}"] = (lambda sc=sc: C_.gemm_big_(A, Bt, Cb, sched=sc))
+                variants[f"big256_sched{sc}"] = (lambda sc=sc: C_.gemm_big_(A, Bt, Cb, sched=sc))
+            variants["big128"] = lambda: C_.gemm_big_(A, Bt, Cb, tile=128)
+            for sp in (int(v) for v in a.splits.split(",") if v):
+                if sp <= K // 64:
+                    def split_fn(sp=sp):
+                        acc = torch.zeros(M, N, device=dev, dtype=torch.float32)
+                        C_.gemm_big_(A, Bt, acc, tile=128, split_k=sp)
+                        outs[f"big128_s{sp}"] = acc.to(torch.bfloat16)
+                    variants[f"big128_s{sp}"] = split_fn
         if a.tile:
             variants["tile"] = lambda: C_.gemm_(A, Bt.t(), Cb, None, None, False, 1.0, 0.0, None, 1)
         # numerics vs fp32 on the same bf16 operands
@@ -70,7 +89,7 @@ def main():
         for k, f in variants.items():
             f()
             torch.cuda.synchronize()
-            out = Cb if k != "torch" else Ct
+            out = outs.get(k, Cb)
             err[k] = float((out.float() - ref).abs().max() / ref.abs().max())
         iters = max(3, min(200, int(2e13 / flops)))
         for f in variants.values():
@@ -86,8 +105,9 @@ def main():
             rec[f"{k}_tflops"] = round(flops / med / 1e12, 1)
             rec[f"{k}_us"] = round(med * 1e6, 2)
             rec[f"{k}_max_rel_err"] = round(err[k], 5)
-        if "big" in res:
-            rec["big_vs_torch"] = round(rec["big_tflops"] / rec["torch_tflops"], 3)
+        if "auto" in res:
+            rec["plan"] = list(plan_big(M, N, K))
+            rec["auto_vs_torch"] = round(rec["auto_tflops"] / rec["torch_tflops"], 3)
         print(json.dumps(rec), flush=True)
 
 

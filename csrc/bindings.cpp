@@ -449,7 +449,8 @@ void gemm_(Tensor A, Tensor B, Tensor C, c10::optional<Tensor> bias, c10::option
   hip_check(gemm(g, cur_stream(A)), "gemm");
 }
 
-// C = alpha*A.Bt^T (+beta C) (+bias) (relu) on the 256x256 LDS-DMA kernel (gemm_big.hip).
+// C = alpha*A.Bt^T (+beta C) (+bias) (relu) on the LDS-DMA kernel (gemm_big.hip): 256x256 or 128x128
+// block tile, optional split-K (f32 C pre-zeroed by the caller).
 // A [M,K], Bt [N,K]: bf16 with unit K stride; C [M,N] f32/bf16 with unit column stride.
 bool gemm_big_ok(Tensor A, Tensor Bt) {
   return A.is_cuda() && Bt.is_cuda() && A.dim() == 2 && Bt.dim() == 2 && A.scalar_type() == at::kBFloat16 &&
@@ -459,7 +460,7 @@ bool gemm_big_ok(Tensor A, Tensor Bt) {
 }
 
 void gemm_big_(Tensor A, Tensor Bt, Tensor C, c10::optional<Tensor> bias, bool relu, double alpha, double beta,
-               int64_t sched) {
+               int64_t sched, int64_t tile, int64_t split_k) {
   TORCH_CHECK(gemm_big_ok(A, Bt), "gemm_big: needs bf16 A[M,K], Bt[N,K] with unit K stride, K % 64 == 0, "
               "16-B aligned rows; got ", A.sizes(), A.strides(), " / ", Bt.sizes(), Bt.strides());
   TORCH_CHECK(C.is_cuda() && C.dim() == 2 && C.size(0) == A.size(0) && C.size(1) == Bt.size(0) && C.stride(1) == 1,
@@ -482,7 +483,11 @@ void gemm_big_(Tensor A, Tensor Bt, Tensor C, c10::optional<Tensor> bias, bool r
   g.relu = relu ? 1 : 0;
   g.alpha = (float)alpha;
   g.beta = (float)beta;
-  g.sched = sched < 0 ? 1 : (int)sched;
+  g.tile = tile == 128 ? 128 : 256;
+  g.sched = sched < 0 ? (g.tile == 256 ? 1 : 0) : (int)sched;
+  g.split_k = split_k > 1 ? (int)split_k : 1;
+  TORCH_CHECK(g.split_k == 1 || (C.scalar_type() == at::kFloat && !relu && beta == 0.0),
+              "gemm_big: split-K accumulates fp32 atomics: C must be f32 (pre-zeroed), no relu/beta");
   c10::hip::HIPGuard guard(A.device().index());
   hip_check(gemm_bf16_big(g, cur_stream(A)), "gemm_big");
 }
@@ -654,7 +659,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("colsum") = py::none(), py::arg("split_k") = 1);
   m.def("gemm_big_ok", &gemm_big_ok);
   m.def("gemm_big_", &gemm_big_, py::arg("A"), py::arg("Bt"), py::arg("C"), py::arg("bias") = py::none(),
-        py::arg("relu") = false, py::arg("alpha") = 1.0, py::arg("beta") = 0.0, py::arg("sched") = -1);
+        py::arg("relu") = false, py::arg("alpha") = 1.0, py::arg("beta") = 0.0, py::arg("sched") = -1,
+        py::arg("tile") = 256, py::arg("split_k") = 1);
   m.def("relu_bwd", &relu_bwd);
   m.def("col_sum_", &col_sum_);
   m.def("philox_", &philox_);

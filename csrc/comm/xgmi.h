@@ -61,13 +61,15 @@ __device__ __forceinline__ void xgmi_push(const XgmiArgs& x, uint32_t s, const f
 __device__ __forceinline__ float xgmi_gather_sum(const XgmiArgs& x, uint32_t s, int i) {
   const int parity = (int)(s & 1u);
   float acc = 0.f;
+  bool dead = false;  // one timed-out peer: do not wait for the others again
   for (int p = 0; p < x.world; ++p) {
     uint64_t* slot = xgmi_slot(x.local, parity, p, x.world, x.max_elems, i);
     uint64_t w = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    uint32_t polls = 0;
+    uint32_t polls = dead ? kXgmiMaxPolls : 0;
     while ((uint32_t)(w >> 32) != s) {
       if (++polls > kXgmiMaxPolls) {  // ~seconds: a peer is gone; fail loudly, never hang
         __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        dead = true;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
@@ -87,15 +89,17 @@ __device__ __forceinline__ float xgmi_gather_sum(const XgmiArgs& x, uint32_t s, 
 __device__ __forceinline__ void xgmi_gather_lds(const XgmiArgs& x, uint32_t s, int i0, int n, float* tmp,
                                                 int tid, int nt, int* lds_flag = nullptr) {
   const int parity = (int)(s & 1u);
+  bool dead = false;  // after one timed-out slot this thread stops waiting: bounded total stall
   for (int e = tid; e < x.world * n; e += nt) {
     const int p = e / n, i = e - p * n;
     uint64_t* slot = xgmi_slot(x.local, parity, p, x.world, x.max_elems, i0 + i);
     uint64_t w = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    uint32_t polls = 0;
+    uint32_t polls = dead ? kXgmiMaxPolls : 0;
     while ((uint32_t)(w >> 32) != s) {
       if (++polls > kXgmiMaxPolls) {
         __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (lds_flag) *lds_flag = 1;
+        dead = true;
         break;
       }
       __builtin_amdgcn_s_sleep(1);

@@ -173,7 +173,7 @@ struct GemmArgs {
 };
 hipError_t gemm(const GemmArgs& g, hipStream_t s);
 
-// Large-shape bf16 GEMM (csrc/kernels/gemm_big.hip): C = alpha*A.Bt^T (+beta*C)(+bias)(ReLU),
+// Throughput bf16 GEMM (csrc/kernels/gemm_big.hip): C = alpha*A.Bt^T (+beta*C)(+bias)(ReLU),
 // A [M,K] and Bt [N,K] both K-contiguous bf16, C f32 or bf16 with row stride ldc.
 struct BigGemmArgs {
   int M, N, K;
@@ -184,7 +184,9 @@ struct BigGemmArgs {
   const void* bias; int bias_dtype;
   int relu;
   float alpha, beta;
-  int sched;  // 0: read-then-multiply per K-tile, 1: ping-pong wave pairs (default)
+  int sched;    // 0: read-then-multiply per K-tile, 1: ping-pong wave pairs (default, 256 tile)
+  int tile;     // 256: 256x256 block tile (8 waves), 128: 128x128 (4 waves, 2 workgroups per CU)
+  int split_k;  // >1: K split over gridDim.y, fp32 atomics into a pre-zeroed f32 C (no ReLU/beta)
 };
 bool gemm_bf16_big_supported(int M, int N, int K, int64_t lda, int64_t ldb, const void* A, const void* Bt);
 hipError_t gemm_bf16_big(const BigGemmArgs& g, hipStream_t s);

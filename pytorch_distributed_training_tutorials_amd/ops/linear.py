@@ -12,8 +12,9 @@ Backward : dx = (dy * relu'(y)) W      -- ReLU mask applied while staging dy
 Long-K / tiny-MN shapes (ToyModel's K=10000, M=20, N=10) run split-K over
 workgroups with fp32 atomics so the launch has enough workgroups to fill the
 chip instead of one workgroup walking 10000 columns.
-Large bf16 shapes (K % 64 == 0, >= 2^24 MACs) run the 256x256 LDS-DMA kernel
-(csrc/kernels/gemm_big.hip, ~1.1 PFLOP/s at 4096^3): the forward directly on
+Large bf16 shapes (K % 64 == 0, >= 2^24 MACs) run the LDS-DMA kernel
+(csrc/kernels/gemm_big.hip: 256x256 tiles ~1.1 PFLOP/s at 4096^3, 128x128 tiles
+and split-K when fewer tiles than CUs, ``plan_big``): the forward directly on
 nn.Linear's [out, in] weight, the backward GEMMs on K-contiguous copies (the
 transposes cost a few % of the GEMM), with the ReLU mask and bias gradient as
 separate elementwise / column-sum kernels.
@@ -47,16 +48,49 @@ _BIG_MIN_MACS = 1 << 24
 
 
 def _big(M: int, N: int, K: int, dtype) -> bool:
-    """Use the 256x256 kernel: bf16, K a multiple of its 64-deep K-tile, enough work."""
+    """Use the LDS-DMA kernel: bf16, K a multiple of its 64-deep K-tile, enough work."""
     return dtype == torch.bfloat16 and K >= 64 and K % 64 == 0 and M * N * K >= _BIG_MIN_MACS
 
 
-def gemm_nt_big(A: torch.Tensor, Bt: torch.Tensor, out_dtype, bias=None, relu: bool = False) -> torch.Tensor:
-    """C = A @ Bt^T on the 256x256 kernel (A [M,K], Bt [N,K], both made K-contiguous)."""
+def plan_big(M: int, N: int, K: int) -> tuple[int, int]:
+    """(block tile, split-K) for gemm_big.hip, from profiles/r1_gemm_bench_v2.jsonl:
+    256x256 tiles when they fill the 256 CUs; else 128x128 tiles (two workgroups
+    per CU); split-K only when one slice-less 128 pass would run long (the zero
+    fill + f32 atomics + cast cost ~10 us), at most one workgroup per CU and
+    >= 4 K-tiles per slice."""
+    nk = K // 64
+    t256 = math.ceil(M / 256) * math.ceil(N / 256)
+    if t256 >= _BIG256_MIN_TILES:
+        return 256, 1
+    t128 = math.ceil(M / 128) * math.ceil(N / 128)
+    waves = math.ceil(t128 / (2 * _CUS))
+    est_us = _KTILE_US * nk * waves
+    if t128 >= _CUS or est_us < _SPLIT_MIN_US:
+        return 128, 1
+    split = max(1, min(_CUS // t128, nk // 4, 16))
+    return 128, split
+
+
+_BIG256_MIN_TILES = 192
+_KTILE_US = 0.85      # one 128x128x64 K-tile step of a workgroup (measured, 2048^3)
+_SPLIT_MIN_US = 25.0
+
+
+def gemm_nt_big(A: torch.Tensor, Bt: torch.Tensor, out_dtype, bias=None, relu: bool = False,
+                plan: tuple[int, int] | None = None) -> torch.Tensor:
+    """C = A @ Bt^T on the LDS-DMA kernel (A [M,K], Bt [N,K], both made K-contiguous)."""
     A = A if A.stride(-1) == 1 and A.stride(0) % 8 == 0 else A.contiguous()
     Bt = Bt if Bt.stride(-1) == 1 and Bt.stride(0) % 8 == 0 else Bt.contiguous()
-    C = torch.empty((A.shape[0], Bt.shape[0]), device=A.device, dtype=out_dtype)
-    native().gemm_big_(A, Bt, C, bias, relu)
+    M, N = A.shape[0], Bt.shape[0]
+    tile, split = plan or plan_big(M, N, A.shape[1])
+    if split > 1:  # fp32 atomics into a zeroed accumulator, ReLU/cast after
+        acc = torch.zeros((M, N), device=A.device, dtype=torch.float32)
+        native().gemm_big_(A, Bt, acc, bias, False, tile=tile, split_k=split)
+        if relu:
+            acc.relu_()
+        return acc if out_dtype == torch.float32 else acc.to(out_dtype)
+    C = torch.empty((M, N), device=A.device, dtype=out_dtype)
+    native().gemm_big_(A, Bt, C, bias, relu, tile=tile)
     return C
 
 

@@ -141,6 +141,58 @@ def test_gemm_big_matches_fp32(native, dev, M, N, K, out_dtype, sched):
     torch.testing.assert_close(C1.float(), F.relu(0.5 * ref + 2.0 * C0.float() + bias), rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (512, 768, 1024), (300, 200, 128), (120, 1000, 2048),
+                                   (1, 257, 64), (1000, 17, 192)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_gemm_big_tile128_matches_fp32(native, dev, M, N, K, out_dtype):
+    """128x128-tile variant (4 waves): same contract as the 256 tile, edges clamped."""
+    torch.manual_seed(M * 5 + N + K)
+    A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    Bt = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    ref = A.float() @ Bt.float().t()
+    tol = 1e-4 * math.sqrt(K) if out_dtype == torch.float32 else 1e-2 * math.sqrt(K) / 8
+    bias = torch.randn(N, device=dev)
+    C0 = torch.randn(M, N, device=dev).to(out_dtype)
+    C1 = C0.clone()
+    native.gemm_big_(A, Bt, C1, bias, True, 0.5, 2.0, tile=128)
+    torch.testing.assert_close(C1.float(), F.relu(0.5 * ref + 2.0 * C0.float() + bias), rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("tile", [128, 256])
+@pytest.mark.parametrize("split", [2, 3, 7, 32])
+def test_gemm_big_split_k(native, dev, tile, split):
+    """split-K slices atomically accumulate into a zeroed f32 C; bias added once (slice 0);
+    uneven slices (K-tiles not divisible by the split) and more slices than K-tiles clamp."""
+    M, N, K = 200, 300, 64 * 13
+    torch.manual_seed(split + tile)
+    A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    Bt = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    C = torch.zeros(M, N, device=dev)
+    native.gemm_big_(A, Bt, C, bias, False, 0.5, tile=tile, split_k=split)
+    ref = 0.5 * (A.float() @ Bt.float().t()) + bias
+    torch.testing.assert_close(C, ref, rtol=1e-3, atol=1e-3)
+    with pytest.raises(RuntimeError):  # atomics need an f32 accumulator
+        native.gemm_big_(A, Bt, torch.zeros(M, N, device=dev, dtype=torch.bfloat16), tile=tile, split_k=split)
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 256), (2048, 2048, 2048), (120, 1000, 2048), (256, 512, 4096)])
+def test_gemm_nt_big_planner(dev, M, N, K):
+    """ops.linear.gemm_nt_big picks (tile, split) by shape; every plan gives the fp32 result."""
+    from pytorch_distributed_training_tutorials_amd.ops.linear import gemm_nt_big, plan_big
+
+    torch.manual_seed(1)
+    A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    Bt = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev).to(torch.bfloat16)
+    ref = F.relu(A.float() @ Bt.float().t() + bias.float())
+    tile, split = plan_big(M, N, K)
+    assert tile in (128, 256) and split >= 1
+    out = gemm_nt_big(A, Bt, torch.bfloat16, bias=bias, relu=True)
+    tol = 1e-2 * math.sqrt(K) / 8
+    torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol)
+
+
 def test_gemm_big_identity_and_strides(native, dev):
     """A = I picks rows of Bt exactly; strided (sliced) operands use their row stride."""
     K = 128
