@@ -5,6 +5,9 @@
 // before launching (a bad launch on MI355X can reset the whole node) and
 // launches on the caller's current HIP stream, so all of them are capturable
 // into hipGraphs via torch.cuda.graph.
+#include <map>
+#include <mutex>
+#include <utility>
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/hip/HIPGuard.h>
@@ -599,6 +602,176 @@ Tensor bn_relu(Tensor x, Tensor scale, Tensor shift, bool relu) {
   return y;
 }
 
+// ------------------------------------------------------------- batchnorm
+// Activations as [M, C] rows: NHWC (channels_last-contiguous 4D) or contiguous 2D.
+void bn_rows(const Tensor& x, int64_t* M, int* C) {
+  TORCH_CHECK(x.is_cuda(), "batchnorm: GPU tensor expected");
+  if (x.dim() == 2) {
+    TORCH_CHECK(x.is_contiguous(), "batchnorm: 2D input must be contiguous");
+  } else {
+    TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "batchnorm: 4D input must be channels_last-contiguous (NHWC)");
+  }
+  *C = (int)x.size(1);
+  *M = x.numel() / std::max<int64_t>(*C, 1);
+  const int V = x.scalar_type() == at::kFloat ? 4 : 8;
+  TORCH_CHECK(*C % V == 0, "batchnorm: channels must be a multiple of ", V);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "batchnorm: 16-byte aligned data expected");
+}
+
+void same_rows(const Tensor& a, const Tensor& x, const char* name) {
+  TORCH_CHECK(a.defined() && a.sizes() == x.sizes() && a.strides() == x.strides() &&
+                  a.scalar_type() == x.scalar_type() && a.device() == x.device(),
+              "batchnorm: ", name, " must match x (shape, strides, dtype, device)");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(a.data_ptr()) % 16 == 0, "batchnorm: ", name, " not 16-byte aligned");
+}
+
+// Ticket array for the last-block hand-off: the caller's (a zeroed int32 tensor
+// owned by the BN module, so two modules never share one), else one per device
+// created outside graph capture. The kernels re-arm what they use.
+int* bn_tickets(const Tensor& x, const c10::optional<Tensor>& given, int need) {
+  if (given.has_value() && given->defined()) {
+    TORCH_CHECK(given->is_cuda() && given->device() == x.device() && given->scalar_type() == at::kInt &&
+                    given->is_contiguous() && given->numel() >= need,
+                "batchnorm: tickets must be a zeroed int32 tensor of >= ", need, " elements on x's device");
+    return given->data_ptr<int>();
+  }
+  static std::mutex mu;
+  static std::map<int, int*> per_device;
+  constexpr int kMax = 1024;
+  TORCH_CHECK(need <= kMax, "batchnorm: too many channel tiles");
+  std::lock_guard<std::mutex> g(mu);
+  const int dev = (int)x.device().index();
+  auto it = per_device.find(dev);
+  if (it != per_device.end()) return it->second;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  hip_check(hipStreamIsCapturing(cur_stream(x), &st), "hipStreamIsCapturing");
+  TORCH_CHECK(st == hipStreamCaptureStatusNone,
+              "batchnorm: pass a tickets tensor (ops.norm.BatchNorm2d does) or run once before graph capture");
+  int* t = nullptr;
+  hip_check(hipMalloc(&t, kMax * sizeof(int)), "hipMalloc(bn tickets)");
+  hip_check(hipMemset(t, 0, kMax * sizeof(int)), "hipMemset(bn tickets)");
+  per_device[dev] = t;
+  return t;
+}
+
+const float* opt_f32(const c10::optional<Tensor>& t, int64_t C, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C,
+              "batchnorm: ", name, " must be a contiguous f32 GPU tensor of C elements");
+  return t->data_ptr<float>();
+}
+
+// Training forward: returns (y, stats[4, C] = mean, invstd, scale, shift).
+std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> weight, c10::optional<Tensor> bias,
+                                 c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var,
+                                 c10::optional<Tensor> num_batches_tracked, c10::optional<Tensor> residual, bool relu,
+                                 double momentum, double eps, c10::optional<Tensor> tickets) {
+  int64_t M;
+  int C;
+  bn_rows(x, &M, &C);
+  c10::hip::HIPGuard guard(x.device().index());
+  BnFwdArgs a{};
+  a.x = x.data_ptr();
+  if (residual.has_value() && residual->defined()) {
+    same_rows(*residual, x, "residual");
+    a.residual = residual->data_ptr();
+  }
+  Tensor y = at::empty_like(x);
+  Tensor stats = at::empty({4, C}, x.options().dtype(at::kFloat));
+  Tensor ws = at::empty({bn_workspace_floats(M, C, dt_of(x))}, x.options().dtype(at::kFloat));
+  a.y = y.data_ptr();
+  a.dtype = dt_of(x);
+  a.M = M;
+  a.C = C;
+  a.relu = relu ? 1 : 0;
+  a.workspace = ws.data_ptr<float>();
+  a.tickets = bn_tickets(x, tickets, bn_num_tickets(C, a.dtype));
+  a.p.weight = opt_f32(weight, C, "weight");
+  a.p.bias = opt_f32(bias, C, "bias");
+  a.p.running_mean = const_cast<float*>(opt_f32(running_mean, C, "running_mean"));
+  a.p.running_var = const_cast<float*>(opt_f32(running_var, C, "running_var"));
+  TORCH_CHECK((a.p.running_mean == nullptr) == (a.p.running_var == nullptr), "batchnorm: running_mean/var together");
+  if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
+    TORCH_CHECK(num_batches_tracked->is_cuda() && num_batches_tracked->scalar_type() == at::kLong &&
+                num_batches_tracked->numel() == 1, "batchnorm: num_batches_tracked must be a 1-element int64 tensor");
+    a.p.num_batches_tracked = num_batches_tracked->data_ptr<int64_t>();
+  }
+  a.p.momentum = (float)momentum;
+  a.p.eps = (float)eps;
+  float* st = stats.data_ptr<float>();
+  a.p.mean = st;
+  a.p.invstd = st + C;
+  a.p.scale = st + 2 * C;
+  a.p.shift = st + 3 * C;
+  hip_check(bn_forward_train(a, cur_stream(x)), "bn_forward_train");
+  return {y, stats};
+}
+
+// Backward: returns (dx, dweight, dbias, dres); dres undefined unless want_dres.
+std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::optional<Tensor> weight, Tensor stats,
+                           bool relu, bool want_dres, bool want_dweight, c10::optional<Tensor> tickets) {
+  int64_t M;
+  int C;
+  bn_rows(x, &M, &C);
+  same_rows(dy, x, "dy");
+  c10::hip::HIPGuard guard(x.device().index());
+  TORCH_CHECK(stats.is_cuda() && stats.scalar_type() == at::kFloat && stats.is_contiguous() && stats.numel() == 4 * C,
+              "batchnorm: stats must be the [4, C] forward statistics");
+  BnBwdArgs a{};
+  a.dy = dy.data_ptr();
+  a.x = x.data_ptr();
+  if (relu) {
+    TORCH_CHECK(y.has_value() && y->defined(), "batchnorm: relu backward needs the forward output");
+    same_rows(*y, x, "y");
+    a.y = y->data_ptr();
+  }
+  Tensor dx = at::empty_like(x);
+  Tensor dres = want_dres ? at::empty_like(x) : Tensor();
+  Tensor dwb = at::empty({5, C}, x.options().dtype(at::kFloat));  // dweight, dbias, A, B, C
+  Tensor ws = at::empty({bn_workspace_floats(M, C, dt_of(x))}, x.options().dtype(at::kFloat));
+  a.dx = dx.data_ptr();
+  a.dres = want_dres ? dres.data_ptr() : nullptr;
+  a.dtype = dt_of(x);
+  a.M = M;
+  a.C = C;
+  a.relu = relu ? 1 : 0;
+  a.workspace = ws.data_ptr<float>();
+  a.tickets = bn_tickets(x, tickets, bn_num_tickets(C, a.dtype));
+  const float* st = stats.data_ptr<float>();
+  a.p.weight = opt_f32(weight, C, "weight");
+  a.p.mean = st;
+  a.p.invstd = st + C;
+  float* d = dwb.data_ptr<float>();
+  a.p.dweight = want_dweight ? d : nullptr;
+  a.p.dbias = want_dweight ? d + C : nullptr;
+  a.p.coef_a = d + 2 * C;
+  a.p.coef_b = d + 3 * C;
+  a.p.coef_c = d + 4 * C;
+  hip_check(bn_backward(a, cur_stream(x)), "bn_backward");
+  Tensor dw = want_dweight ? dwb[0] : Tensor();
+  Tensor db = want_dweight ? dwb[1] : Tensor();
+  return {dx, dw, db, dres};
+}
+
+// y = ReLU?(x*scale + shift (+ residual)), per channel (eval-mode BN).
+Tensor bn_apply_(Tensor x, c10::optional<Tensor> residual, Tensor scale, Tensor shift, bool relu) {
+  int64_t M;
+  int C;
+  bn_rows(x, &M, &C);
+  c10::hip::HIPGuard guard(x.device().index());
+  const void* r = nullptr;
+  if (residual.has_value() && residual->defined()) {
+    same_rows(*residual, x, "residual");
+    r = residual->data_ptr();
+  }
+  const float* sc = opt_f32(scale, C, "scale");
+  const float* sf = opt_f32(shift, C, "shift");
+  Tensor y = at::empty_like(x);
+  hip_check(bn_apply(x.data_ptr(), r, y.data_ptr(), dt_of(x), sc, sf, M, C, relu ? 1 : 0, cur_stream(x)), "bn_apply");
+  return y;
+}
+
 // ------------------------------------------------------------- comm
 ncclDataType_t nccl_dt(const Tensor& t) {
   switch (t.scalar_type()) {
@@ -670,6 +843,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("quantize_int8", &quantize_int8);
   m.def("int8_linear", &int8_linear);
   m.def("bn_relu", &bn_relu);
+  m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
+        py::arg("running_var"), py::arg("num_batches_tracked"), py::arg("residual"), py::arg("relu"),
+        py::arg("momentum"), py::arg("eps"), py::arg("tickets") = py::none());
+  m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("weight"), py::arg("stats"),
+        py::arg("relu"), py::arg("want_dres"), py::arg("want_dweight"), py::arg("tickets") = py::none());
+  m.def("bn_apply", &bn_apply_, py::arg("x"), py::arg("residual"), py::arg("scale"), py::arg("shift"),
+        py::arg("relu"));
 
   m.def("plan_buckets", &plan_buckets);
 

@@ -1,0 +1,534 @@
+// Training-mode BatchNorm over channels-last activations with the ResNet
+// epilogues fused: y = ReLU?(BN(x) + residual?), and its backward.
+//
+// Why (profiles/r1_resnet_window.md): in the ResNet-50 DDP step (bf16,
+// channels_last, B=128) MIOpen's BatchNorm kernels plus the separate ReLU
+// (clamp), residual add, ReLU-backward (threshold) and MIOpen's SubTensorOp
+// passes take ~12 ms of a ~27 ms step -- all of it HBM-bound elementwise and
+// reduction traffic over 11.1 M activations per image. Fusing the epilogues
+// drops whole read/write passes; the reductions are written for the NHWC
+// layout, where one activation row is C contiguous channels.
+//
+// Layout: x is [M, C] with unit channel stride (NHWC channels_last, M = N*H*W,
+// or a plain [M, C] batch), bf16 or f32; weight/bias/statistics f32.
+//
+// Each pass loads 16 B per lane (8 bf16 / 4 f32 channels). A reduction launch is
+// grid (row blocks, channel tiles): threads of a block cover TC channel vectors
+// x RPI rows and walk the block's row range; partial sums are combined in LDS,
+// written per row block, and the LAST row block of each channel tile to finish
+// (atomic ticket, agent-scope fences across the XCD L2s) reduces the partials
+// in fixed order (deterministic), computes the per-channel coefficients and
+// re-arms its ticket. So a BN forward is 2 launches (stats, apply) and a
+// backward 2 launches (reduce, apply).
+//
+// Forward statistics use shifted sums (x - K, K = row 0 of the channel), so
+// E[(x-K)^2] - E[x-K]^2 does not cancel catastrophically for |mean| >> std;
+// the final combine runs in double. Running stats: torch's momentum update
+// with the unbiased variance, num_batches_tracked incremented in-kernel.
+//
+// Backward (dy' = dy * [y > 0] with ReLU):
+//   dbeta = sum dy',  dgamma = invstd * sum dy' (x - mean)
+//   dx    = k dy' - k s2 (x - mean) - k s1,   k = gamma invstd,
+//           s1 = dbeta / M, s2 = invstd^2 sum dy'(x - mean) / M
+// i.e. dx = A dy' + B x + C per channel; with a residual branch d(residual) = dy'.
+#include "common.h"
+#include "kernels.h"
+
+namespace ptdt {
+namespace {
+
+constexpr int kThreads = 256;   // apply kernels
+constexpr int kRed = 512;       // reduction kernels
+constexpr int kMaxTC = 8;       // channel vectors per block row: 64 bf16 / 32 f32 channels per tile
+constexpr int kRedBlocks = 384; // ~1.5 reduction blocks per CU
+constexpr int kMaxGx = 256;     // row blocks per channel tile (bounds the last block's combine)
+
+template <typename T>
+struct VecIO {
+  static constexpr int V = 16 / sizeof(T);
+  __device__ __forceinline__ static void load(const T* p, float (&v)[V]) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    if constexpr (sizeof(T) == 4) {
+      v[0] = __uint_as_float(u.x); v[1] = __uint_as_float(u.y);
+      v[2] = __uint_as_float(u.z); v[3] = __uint_as_float(u.w);
+    } else {
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[2 * i] = __uint_as_float(w[i] << 16);
+        v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+      }
+    }
+  }
+  __device__ __forceinline__ static void store(T* p, const float (&v)[V]) {
+    uint4 u;
+    if constexpr (sizeof(T) == 4) {
+      u.x = __float_as_uint(v[0]); u.y = __float_as_uint(v[1]);
+      u.z = __float_as_uint(v[2]); u.w = __float_as_uint(v[3]);
+    } else {
+      uint32_t w[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f32_to_bf16(v[2 * i]) | ((uint32_t)f32_to_bf16(v[2 * i + 1]) << 16);
+      u.x = w[0]; u.y = w[1]; u.z = w[2]; u.w = w[3];
+    }
+    *reinterpret_cast<uint4*>(p) = u;
+  }
+};
+
+struct Geom {
+  int TC, RPI;       // channel vectors per row, rows per block iteration
+  int gx, gy;        // row blocks, channel tiles
+  int64_t rows_per_block;
+};
+
+template <typename T>
+Geom geom(int64_t M, int C) {
+  constexpr int V = VecIO<T>::V;
+  Geom g;
+  const int cv = C / V;
+  g.TC = cv < kMaxTC ? cv : kMaxTC;
+  g.RPI = kRed / g.TC;
+  g.gy = (cv + g.TC - 1) / g.TC;
+  int64_t want = (M + (int64_t)g.RPI * 16 - 1) / ((int64_t)g.RPI * 16);  // >= 16 rows per thread
+  int64_t cap = kRedBlocks / g.gy;
+  if (cap > kMaxGx) cap = kMaxGx;
+  if (cap < 1) cap = 1;
+  g.gx = (int)(want < 1 ? 1 : (want > cap ? cap : want));
+  g.rows_per_block = (M + g.gx - 1) / g.gx;
+  g.gx = (int)((M + g.rows_per_block - 1) / g.rows_per_block);
+  return g;
+}
+
+// Block-level combine of per-thread V-vectors over the RPI rows sharing a channel
+// vector; returns (in threads t < TC*V) the block's sum for channel c0 + t.
+template <int V, int NS>
+__device__ __forceinline__ void block_rows_sum(float (&acc)[NS][V], float* sh, int TC, int RPI, float (&out)[NS]) {
+  const int tid = threadIdx.x;
+  const int width = TC * V;
+  const int rr = tid / TC, tc = tid % TC;
+  if (rr < RPI) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int v = 0; v < V; ++v) sh[(s * RPI + rr) * width + tc * V + v] = acc[s][v];
+  }
+  __syncthreads();
+  if (tid < width) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      float a = 0.f;
+      for (int r = 0; r < RPI; ++r) a += sh[(s * RPI + r) * width + tid];
+      out[s] = a;
+    }
+  }
+}
+
+// Last block of a channel tile: sum the gx row-block partials (two [gx][C] slabs)
+// of the tile's `width` channels with ALL threads -- thread (part, ch) adds
+// partials part, part + P, ... with 4 loads in flight, then the P part-sums are
+// added in part order through LDS (deterministic). Result in threads t < width.
+__device__ __forceinline__ void combine_partials(const float* ws, int gx, int C, int cbase, int width, float* sh,
+                                                 double& s0, double& s1) {
+  const int P = kRed / width;
+  const int t = threadIdx.x, ch = t % width, part = t / width;
+  const int c = cbase + ch;
+  double a0 = 0.0, a1 = 0.0;
+  const float* w0 = ws;
+  const float* w1 = ws + (int64_t)gx * C;
+  if (part < P && c < C) {
+    int b = part;
+    for (; b + 3 * P < gx; b += 4 * P) {
+      float u[4], v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        u[k] = w0[(int64_t)(b + k * P) * C + c];
+        v[k] = w1[(int64_t)(b + k * P) * C + c];
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        a0 += (double)u[k];
+        a1 += (double)v[k];
+      }
+    }
+    for (; b < gx; b += P) {
+      a0 += (double)w0[(int64_t)b * C + c];
+      a1 += (double)w1[(int64_t)b * C + c];
+    }
+  }
+  __syncthreads();  // the reduction slots in sh are free again
+  double* d = reinterpret_cast<double*>(sh);
+  if (part < P) {
+    d[part * width + ch] = a0;
+    d[(P + part) * width + ch] = a1;
+  }
+  __syncthreads();
+  s0 = s1 = 0.0;
+  if (t < width) {
+    for (int q = 0; q < P; ++q) {
+      s0 += d[q * width + t];
+      s1 += d[(P + q) * width + t];
+    }
+  }
+}
+
+// Atomic ticket: true in exactly one block per channel tile (the last to arrive),
+// after every block's partials are visible to it. The hand-off recipe of
+// cdna_hip_programming.md §6 G16 (per-XCD L2s are not coherent): plain partial
+// stores drained by every wave, barrier, lane 0 agent-scope release + drain, then
+// the relaxed agent-scope ticket; the last arriver's lane 0 agent-scope acquire
+// + drain, barrier, plain loads. The flag travels through the kernel's one LDS array.
+__device__ __forceinline__ bool last_block(int* ticket, int* sh_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == (int)gridDim.x - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *sh_flag = last;
+  }
+  __syncthreads();
+  return *sh_flag != 0;
+}
+
+__device__ __forceinline__ void rearm(int* ticket) {
+  __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kRed) bn_stats_kernel(const T* __restrict__ x, int64_t M, int C, int TC, int RPI,
+                                                        int64_t rows_per_block, float* ws, int* tickets, BnParams p) {
+  constexpr int V = VecIO<T>::V;
+  constexpr int U = 8;  // rows in flight per thread
+  extern __shared__ float sh[];  // 2 x RPI x TC*V reduction slots, then the last-block flag
+  int* flag = reinterpret_cast<int*>(sh + 2 * kRed * V);
+  const int tid = threadIdx.x, rr = tid / TC, tc = tid % TC;
+  const int c0 = (blockIdx.y * TC + tc) * V;  // this thread's channels c0..c0+V
+  const bool active = rr < RPI && c0 < C;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  float acc[2][V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) acc[0][v] = acc[1][v] = 0.f;
+  if (active) {
+    float K[V];
+    VecIO<T>::load(x + c0, K);  // pivot: row 0 (same for every block)
+    int64_t r = r0 + rr;
+    for (; r + (U - 1) * RPI < r1; r += U * RPI) {  // U independent 16-B loads in flight
+      float a[U][V];
+#pragma unroll
+      for (int u = 0; u < U; ++u) VecIO<T>::load(x + (r + u * RPI) * C + c0, a[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const float d = a[u][v] - K[v];
+          acc[0][v] += d;
+          acc[1][v] = fmaf(d, d, acc[1][v]);
+        }
+    }
+    for (; r < r1; r += RPI) {
+      float a[V];
+      VecIO<T>::load(x + r * C + c0, a);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const float d = a[v] - K[v];
+        acc[0][v] += d;
+        acc[1][v] = fmaf(d, d, acc[1][v]);
+      }
+    }
+  }
+  float part[2];
+  block_rows_sum<V, 2>(acc, sh, TC, RPI, part);
+  const int width = TC * V;
+  const int c = blockIdx.y * width + tid;
+  if (tid < width && c < C) {
+    ws[(int64_t)blockIdx.x * C + c] = part[0];
+    ws[((int64_t)gridDim.x + blockIdx.x) * C + c] = part[1];
+  }
+  if (!last_block(tickets + blockIdx.y, flag)) return;
+  double s, q;
+  combine_partials(ws, (int)gridDim.x, C, blockIdx.y * width, width, sh, s, q);
+  if (tid < width && c < C) {
+    const double Kc = (double)Cvt<T>::load(x, c);
+    const double ms = s / (double)M;
+    double var = q / (double)M - ms * ms;
+    if (var < 0.0) var = 0.0;
+    const double mean = Kc + ms;
+    const float invstd = (float)(1.0 / sqrt(var + (double)p.eps));
+    const float w = p.weight ? p.weight[c] : 1.f, b = p.bias ? p.bias[c] : 0.f;
+    p.mean[c] = (float)mean;
+    p.invstd[c] = invstd;
+    p.scale[c] = w * invstd;
+    p.shift[c] = b - (float)mean * w * invstd;
+    if (p.running_mean) {
+      const double unbiased = M > 1 ? var * (double)M / (double)(M - 1) : var;
+      p.running_mean[c] = (float)((1.0 - p.momentum) * p.running_mean[c] + p.momentum * mean);
+      p.running_var[c] = (float)((1.0 - p.momentum) * p.running_var[c] + p.momentum * unbiased);
+    }
+  }
+  if (tid == 0) {
+    rearm(tickets + blockIdx.y);  // for the next launch (stream order)
+    if (blockIdx.y == 0 && p.num_batches_tracked) *p.num_batches_tracked += 1;
+  }
+}
+
+template <typename T, bool RELU, bool RES>
+__global__ void __launch_bounds__(kThreads) bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
+                                                            T* __restrict__ y, const float* __restrict__ scale,
+                                                            const float* __restrict__ shift, int64_t nvec, int C) {
+  constexpr int V = VecIO<T>::V;
+  extern __shared__ float sh[];  // scale[C], shift[C]
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    sh[c] = scale[c];
+    sh[C + c] = shift[c];
+  }
+  __syncthreads();
+  const int cv = C / V;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+    const int c0 = (int)(i % cv) * V;
+    float a[V];
+    VecIO<T>::load(x + i * V, a);
+    float rv[V];
+    if constexpr (RES) VecIO<T>::load(res + i * V, rv);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float o = fmaf(a[v], sh[c0 + v], sh[C + c0 + v]);
+      if constexpr (RES) o += rv[v];
+      if constexpr (RELU) o = fmaxf(o, 0.f);
+      a[v] = o;
+    }
+    VecIO<T>::store(y + i * V, a);
+  }
+}
+
+template <typename T, bool RELU>
+__global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                             const T* __restrict__ y, int64_t M, int C, int TC,
+                                                             int RPI, int64_t rows_per_block, float* ws,
+                                                             int* tickets, BnBwdParams p) {
+  constexpr int V = VecIO<T>::V;
+  constexpr int U = 4;  // rows in flight per thread (x 2-3 loads each)
+  extern __shared__ float sh[];
+  int* flag = reinterpret_cast<int*>(sh + 2 * kRed * V);
+  const int tid = threadIdx.x, rr = tid / TC, tc = tid % TC;
+  const int c0 = (blockIdx.y * TC + tc) * V;
+  const bool active = rr < RPI && c0 < C;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
+  float acc[2][V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) acc[0][v] = acc[1][v] = 0.f;
+  if (active) {
+    float mu[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) mu[v] = p.mean[c0 + v];
+    int64_t r = r0 + rr;
+    for (; r + (U - 1) * RPI < r1; r += U * RPI) {
+      float g[U][V], a[U][V], o[U][V];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t off = (r + u * RPI) * C + c0;
+        VecIO<T>::load(dy + off, g[u]);
+        VecIO<T>::load(x + off, a[u]);
+        if constexpr (RELU) VecIO<T>::load(y + off, o[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const float gg = RELU ? (o[u][v] > 0.f ? g[u][v] : 0.f) : g[u][v];
+          acc[0][v] += gg;
+          acc[1][v] = fmaf(gg, a[u][v] - mu[v], acc[1][v]);
+        }
+    }
+    for (; r < r1; r += RPI) {
+      float g[V], a[V], o[V];
+      const int64_t off = r * C + c0;
+      VecIO<T>::load(dy + off, g);
+      VecIO<T>::load(x + off, a);
+      if constexpr (RELU) VecIO<T>::load(y + off, o);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const float gg = RELU ? (o[v] > 0.f ? g[v] : 0.f) : g[v];
+        acc[0][v] += gg;
+        acc[1][v] = fmaf(gg, a[v] - mu[v], acc[1][v]);
+      }
+    }
+  }
+  float part[2];
+  block_rows_sum<V, 2>(acc, sh, TC, RPI, part);
+  const int width = TC * V;
+  const int c = blockIdx.y * width + tid;
+  if (tid < width && c < C) {
+    ws[(int64_t)blockIdx.x * C + c] = part[0];
+    ws[((int64_t)gridDim.x + blockIdx.x) * C + c] = part[1];
+  }
+  if (!last_block(tickets + blockIdx.y, flag)) return;
+  double sdy, sdx;
+  combine_partials(ws, (int)gridDim.x, C, blockIdx.y * width, width, sh, sdy, sdx);
+  if (tid < width && c < C) {
+    const double invstd = p.invstd[c], mean = p.mean[c];
+    const double w = p.weight ? p.weight[c] : 1.0;
+    if (p.dweight) p.dweight[c] = (float)(sdx * invstd);
+    if (p.dbias) p.dbias[c] = (float)sdy;
+    const double k = w * invstd, s1 = sdy / (double)M, s2 = invstd * invstd * sdx / (double)M;
+    p.coef_a[c] = (float)k;
+    p.coef_b[c] = (float)(-k * s2);
+    p.coef_c[c] = (float)(k * s2 * mean - k * s1);
+  }
+  if (tid == 0) rearm(tickets + blockIdx.y);
+}
+
+template <typename T, bool RELU, bool RES>
+__global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+                                                                const T* __restrict__ y, T* __restrict__ dx,
+                                                                T* __restrict__ dres, const float* __restrict__ ca,
+                                                                const float* __restrict__ cb,
+                                                                const float* __restrict__ cc, int64_t nvec, int C) {
+  constexpr int V = VecIO<T>::V;
+  extern __shared__ float sh[];  // A[C], B[C], C[C]
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    sh[c] = ca[c];
+    sh[C + c] = cb[c];
+    sh[2 * C + c] = cc[c];
+  }
+  __syncthreads();
+  const int cv = C / V;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
+    const int c0 = (int)(i % cv) * V;
+    float g[V], a[V], o[V];
+    VecIO<T>::load(dy + i * V, g);
+    VecIO<T>::load(x + i * V, a);
+    if constexpr (RELU) VecIO<T>::load(y + i * V, o);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      if constexpr (RELU) g[v] = o[v] > 0.f ? g[v] : 0.f;
+      a[v] = fmaf(sh[c0 + v], g[v], fmaf(sh[C + c0 + v], a[v], sh[2 * C + c0 + v]));
+    }
+    VecIO<T>::store(dx + i * V, a);
+    if constexpr (RES) VecIO<T>::store(dres + i * V, g);
+  }
+}
+
+int apply_grid(int64_t nvec) {
+  int64_t b = (nvec + kThreads * 4 - 1) / (kThreads * 4);  // >= 4 vectors per thread
+  if (b > 4096) b = 4096;
+  return (int)(b < 1 ? 1 : b);
+}
+
+template <typename T>
+hipError_t fwd_impl(const BnFwdArgs& a, hipStream_t s) {
+  constexpr int V = VecIO<T>::V;
+  if (a.C % V != 0) return hipErrorInvalidValue;
+  const Geom g = geom<T>(a.M, a.C);
+  const size_t sh_red = (size_t)2 * kRed * V * sizeof(float) + 16;
+  hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(g.gx, g.gy), dim3(kRed), sh_red, s, static_cast<const T*>(a.x),
+                     a.M, a.C, g.TC, g.RPI, g.rows_per_block, a.workspace, a.tickets, a.p);
+  PTDT_HIP_CHECK(hipGetLastError());
+  const int64_t nvec = a.M * a.C / V;
+  const size_t sh_ap = (size_t)2 * a.C * sizeof(float);
+  const T* x = static_cast<const T*>(a.x);
+  const T* r = static_cast<const T*>(a.residual);
+  T* y = static_cast<T*>(a.y);
+  const dim3 grid(apply_grid(nvec)), blk(kThreads);
+  if (a.relu) {
+    if (r) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), grid, blk, sh_ap, s, x, r, y, a.p.scale, a.p.shift, nvec, a.C);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), grid, blk, sh_ap, s, x, r, y, a.p.scale, a.p.shift, nvec, a.C);
+  } else {
+    if (r) hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), grid, blk, sh_ap, s, x, r, y, a.p.scale, a.p.shift, nvec, a.C);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), grid, blk, sh_ap, s, x, r, y, a.p.scale, a.p.shift, nvec, a.C);
+  }
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t apply_impl(const void* x, const void* res, void* y, const float* scale, const float* shift, int64_t M,
+                      int C, int relu, hipStream_t s) {
+  constexpr int V = VecIO<T>::V;
+  if (C % V != 0) return hipErrorInvalidValue;
+  const int64_t nvec = M * C / V;
+  const size_t sh_ap = (size_t)2 * C * sizeof(float);
+  const T* xx = static_cast<const T*>(x);
+  const T* r = static_cast<const T*>(res);
+  T* yy = static_cast<T*>(y);
+  const dim3 grid(apply_grid(nvec)), blk(kThreads);
+  if (relu) {
+    if (r) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), grid, blk, sh_ap, s, xx, r, yy, scale, shift, nvec, C);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), grid, blk, sh_ap, s, xx, r, yy, scale, shift, nvec, C);
+  } else {
+    if (r) hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), grid, blk, sh_ap, s, xx, r, yy, scale, shift, nvec, C);
+    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), grid, blk, sh_ap, s, xx, r, yy, scale, shift, nvec, C);
+  }
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t bwd_impl(const BnBwdArgs& a, hipStream_t s) {
+  constexpr int V = VecIO<T>::V;
+  if (a.C % V != 0) return hipErrorInvalidValue;
+  const Geom g = geom<T>(a.M, a.C);
+  const size_t sh_red = (size_t)2 * kRed * V * sizeof(float) + 16;
+  const T* dy = static_cast<const T*>(a.dy);
+  const T* x = static_cast<const T*>(a.x);
+  const T* y = static_cast<const T*>(a.y);
+  if (a.relu)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(g.gx, g.gy), dim3(kRed), sh_red, s, dy, x, y, a.M,
+                       a.C, g.TC, g.RPI, g.rows_per_block, a.workspace, a.tickets, a.p);
+  else
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(g.gx, g.gy), dim3(kRed), sh_red, s, dy, x, y, a.M,
+                       a.C, g.TC, g.RPI, g.rows_per_block, a.workspace, a.tickets, a.p);
+  PTDT_HIP_CHECK(hipGetLastError());
+  const int64_t nvec = a.M * a.C / V;
+  const size_t sh_ap = (size_t)3 * a.C * sizeof(float);
+  T* dx = static_cast<T*>(a.dx);
+  T* dr = static_cast<T*>(a.dres);
+  const dim3 grid(apply_grid(nvec)), blk(kThreads);
+  const float *A = a.p.coef_a, *B = a.p.coef_b, *Cc = a.p.coef_c;
+  if (a.relu) {
+    if (dr) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), grid, blk, sh_ap, s, dy, x, y, dx, dr, A, B, Cc, nvec, a.C);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, false>), grid, blk, sh_ap, s, dy, x, y, dx, dr, A, B, Cc, nvec, a.C);
+  } else {
+    if (dr) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, true>), grid, blk, sh_ap, s, dy, x, y, dx, dr, A, B, Cc, nvec, a.C);
+    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, false>), grid, blk, sh_ap, s, dy, x, y, dx, dr, A, B, Cc, nvec, a.C);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace
+
+int64_t bn_workspace_floats(int64_t M, int C, int dtype) {
+  const Geom g = dtype == kF32 ? geom<float>(M, C) : geom<uint16_t>(M, C);
+  return (int64_t)2 * g.gx * C;
+}
+int bn_num_tickets(int C, int dtype) {
+  const int V = dtype == kF32 ? 4 : 8;
+  const int cv = C / V;
+  const int TC = cv < kMaxTC ? cv : kMaxTC;
+  return (cv + TC - 1) / TC;
+}
+
+hipError_t bn_forward_train(const BnFwdArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.C <= 0) return hipErrorInvalidValue;
+  return a.dtype == kF32 ? fwd_impl<float>(a, s) : fwd_impl<uint16_t>(a, s);
+}
+
+hipError_t bn_apply(const void* x, const void* residual, void* y, int dtype, const float* scale, const float* shift,
+                    int64_t M, int C, int relu, hipStream_t s) {
+  if (M <= 0 || C <= 0) return hipErrorInvalidValue;
+  return dtype == kF32 ? apply_impl<float>(x, residual, y, scale, shift, M, C, relu, s)
+                       : apply_impl<uint16_t>(x, residual, y, scale, shift, M, C, relu, s);
+}
+
+hipError_t bn_backward(const BnBwdArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.C <= 0) return hipErrorInvalidValue;
+  return a.dtype == kF32 ? bwd_impl<float>(a, s) : bwd_impl<uint16_t>(a, s);
+}
+
+}  // namespace ptdt

@@ -234,4 +234,42 @@ hipError_t int8_weight_gemm(const void* x, int x_dtype, const int8_t* q, const f
 hipError_t bn_relu_apply(const void* x, int dtype, const float* scale, const float* shift, int64_t N,
                          int64_t C, int64_t HW, int relu, void* y, hipStream_t s);
 
+// Training BatchNorm over channels-last [M, C] activations with ReLU / residual
+// epilogues fused (csrc/kernels/batchnorm.hip). Statistics / coefficients are f32
+// [C] device arrays; `tickets` is a zeroed int array (>= bn_num_tickets), re-armed
+// by the kernels; `workspace` holds bn_workspace_floats floats.
+struct BnParams {
+  const float* weight; const float* bias;   // may be null (affine=False)
+  float* running_mean; float* running_var;  // may be null (track_running_stats=False)
+  int64_t* num_batches_tracked;             // may be null
+  float momentum, eps;
+  float* mean; float* invstd;               // saved for backward
+  float* scale; float* shift;               // y = x*scale + shift
+};
+struct BnFwdArgs {
+  const void* x; const void* residual; void* y;  // residual may be null
+  int dtype; int64_t M; int C; int relu;
+  float* workspace; int* tickets;
+  BnParams p;
+};
+struct BnBwdParams {
+  const float* weight; const float* mean; const float* invstd;
+  float* dweight; float* dbias;             // may be null
+  float* coef_a; float* coef_b; float* coef_c;  // scratch [C] each
+};
+struct BnBwdArgs {
+  const void* dy; const void* x; const void* y;  // y: forward output (ReLU mask), used when relu
+  void* dx; void* dres;                          // dres (may be null): gradient of the residual = masked dy
+  int dtype; int64_t M; int C; int relu;
+  float* workspace; int* tickets;
+  BnBwdParams p;
+};
+int64_t bn_workspace_floats(int64_t M, int C, int dtype);
+int bn_num_tickets(int C, int dtype);
+hipError_t bn_forward_train(const BnFwdArgs& a, hipStream_t s);
+hipError_t bn_backward(const BnBwdArgs& a, hipStream_t s);
+// y = ReLU?(x*scale + shift (+ residual)) per channel (eval-mode BN, or any affine epilogue)
+hipError_t bn_apply(const void* x, const void* residual, void* y, int dtype, const float* scale, const float* shift,
+                    int64_t M, int C, int relu, hipStream_t s);
+
 }  // namespace ptdt

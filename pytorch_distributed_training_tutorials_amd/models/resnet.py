@@ -6,11 +6,14 @@ Reference: ``torchvision.models.resnet50(num_classes=1000)`` NB03:560-570 and th
 defined directly; parameter count (25,557,032) and state_dict keys match
 torchvision's so checkpoints interchange.
 
-Execution on MI355X: convolutions / BatchNorm / pooling run on MIOpen through
-PyTorch-ROCm (the reference's cuDNN role; a hand-written conv stack is out of
-scope for this harness and documented as such in SURVEY K15), the classifier
-``fc`` runs on the native MFMA Linear kernel, and ``channels_last=True`` keeps
-activations NHWC, the layout MIOpen's fastest gfx950 conv solvers use.
+Execution on MI355X: convolutions and pooling run on MIOpen through PyTorch-ROCm
+(the reference's cuDNN role; a hand-written conv stack is out of scope for this
+harness and documented as such in SURVEY K15). Every BatchNorm is
+``ops.norm.BatchNorm2d`` with its ReLU and the Bottleneck's residual add fused
+(native NHWC kernels, csrc/kernels/batchnorm.hip, for channels_last
+activations), and the classifier ``fc`` runs on the native MFMA Linear kernel.
+``model.to(memory_format=torch.channels_last)`` keeps activations NHWC, the
+layout MIOpen's fastest gfx950 conv solvers and the BN kernels use.
 """
 from __future__ import annotations
 
@@ -18,6 +21,17 @@ import torch
 import torch.nn as nn
 
 from ..ops.linear import Linear
+from ..ops.norm import BatchNorm2d
+
+
+def bn_act(bn: nn.Module, x: torch.Tensor, residual: torch.Tensor | None = None, relu: bool = False):
+    """``ReLU?(bn(x) + residual)``: fused for ops.norm.BatchNorm2d, composed for any other norm layer."""
+    if isinstance(bn, BatchNorm2d):
+        return bn(x, residual, relu)
+    y = bn(x)
+    if residual is not None:
+        y = y + residual
+    return torch.relu(y) if relu else y
 
 
 def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1):
@@ -35,7 +49,7 @@ class Bottleneck(nn.Module):
     def __init__(self, inplanes, planes, stride=1, downsample=None, groups=1, base_width=64, dilation=1,
                  norm_layer=None):
         super().__init__()
-        norm_layer = norm_layer or nn.BatchNorm2d
+        norm_layer = norm_layer or BatchNorm2d
         width = int(planes * (base_width / 64.0)) * groups
         self.conv1 = conv1x1(inplanes, width)
         self.bn1 = norm_layer(width)
@@ -48,21 +62,17 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
-        identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.relu(self.bn2(self.conv2(out)))
-        out = self.bn3(self.conv3(out))
-        if self.downsample is not None:
-            identity = self.downsample(x)
-        out += identity
-        return self.relu(out)
+        identity = x if self.downsample is None else self.downsample(x)
+        out = bn_act(self.bn1, self.conv1(x), relu=True)
+        out = bn_act(self.bn2, self.conv2(out), relu=True)
+        return bn_act(self.bn3, self.conv3(out), residual=identity, relu=True)
 
 
 class ResNet(nn.Module):
     def __init__(self, block=Bottleneck, layers=(3, 4, 6, 3), num_classes: int = 1000, zero_init_residual=False,
                  groups=1, width_per_group=64, norm_layer=None):
         super().__init__()
-        norm_layer = norm_layer or nn.BatchNorm2d
+        norm_layer = norm_layer or BatchNorm2d
         self._norm_layer = norm_layer
         self.inplanes = 64
         self.dilation = 1
@@ -104,7 +114,7 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def _forward_impl(self, x):
-        x = self.maxpool(self.relu(self.bn1(self.conv1(x))))
+        x = self.maxpool(bn_act(self.bn1, self.conv1(x), relu=True))
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

@@ -1,0 +1,122 @@
+"""BatchNorm with the ResNet epilogues fused: ``y = ReLU?(BN(x) + residual?)``.
+
+Reference call sites: every ``nn.BatchNorm2d`` of torchvision's ResNet-50
+(NB03:560-570, ``ModelParallelResNet50`` NB03:807-833), each
+followed by ``ReLU`` and, at the end of a Bottleneck, by the residual add.
+
+On GPU with channels_last (NHWC) activations the training forward and backward
+run on csrc/kernels/batchnorm.hip: statistics and the normalise / residual /
+ReLU epilogue in two launches, the ReLU mask, both parameter gradients, the
+input gradient and the residual gradient in two more -- instead of MIOpen's BN
+kernels plus separate clamp, add, threshold-backward and tensor-op passes.
+Eval mode applies the running statistics in one launch. Anything else (NCHW,
+CPU, momentum=None, odd channel counts) uses PyTorch's batch_norm with the same
+semantics. Parameters, buffers and state_dict keys are nn.BatchNorm2d's.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .._ext import native
+
+
+def _rows_layout_ok(x: torch.Tensor) -> bool:
+    if not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16):
+        return False
+    vec = 4 if x.dtype == torch.float32 else 8
+    if x.dim() < 2 or x.shape[1] % vec or x.data_ptr() % 16 or x.numel() == 0:
+        return False
+    if x.dim() == 2:
+        return x.is_contiguous()
+    return x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last)
+
+
+def _like(t: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """t in x's memory layout (autograd hands back whatever the consumer produced)."""
+    if t.stride() == x.stride():
+        return t
+    return t.contiguous(memory_format=torch.channels_last) if x.dim() == 4 else t.contiguous()
+
+
+class _BatchNormActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, relu: bool, momentum: float,
+                eps: float, tickets):
+        y, stats = native().bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, residual, relu, momentum,
+                                         eps, tickets)
+        ctx.tickets = tickets
+        ctx.relu = relu
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, y if relu else None, weight, stats)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, weight, stats = ctx.saved_tensors
+        want_dw = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        want_dres = ctx.has_res and ctx.needs_input_grad[3]
+        dx, dw, db, dres = native().bn_bwd(_like(dy, x), x, y, weight, stats, ctx.relu, want_dres, want_dw,
+                                           ctx.tickets)
+        return (dx if ctx.needs_input_grad[0] else None, dw if want_dw else None, db if want_dw else None,
+                dres if want_dres else None, None, None, None, None, None, None, None)
+
+
+def _tickets_of(bn, x):
+    """The module's zeroed ticket array for the kernels' last-block hand-off (None: per-device one)."""
+    t = getattr(bn, "_bn_tickets", None)
+    if t is None or t.device != x.device:
+        return None
+    return t
+
+
+def batch_norm_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: torch.Tensor | None = None,
+                   relu: bool = False) -> torch.Tensor:
+    """``ReLU?(bn(x) + residual)`` with ``bn``'s parameters, buffers and train/eval mode."""
+    fast = _rows_layout_ok(x) and (residual is None or (residual.dtype == x.dtype and residual.shape == x.shape
+                                                        and residual.stride() == x.stride()
+                                                        and residual.data_ptr() % 16 == 0))
+    use_batch_stats = bn.training or not bn.track_running_stats
+    if fast and use_batch_stats and bn.momentum is not None:
+        track = bn.training and bn.track_running_stats
+        return _BatchNormActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean if track else None,
+                                     bn.running_var if track else None, bn.num_batches_tracked if track else None,
+                                     relu, float(bn.momentum), float(bn.eps), _tickets_of(bn, x))
+    needs_grad = torch.is_grad_enabled() and (x.requires_grad or (residual is not None and residual.requires_grad))
+    if fast and not use_batch_stats and not needs_grad:  # eval: one launch with the running statistics
+        scale = torch.rsqrt(bn.running_var.float() + bn.eps)
+        if bn.weight is not None:
+            scale = scale * bn.weight.float()
+        shift = -bn.running_mean.float() * scale
+        if bn.bias is not None:
+            shift = shift + bn.bias.float()
+        return native().bn_apply(x, residual, scale.contiguous(), shift.contiguous(), relu)
+    if bn.training and bn.track_running_stats and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    momentum = bn.momentum
+    if bn.training and bn.track_running_stats and momentum is None:  # cumulative moving average
+        momentum = 1.0 / float(bn.num_batches_tracked)
+    y = F.batch_norm(x, bn.running_mean if not bn.training or bn.track_running_stats else None,
+                     bn.running_var if not bn.training or bn.track_running_stats else None, bn.weight, bn.bias,
+                     use_batch_stats, momentum if momentum is not None else 0.0, bn.eps)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+class BatchNorm2d(nn.BatchNorm2d):
+    """Drop-in ``nn.BatchNorm2d`` (same parameters, buffers, state_dict keys) whose
+    ``forward(x, residual=None, relu=False)`` fuses the residual add and ReLU and
+    runs on the native NHWC kernels for channels_last GPU activations."""
+
+    def __init__(self, num_features: int, *args, **kwargs):
+        super().__init__(num_features, *args, **kwargs)
+        # zeroed int32 tickets for the kernels' last-block hand-off (re-armed in-kernel), one per
+        # channel tile (>= 32 channels); non-persistent: not part of the state_dict
+        self.register_buffer("_bn_tickets", torch.zeros(max(1, -(-num_features // 32)), dtype=torch.int32),
+                             persistent=False)
+
+    def forward(self, x, residual=None, relu: bool = False):
+        self._check_input_dim(x)
+        return batch_norm_act(x, self, residual, relu)

@@ -42,6 +42,17 @@ def _flatten_broadcast(tensors, c: comm_mod.Communicator, src: int = 0):
             off += n
 
 
+def _state_buffers(module: nn.Module):
+    """Buffers that are model state (persistent): running statistics, counters. Non-persistent
+    scratch (e.g. ops.norm.BatchNorm2d's kernel tickets) is neither synced nor checkpointed."""
+    out = []
+    for m in module.modules():
+        for name, b in m._buffers.items():
+            if b is not None and name not in m._non_persistent_buffers_set:
+                out.append(b)
+    return out
+
+
 class DistributedDataParallel(nn.Module):
     def __init__(self, module: nn.Module, device_ids=None, output_device=None, broadcast_buffers: bool = True,
                  bucket_cap_mb: float | None = None, first_bucket_mb: float | None = None,
@@ -76,7 +87,7 @@ class DistributedDataParallel(nn.Module):
 
         if init_sync and self.world_size > 1:
             self._verify_shapes()
-            _flatten_broadcast(list(module.parameters()) + list(module.buffers()), self.comm, 0)
+            _flatten_broadcast(list(module.parameters()) + _state_buffers(module), self.comm, 0)
 
         plan = bucketing.plan(params, None, self._first_cap, self._cap, self.world_size)
         py_ar = None
@@ -121,7 +132,7 @@ class DistributedDataParallel(nn.Module):
     def forward(self, *args, **kwargs):
         self._maybe_rebuild()
         if self.broadcast_buffers and self.world_size > 1:
-            bufs = [b for b in self.module.buffers()]
+            bufs = _state_buffers(self.module)
             if bufs:
                 _flatten_broadcast(bufs, self.comm, 0)
         if torch.is_grad_enabled():

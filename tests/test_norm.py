@@ -1,0 +1,182 @@
+"""BatchNorm with fused residual/ReLU (ops/norm.py, csrc/kernels/batchnorm.hip) vs
+PyTorch's fp32 batch_norm composite. CPU tests cover the fallback and module
+contract; GPU tests the native NHWC kernels."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from pytorch_distributed_training_tutorials_amd.ops.norm import BatchNorm2d, batch_norm_act
+
+
+def _reference(x, bn_ref, residual, relu):
+    y = bn_ref(x)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+def test_module_contract_matches_nn_batchnorm():
+    a, b = BatchNorm2d(64), nn.BatchNorm2d(64)
+    assert list(a.state_dict().keys()) == list(b.state_dict().keys())
+    assert isinstance(a, nn.BatchNorm2d)
+    b.load_state_dict(a.state_dict())
+
+
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True)])
+def test_cpu_fallback_matches_composite(relu, res):
+    torch.manual_seed(0)
+    x = torch.randn(4, 16, 5, 5, requires_grad=True)
+    r = torch.randn(4, 16, 5, 5, requires_grad=True) if res else None
+    ours, ref = BatchNorm2d(16), nn.BatchNorm2d(16)
+    with torch.no_grad():
+        ours.weight.uniform_(0.5, 1.5)
+        ours.bias.uniform_(-0.5, 0.5)
+    ref.load_state_dict(ours.state_dict())
+    x2 = x.detach().clone().requires_grad_()
+    r2 = r.detach().clone().requires_grad_() if res else None
+    y = ours(x, r, relu)
+    y2 = _reference(x2, ref, r2, relu)
+    torch.testing.assert_close(y, y2)
+    y.square().sum().backward()
+    y2.square().sum().backward()
+    torch.testing.assert_close(x.grad, x2.grad)
+    torch.testing.assert_close(ours.weight.grad, ref.weight.grad)
+    for k in ("running_mean", "running_var", "num_batches_tracked"):
+        torch.testing.assert_close(getattr(ours, k), getattr(ref, k))
+    ours.eval(), ref.eval()
+    torch.testing.assert_close(ours(x, r, relu), _reference(x2, ref, r2, relu))
+
+
+def test_resnet_uses_fused_bn_and_keeps_param_count():
+    from pytorch_distributed_training_tutorials_amd.models.resnet import resnet50
+
+    m = resnet50()
+    assert sum(p.numel() for p in m.parameters()) == 25_557_032
+    assert all(type(b) is BatchNorm2d for b in m.modules() if isinstance(b, nn.BatchNorm2d))
+
+
+# ------------------------------------------------------------------------ GPU
+SHAPES = [(4, 64, 14, 14), (2, 256, 7, 7), (3, 2048, 2, 2), (5, 24, 3, 3), (128, 64, 28, 28)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("relu,res", [(False, False), (True, False), (True, True), (False, True)])
+def test_native_bn_train_fwd_bwd(shape, dtype, relu, res):
+    dev = torch.device("cuda", 0)
+    C = shape[1]
+    if C % (4 if dtype == torch.float32 else 8):
+        pytest.skip("channel count not a multiple of the vector width (fallback path)")
+    torch.manual_seed(sum(shape))
+    x0 = (torch.randn(shape, device=dev) * 2 + 3).to(dtype).contiguous(memory_format=torch.channels_last)
+    r0 = torch.randn(shape, device=dev).to(dtype).contiguous(memory_format=torch.channels_last) if res else None
+    g0 = torch.randn(shape, device=dev).to(dtype).contiguous(memory_format=torch.channels_last)
+    ours = BatchNorm2d(C).to(dev)
+    with torch.no_grad():
+        ours.weight.uniform_(0.5, 1.5)
+        ours.bias.uniform_(-0.5, 0.5)
+        ours.running_mean.uniform_(-1, 1)
+    ref = nn.BatchNorm2d(C).to(dev)
+    ref.load_state_dict(ours.state_dict())
+    x = x0.clone().requires_grad_()
+    r = r0.clone().requires_grad_() if res else None
+    y = ours(x, r, relu)
+    assert y.dtype == dtype and y.is_contiguous(memory_format=torch.channels_last)
+    # fp32 reference on the same (rounded) inputs
+    xr = x0.float().clone().requires_grad_()
+    rr = r0.float().clone().requires_grad_() if res else None
+    yr = _reference(xr, ref, rr, relu)
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(y.float(), yr, rtol=tol, atol=tol)
+    y.backward(g0)
+    yr.backward(g0.float())
+    gtol = 1e-4 if dtype == torch.float32 else 5e-2
+    # elements whose pre-ReLU value rounds to the other side of 0 flip their mask: skip them
+    keep = (yr.detach().abs() > 1e-3) | (not relu)
+    torch.testing.assert_close(x.grad.float()[keep], xr.grad[keep], rtol=gtol, atol=gtol)
+    if res:
+        torch.testing.assert_close(r.grad.float()[keep], rr.grad[keep], rtol=gtol, atol=gtol)
+    wtol = 1e-3 * (x0.numel() / C) ** 0.5 if dtype == torch.bfloat16 else 1e-3
+    torch.testing.assert_close(ours.weight.grad, ref.weight.grad, rtol=1e-3, atol=wtol)
+    torch.testing.assert_close(ours.bias.grad, ref.bias.grad, rtol=1e-3, atol=wtol)
+    torch.testing.assert_close(ours.running_mean, ref.running_mean, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ours.running_var, ref.running_var, rtol=1e-4, atol=1e-5)
+    assert int(ours.num_batches_tracked) == int(ref.num_batches_tracked) == 1
+    # eval: running statistics, one launch, same epilogue
+    ours.eval(), ref.eval()
+    with torch.no_grad():
+        torch.testing.assert_close(ours(x0, r0, relu).float(), _reference(x0.float(), ref, r0.float() if res else None,
+                                                                          relu), rtol=tol, atol=tol)
+
+
+@pytest.mark.gpu
+def test_native_bn_large_mean_is_stable():
+    """Shifted sums: |mean| = 1e3 * std must not cancel the variance."""
+    dev = torch.device("cuda", 0)
+    x = (torch.randn(64, 32, 8, 8, device=dev) + 1000.0).contiguous(memory_format=torch.channels_last)
+    bn = BatchNorm2d(32).to(dev)
+    y = bn(x)
+    var = x.float().var(dim=(0, 2, 3), unbiased=False)
+    ref = (x - x.mean(dim=(0, 2, 3), keepdim=True)) / torch.sqrt(var.view(1, -1, 1, 1) + bn.eps)
+    torch.testing.assert_close(y, ref, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_native_bn_2d_and_graph_replay_deterministic():
+    """[M, C] input; two launches on the same stream give bit-identical stats (fixed-order combine)
+    and the in-kernel ticket re-arm survives hipGraph replay."""
+    dev = torch.device("cuda", 0)
+    x = torch.randn(50000, 128, device=dev, dtype=torch.bfloat16)
+    bn = BatchNorm2d(128).to(dev)
+    bn.track_running_stats = False
+    bn.running_mean = bn.running_var = bn.num_batches_tracked = None
+    y1 = batch_norm_act(x, bn, relu=True)
+    y2 = batch_norm_act(x, bn, relu=True)
+    assert torch.equal(y1, y2)
+    ref = F.relu(F.batch_norm(x.float(), None, None, bn.weight, bn.bias, True, 0.1, bn.eps))
+    torch.testing.assert_close(y1.float(), ref, rtol=2e-2, atol=2e-2)
+    out = torch.empty_like(y1)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        batch_norm_act(x, bn, relu=True)  # side-stream warmup before capture (torch.cuda.graph recipe)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out.copy_(batch_norm_act(x, bn, relu=True))
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, y1)
+
+
+@pytest.mark.gpu
+def test_resnet50_fused_bn_matches_plain_bn():
+    """ResNet-50 (channels_last, fp32) with the fused BN path vs the same weights with
+    nn.BatchNorm2d (MIOpen), both against a float64 CPU reference: the fused model's
+    error must be at the level of the plain GPU model's (53 BNs, the deepest
+    normalising 16 rows, amplify fp32 rounding on the way back to conv1)."""
+    from pytorch_distributed_training_tutorials_amd.models.resnet import resnet50
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    ours = resnet50(num_classes=10).to(dev).to(memory_format=torch.channels_last)
+    plain = resnet50(num_classes=10, norm_layer=nn.BatchNorm2d).to(dev).to(memory_format=torch.channels_last)
+    plain.load_state_dict(ours.state_dict())
+    ref = resnet50(num_classes=10, norm_layer=nn.BatchNorm2d).double()
+    ref.load_state_dict(ours.state_dict())
+    x = torch.randn(4, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
+    outs = [m(x.to(dtype=next(m.parameters()).dtype, device=next(m.parameters()).device))
+            for m in (ours, plain, ref)]
+    torch.testing.assert_close(outs[0], outs[1], rtol=2e-3, atol=2e-3)
+    for o in outs:
+        o.square().mean().backward()
+    worst = []
+    for (n, p1), p2, p3 in zip(ours.named_parameters(), plain.parameters(), ref.parameters()):
+        g = p3.grad
+        e_ours = ((p1.grad.double().cpu() - g).norm() / (g.norm() + 1e-30)).item()
+        e_plain = ((p2.grad.double().cpu() - g).norm() / (g.norm() + 1e-30)).item()
+        worst.append((e_ours, e_plain, n))
+        assert e_ours <= 3 * e_plain + 1e-3, f"{n}: fused {e_ours:.3g} vs plain {e_plain:.3g} (rel. to fp64)"
