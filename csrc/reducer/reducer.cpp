@@ -210,6 +210,7 @@ void Reducer::launch(size_t bi) {
   auto& b = buckets_[bi];
   b.launched = true;
   if (on_gpu_) {
+    if (comm_->world() == 1) return;  // the average over one rank is the bucket itself: no collective
     hipStream_t compute = c10::hip::getCurrentHIPStream(device_).stream();
     hipStream_t comm = comm_stream_->stream();
     hip_ok(hipEventRecord(ev_ready_, compute), "hipEventRecord");

@@ -48,8 +48,9 @@ _BIG_MIN_MACS = 1 << 24
 
 
 def _big(M: int, N: int, K: int, dtype) -> bool:
-    """Use the LDS-DMA kernel: bf16, K a multiple of its 64-deep K-tile, enough work."""
-    return dtype == torch.bfloat16 and K >= 64 and K % 64 == 0 and M * N * K >= _BIG_MIN_MACS
+    """Use the LDS-DMA kernel: bf16 with enough work (K not a multiple of its 64-deep
+    K-tile is zero-padded by gemm_nt_big, e.g. ResNet fc's dx with K = 1000 classes)."""
+    return dtype == torch.bfloat16 and K >= 64 and M * N * K >= _BIG_MIN_MACS
 
 
 def plan_big(M: int, N: int, K: int) -> tuple[int, int]:
@@ -79,6 +80,10 @@ _SPLIT_MIN_US = 25.0
 def gemm_nt_big(A: torch.Tensor, Bt: torch.Tensor, out_dtype, bias=None, relu: bool = False,
                 plan: tuple[int, int] | None = None) -> torch.Tensor:
     """C = A @ Bt^T on the LDS-DMA kernel (A [M,K], Bt [N,K], both made K-contiguous)."""
+    K = A.shape[1]
+    if K % 64:  # zero-pad K to the kernel's K-tile (one copy of each operand, made anyway when strided)
+        A = F.pad(A, (0, 64 - K % 64))
+        Bt = F.pad(Bt, (0, 64 - K % 64))
     A = A if A.stride(-1) == 1 and A.stride(0) % 8 == 0 else A.contiguous()
     Bt = Bt if Bt.stride(-1) == 1 and Bt.stride(0) % 8 == 0 else Bt.contiguous()
     M, N = A.shape[0], Bt.shape[0]
@@ -150,13 +155,16 @@ class _LinearFn(torch.autograd.Function):
         mask = y if ctx.relu else None
         dx = dw = db = None
         M, Nout, Kin = dy2.shape[0], weight.shape[0], weight.shape[1]
-        if _big(M, Kin, Nout, dy2.dtype) and _big(Nout, Kin, M, dy2.dtype):
+        big_dx = _big(M, Kin, Nout, dy2.dtype)
+        big_dw = _big(Nout, Kin, M, dy2.dtype)
+        if big_dx or big_dw:
             C_ = native()
             g = C_.relu_bwd(dy2, mask) if mask is not None else dy2
             if ctx.needs_input_grad[0]:
-                dx = gemm_nt_big(g, weight.t(), x2.dtype).reshape(ctx.in_shape)
+                dx = (gemm_nt_big(g, weight.t(), x2.dtype) if big_dx else
+                      gemm(g, weight, out_dtype=x2.dtype)).reshape(ctx.in_shape)
             if ctx.needs_input_grad[1]:
-                dw = gemm_nt_big(g.t(), x2.t(), weight.dtype)
+                dw = gemm_nt_big(g.t(), x2.t(), weight.dtype) if big_dw else gemm(g.t(), x2, out_dtype=weight.dtype)
             if ctx.has_bias and ctx.needs_input_grad[2]:
                 cs = torch.empty(Nout, device=dy.device, dtype=torch.float32)
                 C_.col_sum_(g, cs, False)
