@@ -772,6 +772,54 @@ Tensor bn_apply_(Tensor x, c10::optional<Tensor> residual, Tensor scale, Tensor 
   return y;
 }
 
+// ------------------------------------------------------------- max pooling (NHWC)
+PoolArgs pool_args(const Tensor& x, int64_t Ho, int64_t Wo, std::vector<int64_t> k, std::vector<int64_t> st,
+                   std::vector<int64_t> pad) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "maxpool: x must be a channels_last-contiguous 4D GPU tensor");
+  TORCH_CHECK(k.size() == 2 && st.size() == 2 && pad.size() == 2, "maxpool: 2D kernel/stride/padding");
+  PoolArgs a{};
+  a.N = (int)x.size(0); a.C = (int)x.size(1); a.H = (int)x.size(2); a.W = (int)x.size(3);
+  a.Ho = (int)Ho; a.Wo = (int)Wo;
+  a.kh = (int)k[0]; a.kw = (int)k[1]; a.sh = (int)st[0]; a.sw = (int)st[1]; a.ph = (int)pad[0]; a.pw = (int)pad[1];
+  TORCH_CHECK(a.kh >= 1 && a.kw >= 1 && a.kh * a.kw <= 256 && a.sh >= 1 && a.sw >= 1 && a.ph >= 0 && a.pw >= 0 &&
+                  2 * a.ph <= a.kh && 2 * a.pw <= a.kw,
+              "maxpool: unsupported window");
+  TORCH_CHECK((int64_t)(a.H + 2 * a.ph - a.kh) / a.sh + 1 == Ho && (int64_t)(a.W + 2 * a.pw - a.kw) / a.sw + 1 == Wo,
+              "maxpool: output size mismatch");
+  const int V = x.scalar_type() == at::kFloat ? 4 : 8;
+  TORCH_CHECK(a.C % V == 0, "maxpool: channels must be a multiple of ", V);
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "maxpool: 16-byte aligned data expected");
+  return a;
+}
+
+std::vector<Tensor> maxpool2d_fwd(Tensor x, std::vector<int64_t> k, std::vector<int64_t> st, std::vector<int64_t> pad) {
+  const int64_t Ho = (x.size(2) + 2 * pad[0] - k[0]) / st[0] + 1, Wo = (x.size(3) + 2 * pad[1] - k[1]) / st[1] + 1;
+  PoolArgs a = pool_args(x, Ho, Wo, k, st, pad);
+  c10::hip::HIPGuard guard(x.device().index());
+  auto opts = x.options().memory_format(at::MemoryFormat::ChannelsLast);
+  Tensor y = at::empty({x.size(0), x.size(1), Ho, Wo}, opts);
+  Tensor arg = at::empty({x.size(0), x.size(1), Ho, Wo}, opts.dtype(at::kByte));
+  hip_check(maxpool2d_nhwc_forward(x.data_ptr(), y.data_ptr(), arg.data_ptr<uint8_t>(), dt_of(x), a, cur_stream(x)),
+            "maxpool2d_nhwc_forward");
+  return {y, arg};
+}
+
+Tensor maxpool2d_bwd(Tensor gy, Tensor arg, std::vector<int64_t> in_size, std::vector<int64_t> k,
+                     std::vector<int64_t> st, std::vector<int64_t> pad) {
+  TORCH_CHECK(in_size.size() == 4, "maxpool: input size [N, C, H, W]");
+  TORCH_CHECK(gy.is_cuda() && gy.dim() == 4 && gy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  arg.sizes() == gy.sizes() && arg.strides() == gy.strides() && arg.scalar_type() == at::kByte,
+              "maxpool backward: gy / argmax must be matching channels_last tensors");
+  Tensor gx = at::empty(in_size, gy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  PoolArgs a = pool_args(gx, gy.size(2), gy.size(3), k, st, pad);
+  c10::hip::HIPGuard guard(gy.device().index());
+  hip_check(maxpool2d_nhwc_backward(gy.data_ptr(), arg.data_ptr<uint8_t>(), gx.data_ptr(), dt_of(gy), a,
+                                    cur_stream(gy)),
+            "maxpool2d_nhwc_backward");
+  return gx;
+}
+
 // ------------------------------------------------------------- comm
 ncclDataType_t nccl_dt(const Tensor& t) {
   switch (t.scalar_type()) {
@@ -848,6 +896,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("momentum"), py::arg("eps"), py::arg("tickets") = py::none());
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("weight"), py::arg("stats"),
         py::arg("relu"), py::arg("want_dres"), py::arg("want_dweight"), py::arg("tickets") = py::none());
+  m.def("maxpool2d_fwd", &maxpool2d_fwd);
+  m.def("maxpool2d_bwd", &maxpool2d_bwd);
   m.def("bn_apply", &bn_apply_, py::arg("x"), py::arg("residual"), py::arg("scale"), py::arg("shift"),
         py::arg("relu"));
 

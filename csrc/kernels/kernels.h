@@ -272,4 +272,15 @@ hipError_t bn_backward(const BnBwdArgs& a, hipStream_t s);
 hipError_t bn_apply(const void* x, const void* residual, void* y, int dtype, const float* scale, const float* shift,
                     int64_t M, int C, int relu, hipStream_t s);
 
+// Max pooling over NHWC activations (csrc/kernels/pool.hip): argmax is one byte per
+// output element (window offset dy*kw + dx), the backward a deterministic gather.
+struct PoolArgs {
+  int N, H, W, C, Ho, Wo;
+  int kh, kw, sh, sw, ph, pw;
+};
+hipError_t maxpool2d_nhwc_forward(const void* x, void* y, uint8_t* argmax, int dtype, const PoolArgs& a,
+                                  hipStream_t s);
+hipError_t maxpool2d_nhwc_backward(const void* gy, const uint8_t* argmax, void* gx, int dtype, const PoolArgs& a,
+                                   hipStream_t s);
+
 }  // namespace ptdt

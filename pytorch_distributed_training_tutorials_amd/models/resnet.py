@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.linear import Linear
-from ..ops.norm import BatchNorm2d
+from ..ops.norm import BatchNorm2d, MaxPool2d
 
 
 def bn_act(bn: nn.Module, x: torch.Tensor, residual: torch.Tensor | None = None, relu: bool = False):
@@ -81,7 +81,7 @@ class ResNet(nn.Module):
         self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = norm_layer(self.inplanes)
         self.relu = nn.ReLU(inplace=True)
-        self.maxpool = nn.MaxPool2d(kernel_size=3, stride=2, padding=1)
+        self.maxpool = MaxPool2d(kernel_size=3, stride=2, padding=1)
         self.layer1 = self._make_layer(block, 64, layers[0])
         self.layer2 = self._make_layer(block, 128, layers[1], stride=2)
         self.layer3 = self._make_layer(block, 256, layers[2], stride=2)

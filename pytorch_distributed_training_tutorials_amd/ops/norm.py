@@ -1,4 +1,5 @@
-"""BatchNorm with the ResNet epilogues fused: ``y = ReLU?(BN(x) + residual?)``.
+"""BatchNorm with the ResNet epilogues fused: ``y = ReLU?(BN(x) + residual?)``,
+and NHWC max pooling (the ResNet stem pool).
 
 Reference call sites: every ``nn.BatchNorm2d`` of torchvision's ResNet-50
 (NB03:560-570, ``ModelParallelResNet50`` NB03:807-833), each
@@ -120,3 +121,40 @@ class BatchNorm2d(nn.BatchNorm2d):
     def forward(self, x, residual=None, relu: bool = False):
         self._check_input_dim(x)
         return batch_norm_act(x, self, residual, relu)
+
+
+# ----------------------------------------------------------------------------- pooling
+class _MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k, s, p):
+        y, arg = native().maxpool2d_fwd(x, k, s, p)
+        ctx.save_for_backward(arg)
+        ctx.cfg = (list(x.shape), k, s, p)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (arg,) = ctx.saved_tensors
+        size, k, s, p = ctx.cfg
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        return native().maxpool2d_bwd(gy, arg, size, k, s, p), None, None, None
+
+
+def _pair(v):
+    return [int(v), int(v)] if isinstance(v, int) else [int(t) for t in v]
+
+
+class MaxPool2d(nn.MaxPool2d):
+    """Drop-in ``nn.MaxPool2d``; channels_last GPU activations run on the native NHWC
+    kernels (csrc/kernels/pool.hip: one-byte window argmax, gather backward)."""
+
+    def forward(self, x):
+        k, s, p = _pair(self.kernel_size), _pair(self.stride or self.kernel_size), _pair(self.padding)
+        d = _pair(self.dilation)
+        vec = 4 if x.dtype == torch.float32 else 8
+        if (x.is_cuda and x.dim() == 4 and x.dtype in (torch.float32, torch.bfloat16) and d == [1, 1]
+                and not self.ceil_mode and not self.return_indices and x.shape[1] % vec == 0
+                and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0
+                and 2 * p[0] <= k[0] and 2 * p[1] <= k[1]):
+            return _MaxPoolFn.apply(x, k, s, p)
+        return super().forward(x)

@@ -185,3 +185,33 @@ def test_resnet50_fused_bn_matches_plain_bn():
         assert e1 ** 0.5 <= 0.1 * g.norm().item() + 1e-6, f"{n}: fused gradient off by {e1 ** 0.5:.3g}"
     e_ours, e_plain = (d_ours / ref_sq) ** 0.5, (d_plain / ref_sq) ** 0.5
     assert e_ours <= 3 * e_plain + 1e-3, f"whole-model gradient error: fused {e_ours:.3g} vs plain {e_plain:.3g}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,k,s,p", [((4, 64, 112, 112), 3, 2, 1), ((2, 32, 9, 7), 3, 2, 1),
+                                         ((3, 16, 8, 8), 2, 2, 0), ((2, 24, 7, 5), 3, 1, 1)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_native_maxpool_nhwc_matches_torch(shape, k, s, p, dtype):
+    from pytorch_distributed_training_tutorials_amd.ops.norm import MaxPool2d
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(sum(shape))
+    x0 = torch.randn(shape, device=dev).to(dtype).contiguous(memory_format=torch.channels_last)
+    x = x0.clone().requires_grad_()
+    xr = x0.float().clone().requires_grad_()
+    y = MaxPool2d(k, s, p)(x)
+    yr = F.max_pool2d(xr, k, s, p)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    torch.testing.assert_close(y.float(), yr, rtol=0, atol=0)  # a max is exact
+    g = torch.randn(yr.shape, device=dev).to(dtype)
+    y.backward(g.contiguous(memory_format=torch.channels_last))
+    yr.backward(g.float())
+    tol = 1e-6 if dtype == torch.float32 else 2e-2  # overlapping windows: summation order
+    torch.testing.assert_close(x.grad.float(), xr.grad, rtol=tol, atol=tol)
+
+
+def test_maxpool_cpu_falls_back():
+    from pytorch_distributed_training_tutorials_amd.ops.norm import MaxPool2d
+
+    x = torch.randn(2, 8, 9, 9)
+    torch.testing.assert_close(MaxPool2d(3, 2, 1)(x), F.max_pool2d(x, 3, 2, 1))
