@@ -37,7 +37,10 @@ def main(argv=None):
     ap.add_argument("--bucket_cap_mb", type=float, default=None)
     ap.add_argument("--impl", default="native", choices=["native", "torch"],
                     help="native DDP reducer + fused optimizer, or stock torch DDP + torch.optim.SGD (comparator)")
+    ap.add_argument("--no_cudnn_benchmark", action="store_true",
+                    help="keep MIOpen's heuristic solver choice (default: exhaustive find per conv shape)")
     a = ap.parse_args(argv)
+    torch.backends.cudnn.benchmark = not a.no_cudnn_benchmark
 
     from pytorch_distributed_training_tutorials_amd import native
     from pytorch_distributed_training_tutorials_amd.models.resnet import resnet50
@@ -103,7 +106,7 @@ def main(argv=None):
             "dtype": a.dtype, "data": "synthetic ImageNet-shaped (generated on device)",
             "config": {"model": "resnet50", "per_device_batch": a.batch_size, "image": a.image,
                        "parallelism": f"dp{world}", "channels_last": not a.no_channels_last},
-            "impl": a.impl,
+            "impl": a.impl, "miopen_find": "exhaustive (cudnn.benchmark)" if torch.backends.cudnn.benchmark else "heuristic",
             "buckets_MB": [round(b / 2 ** 20, 2) for b in ddp.bucket_sizes_bytes()] if a.impl == "native" else None,
             "final_loss": float(loss.detach()),
         }), flush=True)

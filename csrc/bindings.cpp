@@ -710,7 +710,8 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> weight, c10::op
 
 // Backward: returns (dx, dweight, dbias, dres); dres undefined unless want_dres.
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::optional<Tensor> weight, Tensor stats,
-                           bool relu, bool want_dres, bool want_dweight, c10::optional<Tensor> tickets) {
+                           bool relu, bool want_dres, bool want_dweight, c10::optional<Tensor> tickets,
+                           c10::optional<Tensor> dweight_out, c10::optional<Tensor> dbias_out) {
   int64_t M;
   int C;
   bn_rows(x, &M, &C);
@@ -745,12 +746,22 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::op
   float* d = dwb.data_ptr<float>();
   a.p.dweight = want_dweight ? d : nullptr;
   a.p.dbias = want_dweight ? d + C : nullptr;
+  // parameter-gradient destinations given by the caller (DDP bucket slots): written in place
+  Tensor dw_out, db_out;
+  if (want_dweight && dweight_out.has_value() && dweight_out->defined()) {
+    a.p.dweight = const_cast<float*>(opt_f32(dweight_out, C, "dweight_out"));
+    dw_out = *dweight_out;
+  }
+  if (want_dweight && dbias_out.has_value() && dbias_out->defined()) {
+    a.p.dbias = const_cast<float*>(opt_f32(dbias_out, C, "dbias_out"));
+    db_out = *dbias_out;
+  }
   a.p.coef_a = d + 2 * C;
   a.p.coef_b = d + 3 * C;
   a.p.coef_c = d + 4 * C;
   hip_check(bn_backward(a, cur_stream(x)), "bn_backward");
-  Tensor dw = want_dweight ? dwb[0] : Tensor();
-  Tensor db = want_dweight ? dwb[1] : Tensor();
+  Tensor dw = want_dweight ? (dw_out.defined() ? dw_out : dwb[0]) : Tensor();
+  Tensor db = want_dweight ? (db_out.defined() ? db_out : dwb[1]) : Tensor();
   return {dx, dw, db, dres};
 }
 
@@ -895,7 +906,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("running_var"), py::arg("num_batches_tracked"), py::arg("residual"), py::arg("relu"),
         py::arg("momentum"), py::arg("eps"), py::arg("tickets") = py::none());
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("weight"), py::arg("stats"),
-        py::arg("relu"), py::arg("want_dres"), py::arg("want_dweight"), py::arg("tickets") = py::none());
+        py::arg("relu"), py::arg("want_dres"), py::arg("want_dweight"), py::arg("tickets") = py::none(),
+        py::arg("dweight_out") = py::none(), py::arg("dbias_out") = py::none());
   m.def("maxpool2d_fwd", &maxpool2d_fwd);
   m.def("maxpool2d_bwd", &maxpool2d_bwd);
   m.def("bn_apply", &bn_apply_, py::arg("x"), py::arg("residual"), py::arg("scale"), py::arg("shift"),
@@ -1059,6 +1071,7 @@ PYBIND11_MODULE(_C, m) {
       .def("buckets", &Reducer::buckets)
       .def("bucket_tensors", &Reducer::bucket_tensors)
       .def("zero_grads", &Reducer::zero_grads)
+      .def("grad_view", &Reducer::grad_view)
       .def_property_readonly("iteration", &Reducer::iteration)
       .def_property_readonly("in_backward", &Reducer::in_backward);
 }

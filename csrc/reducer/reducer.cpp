@@ -167,6 +167,11 @@ at::Tensor Reducer::bucket_view(const Bucket& b, size_t k, int64_t i) const {
   return flat.view(p.sizes());
 }
 
+at::Tensor Reducer::grad_view(int64_t i) const {
+  if (i < 0 || i >= (int64_t)params_.size()) throw std::out_of_range("Reducer::grad_view");
+  return bucket_view(buckets_[param_bucket_[i]], (size_t)param_slot_[i], i);
+}
+
 // Make params_[i].grad the bucket view again (a user may have set grads to
 // None, or autograd may have assigned a fresh tensor on the first accumulation).
 void Reducer::ensure_view(int64_t i) {

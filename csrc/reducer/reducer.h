@@ -70,6 +70,10 @@ class Reducer {
   int64_t iteration() const { return iteration_; }
   bool in_backward() const { return in_backward_; }
   void zero_grads();
+  // A fresh view of parameter i's slot in its bucket (the parameter's own strides):
+  // autograd "steals" it as .grad when a cast's backward writes the gradient straight
+  // into it (ops/conv.py grad sinks), so no separate accumulate kernel runs.
+  at::Tensor grad_view(int64_t i) const;
 
  private:
   struct Bucket {

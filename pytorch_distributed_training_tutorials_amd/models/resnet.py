@@ -20,6 +20,7 @@ from __future__ import annotations
 import torch
 import torch.nn as nn
 
+from ..ops.conv import Conv2d
 from ..ops.linear import Linear
 from ..ops.norm import BatchNorm2d, MaxPool2d
 
@@ -35,12 +36,12 @@ def bn_act(bn: nn.Module, x: torch.Tensor, residual: torch.Tensor | None = None,
 
 
 def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1):
-    return nn.Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, padding=dilation, groups=groups,
+    return Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, padding=dilation, groups=groups,
                      bias=False, dilation=dilation)
 
 
 def conv1x1(in_planes, out_planes, stride=1):
-    return nn.Conv2d(in_planes, out_planes, kernel_size=1, stride=stride, bias=False)
+    return Conv2d(in_planes, out_planes, kernel_size=1, stride=stride, bias=False)
 
 
 class Bottleneck(nn.Module):
@@ -78,7 +79,7 @@ class ResNet(nn.Module):
         self.dilation = 1
         self.groups = groups
         self.base_width = width_per_group
-        self.conv1 = nn.Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
+        self.conv1 = Conv2d(3, self.inplanes, kernel_size=7, stride=2, padding=3, bias=False)
         self.bn1 = norm_layer(self.inplanes)
         self.relu = nn.ReLU(inplace=True)
         self.maxpool = MaxPool2d(kernel_size=3, stride=2, padding=1)

@@ -1,0 +1,70 @@
+"""Conv2d whose mixed-precision weight cast writes its gradient straight into
+the DDP gradient bucket.
+
+Under ``torch.autocast("cuda", torch.bfloat16)`` every convolution casts its
+fp32 master weight to bf16 in the forward; in the backward the bf16 weight
+gradient is cast back to fp32 (one kernel) and then accumulated into the
+parameter's ``.grad`` -- a bucket view of the DDP reducer -- by a second
+elementwise kernel (``AccumulateGrad``'s ``grad += new``). In the ResNet-50 DDP
+step that is 2 x 161 kernels (profiles/r1_resnet_window.md: the bf16->fp32
+copies and the ``add<float>`` kernels).
+
+``Conv2d`` here performs that cast through :class:`SinkCast`: when the
+parameter carries a *grad sink* (installed by ``parallel.ddp``; returns a fresh
+view of the parameter's bucket slot) and its ``.grad`` is ``None`` (DDP's
+``zero_grad`` clears it), the backward converts the bf16 gradient directly into
+the bucket slot with one copy kernel and hands that view to autograd, which
+adopts it as ``.grad`` without another kernel. Without a sink, outside autocast,
+or while gradients accumulate (``no_sync``) it behaves exactly like the
+autocast cast. Parameters and state_dict are ``nn.Conv2d``'s.
+
+Reference call sites: the 53 convolutions of torchvision's ResNet-50
+(NB03:560-570, NB03:807-833).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+
+class SinkCast(torch.autograd.Function):
+    """``w.to(dtype)`` whose backward can land the gradient in ``w``'s DDP bucket slot."""
+
+    @staticmethod
+    def forward(ctx, w, dtype):
+        ctx.w = w
+        return w.to(dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        w = ctx.w
+        sink = getattr(w, "_ptdt_grad_sink", None)
+        if sink is not None and w.grad is None:
+            out = sink()
+            out.copy_(g)  # bf16 -> fp32 conversion straight into the bucket
+            return out, None
+        return g.to(w.dtype), None
+
+
+def cast_weight(w: torch.Tensor) -> torch.Tensor:
+    """The autocast dtype copy of an fp32 parameter (through SinkCast when it needs a gradient)."""
+    if not (w.is_cuda and w.dtype == torch.float32 and torch.is_autocast_enabled("cuda")):
+        return w
+    dt = torch.get_autocast_dtype("cuda")
+    if dt not in (torch.bfloat16, torch.float16):
+        return w
+    if w.requires_grad and torch.is_grad_enabled():
+        return SinkCast.apply(w, dt)
+    return w.to(dt)
+
+
+class Conv2d(nn.Conv2d):
+    """Drop-in ``nn.Conv2d`` (same parameters, init, state_dict) with the grad-sink weight cast."""
+
+    def forward(self, x):
+        w = cast_weight(self.weight)
+        if w is not self.weight:
+            x = x.to(w.dtype)
+            b = self.bias.to(w.dtype) if self.bias is not None else None
+            return self._conv_forward(x, w, b)
+        return self._conv_forward(x, self.weight, self.bias)

@@ -191,9 +191,12 @@ def linear(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor | None = No
         if torch.is_autocast_enabled("cuda"):
             # autocast region: compute in the autocast dtype on MFMA, grads flow
             # back to the fp32 master weight through the differentiable casts
+            # (the weight's through ops.conv.cast_weight: DDP bucket grad sink)
             dt = torch.get_autocast_dtype("cuda")
-            if dt in (torch.bfloat16, torch.float32):
-                x, weight = x.to(dt), weight.to(dt)
+            if dt == torch.bfloat16:
+                from .conv import cast_weight
+
+                x, weight = x.to(dt), cast_weight(weight)
         if x.dtype not in (torch.float32, torch.bfloat16) or weight.dtype != x.dtype:
             raise TypeError(f"native linear supports fp32/bf16 with matching dtypes, got {x.dtype}/{weight.dtype}")
         return _LinearFn.apply(x, weight, bias, relu)

@@ -48,6 +48,7 @@ class _BatchNormActFn(torch.autograd.Function):
         y, stats = native().bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, residual, relu, momentum,
                                          eps, tickets)
         ctx.tickets = tickets
+        ctx.params = (weight, bias)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, y if relu else None, weight, stats)
@@ -58,8 +59,13 @@ class _BatchNormActFn(torch.autograd.Function):
         x, y, weight, stats = ctx.saved_tensors
         want_dw = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         want_dres = ctx.has_res and ctx.needs_input_grad[3]
+        sinks = [None, None]
+        if want_dw:  # DDP grad sinks (ops/conv.py): write dweight/dbias straight into the bucket slots
+            for k, p in enumerate(ctx.params):
+                if p is not None and p.grad is None and getattr(p, "_ptdt_grad_sink", None) is not None:
+                    sinks[k] = p._ptdt_grad_sink()
         dx, dw, db, dres = native().bn_bwd(_like(dy, x), x, y, weight, stats, ctx.relu, want_dres, want_dw,
-                                           ctx.tickets)
+                                           ctx.tickets, sinks[0], sinks[1])
         return (dx if ctx.needs_input_grad[0] else None, dw if want_dw else None, db if want_dw else None,
                 dres if want_dres else None, None, None, None, None, None, None, None)
 

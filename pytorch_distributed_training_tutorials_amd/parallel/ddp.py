@@ -98,6 +98,21 @@ class DistributedDataParallel(nn.Module):
                                         py_ar, find_unused_parameters)
         self._queued = False
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
+        # grad sinks (ops/conv.py): weights cast through SinkCast land their gradient directly in
+        # the bucket slot when .grad is None, which zero_grad arranges for exactly these params
+        self._sink_params = []
+        if self.device.type == "cuda":
+            from ..ops.conv import Conv2d
+            from ..ops.linear import Linear
+            from ..ops.norm import BatchNorm2d
+
+            sink_ids = {id(m.weight) for m in module.modules() if isinstance(m, (Conv2d, Linear))}
+            sink_ids |= {id(t) for m in module.modules() if isinstance(m, BatchNorm2d)
+                         for t in (m.weight, m.bias) if t is not None}
+            for i, p in enumerate(params):
+                if id(p) in sink_ids:
+                    p._ptdt_grad_sink = (lambda i=i, r=self.reducer: r.grad_view(i))
+                    self._sink_params.append(p)
 
     # --------------------------------------------------------------- internals
     def _verify_shapes(self):
@@ -155,5 +170,8 @@ class DistributedDataParallel(nn.Module):
         return self.reducer.buckets()
 
     def zero_grad(self, set_to_none: bool = False):
-        """Zero the gradient buckets in place (keeps .grad as bucket views)."""
+        """Zero the gradient buckets in place (keeps .grad as bucket views; grad-sink
+        parameters get ``None``, refilled in place by their cast's backward)."""
         self.reducer.zero_grads()
+        for p in self._sink_params:
+            p.grad = None
