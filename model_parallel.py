@@ -27,6 +27,9 @@ def main(argv=None):
     ap.add_argument("--repeat", type=int, default=10)
     ap.add_argument("--split_sizes", default="20", help="pipeline micro-batch sizes, comma list")
     ap.add_argument("--channels_last", action="store_true")
+    ap.add_argument("--cudnn_benchmark", default="auto", choices=["auto", "on", "off"],
+                    help="resnet: MIOpen exhaustive solver find in the warm-up train() (auto: with --channels_last; "
+                         "the NCHW fp32 search runs minutes)")
     ap.add_argument("--fig", default="mp_vs_single.png")
     ap.add_argument("--json", default=None)
     ap.add_argument("--devices", type=int, default=4, help="placement: number of devices to plan for")
@@ -38,6 +41,9 @@ def main(argv=None):
         d0, d1 = _devs(a)
         print(f"loss {mp.toy_step(d0, d1):.6f}")
     elif a.what == "resnet":
+        import torch
+
+        torch.backends.cudnn.benchmark = a.cudnn_benchmark == "on" or (a.cudnn_benchmark == "auto" and a.channels_last)
         res = mp.benchmark(a.repeat, _devs(a), tuple(int(s) for s in a.split_sizes.split(",") if s),
                            a.channels_last, a.fig, a.json)
         print(json.dumps(res, indent=1))

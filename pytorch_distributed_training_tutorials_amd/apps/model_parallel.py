@@ -93,6 +93,7 @@ def benchmark(repeat: int = 10, devs=("cuda:0", "cuda:1"), split_sizes=(20,), ch
     for name, mk in setups.items():
         model = mk()
         in_dev = torch.device(devs[0])
+        print(f"[mp bench] {name}: warm-up (MIOpen solver search, allocator)", flush=True)
         train(model, in_dev)  # warm-up (MIOpen solver search, allocator)
         times = timeit.repeat(lambda: train(model, in_dev), number=1, repeat=repeat)
         results[name] = {"mean_s": float(np.mean(times)), "std_s": float(np.std(times)),
