@@ -205,7 +205,9 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
     pa.cursor_host_j = (int)cursor_j;
   }
   const bool wave = variant != kPersistWorkgroup && linear_wave_supported(a, pa);
-  TORCH_CHECK(wave || variant < kPersistWave, "persistent: the wave engine does not support this configuration");
+  const bool mfma = !wave && mlp_mfma_persistent_supported(a, pa);
+  TORCH_CHECK(wave || mfma || (variant < kPersistWave),
+              "persistent: the requested engine variant does not support this configuration");
   TORCH_CHECK(wave || fused_mlp_persistent_lds_bytes((int)B, (int)Din, (int)H, (int)Dout, (int)num_samples,
                                                      world) <= 160 * 1024,
               "persistent: model + epoch index list do not fit one workgroup's LDS");
@@ -229,6 +231,7 @@ std::string persistent_engine(int64_t B, int64_t Din, int64_t H, int64_t Dout, i
     linear_wave_layout(a, pa, &L, &R, &kp);
     return "wave:L" + std::to_string(L) + "R" + std::to_string(R) + "K" + std::to_string(kp);
   }
+  if (variant != kPersistWorkgroup && mlp_mfma_persistent_supported(a, pa)) return "workgroup:mfma";
   return "workgroup";
 }
 

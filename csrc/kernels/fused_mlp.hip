@@ -437,6 +437,247 @@ __global__ void __launch_bounds__(1024) fused_mlp_step_kernel(FusedMlpArgs a) {
 }
 
 // ------------------------------------------------------------------ persistent engine
+// ---------------------------------------------------------------------------
+// MFMA step body for Linear(Din, H)-ReLU-Linear(H, Dout) (the "toy MLP"):
+// four waves, every product on v_mfma_f32_16x16x4f32 (exact fp32 multiply-adds)
+// with LDS-staged operand tiles, instead of the LDS dot products of step_body.
+// Shapes: B <= 32 rows, Din <= 32, H in {16, 32, 48, 64} (wave w owns hidden
+// tile w), Dout <= 16. LDS matrices use padded row strides (H+8, 17) so the
+// lanes reading a fragment hit at most 2 lanes per bank.
+// Layout of v_mfma_f32_16x16x4f32: lane l supplies A[l%16][l/16] and
+// B[l/16][l%16]; the result lane holds C[4*(l/16) + r][l%16], r = 0..3.
+//   fwd1  A1 = relu(X W1^T + b1)       wave w: rows 0-31 x hidden 16w..16w+15
+//   fwd2  Z2 = A1 W2^T + b2, loss,      waves 0/1: rows 16w..16w+15; the
+//         dL/dZ2 in registers           softmax row reductions are DPP adds
+//                                       inside one 16-lane DPP row
+//   bwd   dW2 = dZ2^T A1, dA1 = dZ2 W2, dZ1 = dA1 * [A1 > 0], db1 (permlane
+//         swaps across the 4 DPP rows), dW1 = dZ1^T X; db2 from fwd2's partials
+typedef __attribute__((ext_vector_type(4))) float mf4;
+
+__device__ __forceinline__ mf4 mfma4(float a, float b, mf4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f<kDppXor1>(v));
+  v = fmaxf(v, dpp_f<kDppXor2>(v));
+  v = fmaxf(v, dpp_f<kDppHalfMirror>(v));
+  return fmaxf(v, dpp_f<kDppMirror>(v));
+}
+// sum of the 4 lanes l%16 == c (one per DPP row), in all of them
+__device__ __forceinline__ float across_rows_sum(float v) {
+  auto p = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+  v = __int_as_float(p[0]) + __int_as_float(p[1]);
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_int(v), __float_as_int(v), false, false);
+  return __int_as_float(q[0]) + __int_as_float(q[1]);
+}
+
+constexpr int kMfThreads = 256;
+constexpr int kMfRows = 32;
+constexpr int kMfZ = 17;  // dz row stride (Dout <= 16)
+// a1 / dz1 / w2p row stride: fragments are read both with lanes along rows (c*la + g)
+// and along columns (g*la + c); H + 8 keeps both at <= 2-way bank conflicts
+__host__ __device__ constexpr int kMfPad(int H) { return H + 8; }
+
+__host__ __device__ inline bool mlp_mfma_shape_ok(int B, int Din, int H, int Dout) {
+  return B >= 1 && B <= kMfRows && Din >= 1 && Din <= 32 && H >= 16 && H <= 64 && H % 16 == 0 && Dout >= 1 &&
+         Dout <= 16;
+}
+
+// Operands of a whole K chain are loaded into registers first (all LDS reads in
+// flight together), then the MFMAs run as two independent accumulator chains:
+// the step is otherwise a series of LDS-latency + MFMA-latency round trips.
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS traffic,
+// not for its global loads, so the next step's register prefetch stays in flight
+// (__syncthreads' workgroup fence would drain it -- cdna_hip_programming.md §5).
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+}
+
+template <int NK>
+__device__ __forceinline__ mf4 mfma_chain(const float (&av)[NK], const float (&bv)[NK]) {
+  mf4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < NK; k += 2) {
+    c0 = mfma4(av[k], bv[k], c0);
+    if (k + 1 < NK) c1 = mfma4(av[k + 1], bv[k + 1], c1);
+  }
+  return c0 + c1;
+}
+
+template <int LOSS, int HT>
+__device__ __forceinline__ void step_body_mfma(const FusedMlpArgs& a, const Dims& d, const float* Ps,
+                                               const Scratch& s, float* gdst, float* loss_out, int tid, Stamps& st) {
+  constexpr int H = 16 * HT, la = kMfPad(H);
+  const int B = d.B, Din = d.Din, Dout = d.Dout;
+  const float* W1 = Ps;
+  const float* b1 = Ps + d.nW1;
+  const float* W2 = Ps + d.nW1 + d.nb1;
+  const float* b2 = W2 + d.nW2;
+  const bool bias1 = d.nb1 != 0, bias2 = d.nb2 != 0;
+  float* a1 = s.as;   // [32][la] relu(Z1), rows >= B zero
+  float* dz = s.zs;   // [32][17]  dL/dZ2, scaled; rows >= B and cols >= Dout zero
+  float* dz1 = s.ds;  // [32][la] dL/dZ1
+  float* w2p = s.ds;  // [Dout][la] W2 copy for fwd2 (dead before dz1 is written)
+  float* red = s.red; // [64]: loss partials, db2 partials
+  const float* xs = s.xs;
+  const int w = tid >> 6, l = tid & 63, g = l >> 4, c = l & 15;
+  float* gW1 = gdst;
+  float* gb1 = gdst + d.nW1;
+  float* gW2 = gdst + d.nW1 + d.nb1;
+  float* gb2 = gW2 + d.nW2;
+
+  for (int e = tid; e < Dout * H; e += kMfThreads) {
+    const int o = e / H;
+    w2p[o * la + (e - o * H)] = W2[e];
+  }
+  // ---- fwd1: wave w -> hidden tile w, both 16-row tiles (K = Din <= 32: 8 steps, masked)
+  if (w < HT) {
+    const int h = 16 * w + c;
+    const float bb = bias1 ? b1[h] : 0.f;
+    float bv[8], av0[8], av1[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = 4 * q + g;
+      const bool kin = k < Din;
+      bv[q] = kin ? W1[h * Din + k] : 0.f;
+      av0[q] = (kin && c < B) ? xs[c * Din + k] : 0.f;
+      av1[q] = (kin && 16 + c < B) ? xs[(16 + c) * Din + k] : 0.f;
+    }
+    const mf4 z0 = mfma_chain<8>(av0, bv), z1 = mfma_chain<8>(av1, bv);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int r0 = 4 * g + r, r1 = 16 + 4 * g + r;
+      a1[r0 * la + h] = r0 < B ? fmaxf(z0[r] + bb, 0.f) : 0.f;
+      a1[r1 * la + h] = r1 < B ? fmaxf(z1[r] + bb, 0.f) : 0.f;
+    }
+  }
+  lds_sync();
+  // ---- fwd2 + loss + dL/dZ2 (waves 0, 1: row tile w)
+  if (w < 2) {
+    float av[4 * HT], bv[4 * HT];
+#pragma unroll
+    for (int q = 0; q < 4 * HT; ++q) {
+      av[q] = a1[(16 * w + c) * la + 4 * q + g];
+      bv[q] = c < Dout ? w2p[c * la + 4 * q + g] : 0.f;
+    }
+    const mf4 acc = mfma_chain<4 * HT>(av, bv);
+    st.tick(1);
+    const bool col = c < Dout;
+    const float bz = (bias2 && col) ? b2[c] : 0.f;
+    float denom;
+    if constexpr (LOSS == kLossCEIndex) {
+      const int* yl = reinterpret_cast<const int*>(s.ys);
+      const bool v = l < B && yl[l] != a.ignore_index;
+      denom = (float)__builtin_popcountll(__ballot(v));
+    } else {
+      denom = (LOSS == kLossMSE) ? (float)(B * Dout) : (float)B;
+    }
+    const float coef = a.grad_scale / (denom > 0.f ? denom : 1.f);
+    float lsum = 0.f, csum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = 16 * w + 4 * g + r;
+      const bool rv = row < B;
+      const float z = acc[r] + bz;
+      float dzv = 0.f;
+      if constexpr (LOSS == kLossMSE) {
+        const float t = (rv && col) ? s.ys[row * Dout + c] : 0.f;
+        const float df = (rv && col) ? z - t : 0.f;
+        lsum = fmaf(df, df, lsum);
+        dzv = 2.f * df;
+      } else {
+        const float m = row16_max(col ? z : -INFINITY);
+        const float ez = col ? __expf(z - m) : 0.f;
+        const float lse = m + __logf(group_sum<16>(ez));
+        if constexpr (LOSS == kLossCESoft) {
+          const float t = (rv && col) ? s.ys[row * Dout + c] : 0.f;
+          const float tsum = group_sum<16>(t);
+          const float lrow = group_sum<16>(col ? -t * (z - lse) : 0.f);
+          if (c == 0) lsum += lrow;
+          dzv = (rv && col) ? __expf(z - lse) * tsum - t : 0.f;
+        } else {
+          const int y = rv ? reinterpret_cast<const int*>(s.ys)[row] : -1;
+          const bool ok = rv && y != a.ignore_index;
+          if (ok && c == y) lsum += lse - z;
+          dzv = (ok && col) ? __expf(z - lse) - (c == y ? 1.f : 0.f) : 0.f;
+        }
+      }
+      dzv *= coef;
+      dz[row * kMfZ + c] = dzv;
+      csum += dzv;
+    }
+    const float lw = wave_sum(lsum);
+    const float cs = across_rows_sum(csum);  // this row tile's column sums (db2 partials)
+    if (l == 0) red[w] = lw;
+    if (l < 16) red[16 + 16 * w + l] = cs;
+    if (tid == 0) red[2] = denom;
+  }
+  lds_sync();
+  st.tick(2);
+  if (tid == 0) {
+    if constexpr (LOSS == kLossCEIndex) *loss_out = red[2] > 0.f ? (red[0] + red[1]) / red[2] : NAN;
+    else *loss_out = (red[0] + red[1]) / red[2];
+  }
+  // ---- backward: dW2, dA1 -> dZ1, db1, db2 (wave w: hidden tile w)
+  if (w < HT) {
+    const int h = 16 * w + c;
+    float av[8], bv[8], ad0[4], ad1[4], bw[4], m0[4], m1[4];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {  // dW2[o][h] = sum_row dz[row][o] a1[row][h]
+      av[q] = dz[(4 * q + g) * kMfZ + c];
+      bv[q] = a1[(4 * q + g) * la + h];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // dA1[row][h] = sum_o dz[row][o] W2[o][h]
+      const int o = 4 * q + g;
+      ad0[q] = dz[c * kMfZ + o];
+      ad1[q] = dz[(16 + c) * kMfZ + o];
+      bw[q] = o < Dout ? W2[o * H + h] : 0.f;
+      m0[q] = a1[(4 * g + q) * la + h];
+      m1[q] = a1[(16 + 4 * g + q) * la + h];
+    }
+    const mf4 gw2 = mfma_chain<8>(av, bv);
+    const mf4 da0 = mfma_chain<4>(ad0, bw), da1 = mfma_chain<4>(ad1, bw);
+    float db = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int o = 4 * g + r;
+      if (o < Dout) gW2[o * H + h] = gw2[r];
+      const float v0 = m0[r] > 0.f ? da0[r] : 0.f, v1 = m1[r] > 0.f ? da1[r] : 0.f;
+      dz1[(4 * g + r) * la + h] = v0;
+      dz1[(16 + 4 * g + r) * la + h] = v1;
+      db += v0 + v1;
+    }
+    db = across_rows_sum(db);
+    if (bias1 && l < 16) gb1[h] = db;
+  }
+  if (bias2 && tid < Dout) gb2[tid] = red[16 + tid] + red[32 + tid];
+  lds_sync();
+  // ---- dW1[h][k] = sum_row dz1[row][h] x[row][k]
+  if (w < HT) {
+    float av[8], bv0[8], bv1[8];
+    const bool two = Din > 16;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int row = 4 * q + g;
+      av[q] = dz1[row * la + 16 * w + c];
+      bv0[q] = (row < B && c < Din) ? xs[row * Din + c] : 0.f;
+      bv1[q] = (two && row < B && 16 + c < Din) ? xs[row * Din + 16 + c] : 0.f;
+    }
+    const mf4 g0 = mfma_chain<8>(av, bv0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (c < Din) gW1[(16 * w + 4 * g + r) * Din + c] = g0[r];
+    if (two) {
+      const mf4 g1 = mfma_chain<8>(av, bv1);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (16 + c < Din) gW1[(16 * w + 4 * g + r) * Din + 16 + c] = g1[r];
+    }
+  }
+}
+
 // Per-thread register prefetch of the NEXT step's batch rows: the global loads
 // are issued before this step's compute and written to the other LDS batch
 // buffer after it, so the gather latency is off the critical path.
@@ -482,8 +723,8 @@ struct Prefetch {
   }
 };
 
-template <bool HID, int LOSS>
-__global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs a, PersistArgs pa) {
+template <bool HID, int LOSS, bool MF>
+__global__ void __launch_bounds__(MF ? kMfThreads : 1024) fused_mlp_persistent_kernel(FusedMlpArgs a, PersistArgs pa) {
   extern __shared__ float lds[];
   constexpr bool FY = LOSS != kLossCEIndex;
   const int tid = threadIdx.x, NT = blockDim.x;
@@ -503,10 +744,16 @@ __global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs
   const int ystride = ylen;
   Scratch s;
   s.as = ys0 + 2 * ystride;
-  s.zs = s.as + al4(B * full.H);
-  s.ds = s.zs + al4(B * full.Dout);
-  s.red = s.ds + al4(B * full.H);
-  float* tmp = s.red + 32;                         // [world * np]
+  if constexpr (MF) {  // MFMA body: padded row strides, 32 rows (mlp_mfma_lds_floats)
+    s.zs = s.as + al4(kMfRows * kMfPad(full.H));
+    s.ds = s.zs + al4(kMfRows * kMfZ);
+    s.red = s.ds + al4(kMfRows * kMfPad(full.H));
+  } else {
+    s.zs = s.as + al4(B * full.H);
+    s.ds = s.zs + al4(B * full.Dout);
+    s.red = s.ds + al4(B * full.H);
+  }
+  float* tmp = s.red + (MF ? 64 : 32);             // [world * np]
   int* const eb0 = reinterpret_cast<int*>(tmp + al4((a.ar.world > 1 ? a.ar.world : 1) * np));  // epoch lists
   const int estride = al4(pa.num_samples);
   auto ebuf = [&](int e) { return eb0 + (e & 1) * estride; };
@@ -567,16 +814,35 @@ __global__ void __launch_bounds__(1024) fused_mlp_persistent_kernel(FusedMlpArgs
     s.xs = xs0 + cur * xstride;
     s.ys = ys0 + cur * ystride;
     const Dims d(batch_size(j), full.Din, full.H, full.Dout, a.has_bias != 0);
-    step_body<HID, LOSS>(a, d, Ps, s, gs, false, pa.losses + step, tid, NT, st);
-    __syncthreads();
+    if constexpr (MF) {
+      switch (full.H >> 4) {  // uniform: one hidden-width instantiation per launch
+        case 1: step_body_mfma<LOSS, 1>(a, d, Ps, s, gs, pa.losses + step, tid, st); break;
+        case 2: step_body_mfma<LOSS, 2>(a, d, Ps, s, gs, pa.losses + step, tid, st); break;
+        case 3: step_body_mfma<LOSS, 3>(a, d, Ps, s, gs, pa.losses + step, tid, st); break;
+        default: step_body_mfma<LOSS, 4>(a, d, Ps, s, gs, pa.losses + step, tid, st); break;
+      }
+      lds_sync();  // grads visible; the prefetch is still in flight
+    } else {
+      step_body<HID, LOSS>(a, d, Ps, s, gs, false, pa.losses + step, tid, NT, st);
+      __syncthreads();
+    }
     st.tick(3);
     seq += 1u;
     allreduce_lds(a.ar, seq, gs, tmp, np, tid, NT, lds_err);
     st.tick(4);
     const bool first = opt_step == 0;
-    for (int i = tid; i < np; i += NT)
-      Ps[i] = sgd_one(Ps[i], gs[i], use_mom ? Ms : nullptr, i, first, a.lr, a.momentum, a.dampening,
-                      a.weight_decay, a.nesterov);
+    {  // 4 independent updates per iteration: their LDS loads overlap instead of chaining
+      int i = tid;
+      for (; i + 3 * NT < np; i += 4 * NT) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          Ps[i + u * NT] = sgd_one(Ps[i + u * NT], gs[i + u * NT], use_mom ? Ms : nullptr, i + u * NT, first, a.lr,
+                                   a.momentum, a.dampening, a.weight_decay, a.nesterov);
+      }
+      for (; i < np; i += NT)
+        Ps[i] = sgd_one(Ps[i], gs[i], use_mom ? Ms : nullptr, i, first, a.lr, a.momentum, a.dampening,
+                        a.weight_decay, a.nesterov);
+    }
     ++opt_step;
     // land the prefetched batch in the other buffer (last read two steps ago)
     if (have_next) {
@@ -636,13 +902,18 @@ const void* pick_loss(int loss, int mode) {
   }
 }
 
-template <bool HID>
+template <bool HID, bool MF = false>
 const void* pick_persist(int loss) {
   switch (loss) {
-    case kLossCEIndex: return (const void*)fused_mlp_persistent_kernel<HID, kLossCEIndex>;
-    case kLossMSE: return (const void*)fused_mlp_persistent_kernel<HID, kLossMSE>;
-    default: return (const void*)fused_mlp_persistent_kernel<HID, kLossCESoft>;
+    case kLossCEIndex: return (const void*)fused_mlp_persistent_kernel<HID, kLossCEIndex, MF>;
+    case kLossMSE: return (const void*)fused_mlp_persistent_kernel<HID, kLossMSE, MF>;
+    default: return (const void*)fused_mlp_persistent_kernel<HID, kLossCESoft, MF>;
   }
+}
+
+bool mfma_engine(const FusedMlpArgs& a, const PersistArgs& p) {
+  return a.H > 0 && (p.variant == kPersistAuto || p.variant == kPersistMfma) &&
+         mlp_mfma_shape_ok(a.B, a.Din, a.H, a.Dout);
 }
 
 hipError_t check_dims(const FusedMlpArgs& a) {
@@ -671,9 +942,13 @@ size_t fused_mlp_lds_bytes(int B, int Din, int H, int Dout) {
 size_t fused_mlp_persistent_lds_bytes(int B, int Din, int H, int Dout, int num_samples, int world) {
   const int Dh = H > 0 ? H : Din;
   const int np = (H > 0 ? H * Din + H : 0) + Dout * Dh + Dout;
-  const int64_t fl = 3 * (int64_t)al4(np) + 2 * al4(B * Din) + 2 * al4(B * H) + al4(B * Dout) +
-                     2 * al4(B * Dout > B ? B * Dout : B) + 32 + al4((world > 1 ? world : 1) * np) +
-                     2 * al4(num_samples) + 4;
+  const int64_t common = 3 * (int64_t)al4(np) + 2 * al4(B * Din) + 2 * al4(B * Dout > B ? B * Dout : B) +
+                         al4((world > 1 ? world : 1) * np) + 2 * al4(num_samples) + 4;
+  int64_t fl = common + 2 * al4(B * H) + al4(B * Dout) + 32;
+  if (H > 0 && mlp_mfma_shape_ok(B, Din, H, Dout)) {  // the MFMA body's padded scratch (the larger of the two)
+    const int64_t mf = common + 2 * al4(kMfRows * kMfPad(H)) + al4(kMfRows * kMfZ) + 64;
+    if (mf > fl) fl = mf;
+  }
   return (size_t)fl * sizeof(float);
 }
 
@@ -706,15 +981,20 @@ hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hip
       p.cursor_host_j + p.n_steps > (p.num_samples + a.B - 1) / a.B)
     return hipErrorInvalidValue;  // an explicit index list covers one epoch only
   if (p.variant != kPersistWorkgroup && linear_wave_supported(a, p)) return linear_wave_persistent(a, p, s);
-  if (p.variant >= kPersistWave) return hipErrorInvalidValue;
+  if (p.variant >= kPersistWave && p.variant != kPersistMfma) return hipErrorInvalidValue;
   const size_t lds = fused_mlp_persistent_lds_bytes(a.B, a.Din, a.H, a.Dout, p.num_samples, a.ar.world);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  const void* fn = a.H > 0 ? pick_persist<true>(a.loss_kind) : pick_persist<false>(a.loss_kind);
+  const bool mf = mfma_engine(a, p);
+  if (p.variant == kPersistMfma && !mf) return hipErrorInvalidValue;
+  const void* fn = mf ? pick_persist<true, true>(a.loss_kind)
+                      : (a.H > 0 ? pick_persist<true>(a.loss_kind) : pick_persist<false>(a.loss_kind));
   if (lds > 64 * 1024)
     PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  const int threads = a.H > 0 ? 1024 : 256;
+  const int threads = mf ? kMfThreads : (a.H > 0 ? 1024 : 256);
   void* args[] = {const_cast<FusedMlpArgs*>(&a), const_cast<PersistArgs*>(&p)};
   return hipLaunchKernel(fn, dim3(1), dim3(threads), args, lds, s);
 }
+
+bool mlp_mfma_persistent_supported(const FusedMlpArgs& a, const PersistArgs& p) { return mfma_engine(a, p); }
 
 }  // namespace ptdt

@@ -85,11 +85,16 @@ struct PersistArgs {
 // kPersistWaveRows / kPersistWaveF restrict the wave engine to one lane-layout
 // family (row groups across DPP rows / feature groups across DPP rows).
 constexpr int kWavePrefetch = 3;  // batches in flight in the wave engine (register buffers)
+// kPersistMfma: the workgroup engine with the 4-wave MFMA step body for
+// Linear-ReLU-Linear (B <= 32, Din <= 32, H in 16..64 step 16, Dout <= 16);
+// kPersistAuto picks it for those shapes.
 enum PersistVariant : int {
-  kPersistAuto = 0, kPersistWorkgroup = 1, kPersistWave = 2, kPersistWaveRows = 3, kPersistWaveF = 4
+  kPersistAuto = 0, kPersistWorkgroup = 1, kPersistWave = 2, kPersistWaveRows = 3, kPersistWaveF = 4,
+  kPersistMfma = 5
 };
 hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s);
 bool linear_wave_supported(const FusedMlpArgs& a, const PersistArgs& p);
+bool mlp_mfma_persistent_supported(const FusedMlpArgs& a, const PersistArgs& p);
 // lane layout the wave engine picks: L lanes per row, R rows per lane group, kp features per lane
 void linear_wave_layout(const FusedMlpArgs& a, const PersistArgs& p, int* L, int* R, int* kp);
 hipError_t linear_wave_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s);

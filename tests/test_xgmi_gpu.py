@@ -94,7 +94,9 @@ def test_persistent_engine_world1_equals_per_step(dev):
             if mode == "persistent":
                 cursor = torch.zeros(2, dtype=torch.int32, device=dev)
                 losses = torch.zeros(40, device=dev)
-                eng.run_persistent(X, Y, 150, 32, sampler, cursor, losses, max_steps_per_launch=40)
+                # the LDS workgroup body: same summation order as the per-step kernel (bitwise-close)
+                eng.run_persistent(X, Y, 150, 32, sampler, cursor, losses, max_steps_per_launch=40,
+                                   variant="workgroup" if kind == "mlp" else None)
                 torch.cuda.synchronize()
                 S = -(-X.shape[0] // 32)
                 assert cursor.tolist() == [150 // S, 150 % S]
@@ -181,3 +183,37 @@ def test_wave_engine_matches_workgroup_engine(dev, cfg):
         torch.testing.assert_close(res[w], res["per_step"], rtol=1e-5, atol=1e-5)
         torch.testing.assert_close(res[w + "_loss"], res["workgroup_loss"], rtol=1e-4, atol=1e-5, equal_nan=True)
         torch.testing.assert_close(res[w + "_G"], res["workgroup_G"], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,Din,H,Dout,loss", [(32, 20, 64, 10, "ce_index"), (16, 7, 32, 3, "ce_soft"),
+                                               (32, 32, 16, 16, "mse"), (24, 20, 48, 1, "ce_soft"),
+                                               (32, 20, 64, 10, "ce_soft")])
+def test_mfma_mlp_engine_matches_workgroup_engine(dev, B, Din, H, Dout, loss):
+    """The 4-wave MFMA step body (toy MLP) vs the LDS dot-product body: same training trajectory
+    (fp32 MFMA: only the summation order differs), partial last batches included."""
+    from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+
+    N = 7 * B + 5  # a partial batch at every epoch end
+    g = torch.Generator(device=dev).manual_seed(B + Din + H)
+    X = torch.randn(N, Din, device=dev, generator=g)
+    if loss == "ce_index":
+        Y = torch.randint(0, Dout, (N,), device=dev, generator=g)
+    elif loss == "ce_soft":
+        Y = torch.rand(N, Dout, device=dev, generator=g)
+    else:
+        Y = torch.randn(N, Dout, device=dev, generator=g)
+    out = {}
+    for variant in ("mfma", "workgroup"):
+        torch.manual_seed(3)
+        eng = FusedMLPStep(ToyMLP(Din, H, Dout).to(dev), loss=loss, lr=0.05, momentum=0.9)
+        sampler = DeviceDistributedSampler(N, 1, 0, seed=2, device=dev)
+        assert eng.persistent_engine(B, sampler, variant) == ("workgroup:mfma" if variant == "mfma" else "workgroup")
+        cursor = torch.zeros(2, dtype=torch.int32, device=dev)
+        losses = torch.zeros(64, device=dev)
+        eng.run_persistent(X, Y, 40, B, sampler, cursor, losses, max_steps_per_launch=64, variant=variant)
+        torch.cuda.synchronize()
+        out[variant] = (eng.P.clone(), losses[:40].clone())
+    torch.testing.assert_close(out["mfma"][1], out["workgroup"][1], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(out["mfma"][0], out["workgroup"][0], rtol=1e-4, atol=1e-5)
