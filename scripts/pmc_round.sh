@@ -25,6 +25,10 @@ for p in ${PASSES:-gemm}; do
     mlp)  M="python3 bench.py --model mlp --steps 5000 --warmup 500"
           pass mlp_sq "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA" $M
           pass mlp_lds "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_BRANCH" $M ;;
+    bn)   N="python3 benchmarks/bn_bench.py --iters 5"
+          pass bn_fetch "FETCH_SIZE GRBM_GUI_ACTIVE GRBM_COUNT" $N
+          pass bn_write "WRITE_SIZE" $N
+          pass bn_sq "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" $N ;;
   esac
 done
 echo "=== done"
