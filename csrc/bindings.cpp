@@ -725,8 +725,7 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::op
   BnBwdArgs a{};
   a.dy = dy.data_ptr();
   a.x = x.data_ptr();
-  if (relu) {
-    TORCH_CHECK(y.has_value() && y->defined(), "batchnorm: relu backward needs the forward output");
+  if (relu && y.has_value() && y->defined()) {  // else: the mask is recomputed from x (no residual)
     same_rows(*y, x, "y");
     a.y = y->data_ptr();
   }
@@ -746,6 +745,8 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::op
   a.p.weight = opt_f32(weight, C, "weight");
   a.p.mean = st;
   a.p.invstd = st + C;
+  a.p.scale = st + 2 * C;
+  a.p.shift = st + 3 * C;
   float* d = dwb.data_ptr<float>();
   a.p.dweight = want_dweight ? d : nullptr;
   a.p.dbias = want_dweight ? d + C : nullptr;

@@ -31,6 +31,9 @@
 //   dx    = k dy' - k s2 (x - mean) - k s1,   k = gamma invstd,
 //           s1 = dbeta / M, s2 = invstd^2 sum dy'(x - mean) / M
 // i.e. dx = A dy' + B x + C per channel; with a residual branch d(residual) = dy'.
+// The ReLU mask comes from the forward output y, or -- for BNs without a residual
+// -- is recomputed from x with the forward's own fmaf(x, scale, shift), sparing
+// one of the three reads in both backward passes.
 #include "common.h"
 #include "kernels.h"
 
@@ -307,7 +310,17 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const T* __restrict_
   }
 }
 
-template <typename T, bool RELU>
+// MASK: 0 no ReLU, 1 ReLU mask from the forward output y, 2 ReLU mask recomputed
+// from x (y > 0 <=> fmaf(x, scale, shift) > 0 bit-exactly, as the forward applied
+// it): BNs without a residual skip reading y in both backward passes.
+template <int MASK, int V>
+__device__ __forceinline__ float masked_dy(float g, float x, float y, float sc, float sf) {
+  if constexpr (MASK == 1) return y > 0.f ? g : 0.f;
+  if constexpr (MASK == 2) return fmaf(x, sc, sf) > 0.f ? g : 0.f;
+  return g;
+}
+
+template <typename T, int MASK>
 __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                              const T* __restrict__ y, int64_t M, int C, int TC,
                                                              int RPI, int64_t rows_per_block, float* ws,
@@ -325,9 +338,13 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
 #pragma unroll
   for (int v = 0; v < V; ++v) acc[0][v] = acc[1][v] = 0.f;
   if (active) {
-    float mu[V];
+    float mu[V], sc[V], sf[V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) mu[v] = p.mean[c0 + v];
+    for (int v = 0; v < V; ++v) {
+      mu[v] = p.mean[c0 + v];
+      sc[v] = MASK == 2 ? p.scale[c0 + v] : 0.f;
+      sf[v] = MASK == 2 ? p.shift[c0 + v] : 0.f;
+    }
     int64_t r = r0 + rr;
     for (; r + (U - 1) * RPI < r1; r += U * RPI) {
       float g[U][V], a[U][V], o[U][V];
@@ -336,13 +353,13 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
         const int64_t off = (r + u * RPI) * C + c0;
         VecIO<T>::load(dy + off, g[u]);
         VecIO<T>::load(x + off, a[u]);
-        if constexpr (RELU) VecIO<T>::load(y + off, o[u]);
+        if constexpr (MASK == 1) VecIO<T>::load(y + off, o[u]);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int v = 0; v < V; ++v) {
-          const float gg = RELU ? (o[u][v] > 0.f ? g[u][v] : 0.f) : g[u][v];
+          const float gg = masked_dy<MASK, V>(g[u][v], a[u][v], MASK == 1 ? o[u][v] : 0.f, sc[v], sf[v]);
           acc[0][v] += gg;
           acc[1][v] = fmaf(gg, a[u][v] - mu[v], acc[1][v]);
         }
@@ -352,10 +369,10 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
       const int64_t off = r * C + c0;
       VecIO<T>::load(dy + off, g);
       VecIO<T>::load(x + off, a);
-      if constexpr (RELU) VecIO<T>::load(y + off, o);
+      if constexpr (MASK == 1) VecIO<T>::load(y + off, o);
 #pragma unroll
       for (int v = 0; v < V; ++v) {
-        const float gg = RELU ? (o[v] > 0.f ? g[v] : 0.f) : g[v];
+        const float gg = masked_dy<MASK, V>(g[v], a[v], MASK == 1 ? o[v] : 0.f, sc[v], sf[v]);
         acc[0][v] += gg;
         acc[1][v] = fmaf(gg, a[v] - mu[v], acc[1][v]);
       }
@@ -385,18 +402,21 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
   if (tid == 0) rearm(tickets + blockIdx.y);
 }
 
-template <typename T, bool RELU, bool RES>
+template <typename T, int MASK, bool RES>
 __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                                 const T* __restrict__ y, T* __restrict__ dx,
-                                                                T* __restrict__ dres, const float* __restrict__ ca,
-                                                                const float* __restrict__ cb,
-                                                                const float* __restrict__ cc, int64_t nvec, int C) {
+                                                                T* __restrict__ dres, BnBwdParams p, int64_t nvec,
+                                                                int C) {
   constexpr int V = VecIO<T>::V;
-  extern __shared__ float sh[];  // A[C], B[C], C[C]
+  extern __shared__ float sh[];  // A[C], B[C], C[C] (+ scale[C], shift[C] for MASK 2)
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    sh[c] = ca[c];
-    sh[C + c] = cb[c];
-    sh[2 * C + c] = cc[c];
+    sh[c] = p.coef_a[c];
+    sh[C + c] = p.coef_b[c];
+    sh[2 * C + c] = p.coef_c[c];
+    if constexpr (MASK == 2) {
+      sh[3 * C + c] = p.scale[c];
+      sh[4 * C + c] = p.shift[c];
+    }
   }
   __syncthreads();
   const int cv = C / V;
@@ -406,10 +426,11 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const T* __restr
     float g[V], a[V], o[V];
     VecIO<T>::load(dy + i * V, g);
     VecIO<T>::load(x + i * V, a);
-    if constexpr (RELU) VecIO<T>::load(y + i * V, o);
+    if constexpr (MASK == 1) VecIO<T>::load(y + i * V, o);
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      if constexpr (RELU) g[v] = o[v] > 0.f ? g[v] : 0.f;
+      g[v] = masked_dy<MASK, V>(g[v], a[v], MASK == 1 ? o[v] : 0.f, MASK == 2 ? sh[3 * C + c0 + v] : 0.f,
+                                MASK == 2 ? sh[4 * C + c0 + v] : 0.f);
       a[v] = fmaf(sh[c0 + v], g[v], fmaf(sh[C + c0 + v], a[v], sh[2 * C + c0 + v]));
     }
     VecIO<T>::store(dx + i * V, a);
@@ -469,36 +490,35 @@ hipError_t apply_impl(const void* x, const void* res, void* y, const float* scal
   return hipGetLastError();
 }
 
+template <typename T, int MASK>
+hipError_t bwd_launch(const BnBwdArgs& a, const Geom& g, hipStream_t s) {
+  constexpr int V = VecIO<T>::V;
+  const size_t sh_red = (size_t)2 * kRed * V * sizeof(float) + 16;
+  const T* dy = static_cast<const T*>(a.dy);
+  const T* x = static_cast<const T*>(a.x);
+  const T* y = static_cast<const T*>(a.y);
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK>), dim3(g.gx, g.gy), dim3(kRed), sh_red, s, dy, x, y, a.M, a.C,
+                     g.TC, g.RPI, g.rows_per_block, a.workspace, a.tickets, a.p);
+  PTDT_HIP_CHECK(hipGetLastError());
+  const int64_t nvec = a.M * a.C / V;
+  const size_t sh_ap = (size_t)(MASK == 2 ? 5 : 3) * a.C * sizeof(float);
+  T* dx = static_cast<T*>(a.dx);
+  T* dr = static_cast<T*>(a.dres);
+  const dim3 grid(apply_grid(nvec)), blk(kThreads);
+  if (dr) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, MASK, true>), grid, blk, sh_ap, s, dy, x, y, dx, dr, a.p, nvec, a.C);
+  else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, MASK, false>), grid, blk, sh_ap, s, dy, x, y, dx, dr, a.p, nvec, a.C);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t bwd_impl(const BnBwdArgs& a, hipStream_t s) {
   constexpr int V = VecIO<T>::V;
   if (a.C % V != 0) return hipErrorInvalidValue;
   const Geom g = geom<T>(a.M, a.C);
-  const size_t sh_red = (size_t)2 * kRed * V * sizeof(float) + 16;
-  const T* dy = static_cast<const T*>(a.dy);
-  const T* x = static_cast<const T*>(a.x);
-  const T* y = static_cast<const T*>(a.y);
-  if (a.relu)
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(g.gx, g.gy), dim3(kRed), sh_red, s, dy, x, y, a.M,
-                       a.C, g.TC, g.RPI, g.rows_per_block, a.workspace, a.tickets, a.p);
-  else
-    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(g.gx, g.gy), dim3(kRed), sh_red, s, dy, x, y, a.M,
-                       a.C, g.TC, g.RPI, g.rows_per_block, a.workspace, a.tickets, a.p);
-  PTDT_HIP_CHECK(hipGetLastError());
-  const int64_t nvec = a.M * a.C / V;
-  const size_t sh_ap = (size_t)3 * a.C * sizeof(float);
-  T* dx = static_cast<T*>(a.dx);
-  T* dr = static_cast<T*>(a.dres);
-  const dim3 grid(apply_grid(nvec)), blk(kThreads);
-  const float *A = a.p.coef_a, *B = a.p.coef_b, *Cc = a.p.coef_c;
-  if (a.relu) {
-    if (dr) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), grid, blk, sh_ap, s, dy, x, y, dx, dr, A, B, Cc, nvec, a.C);
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, false>), grid, blk, sh_ap, s, dy, x, y, dx, dr, A, B, Cc, nvec, a.C);
-  } else {
-    if (dr) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, true>), grid, blk, sh_ap, s, dy, x, y, dx, dr, A, B, Cc, nvec, a.C);
-    else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false, false>), grid, blk, sh_ap, s, dy, x, y, dx, dr, A, B, Cc, nvec, a.C);
-  }
-  return hipGetLastError();
+  if (!a.relu) return bwd_launch<T, 0>(a, g, s);
+  if (a.y != nullptr) return bwd_launch<T, 1>(a, g, s);
+  if (a.p.scale == nullptr || a.p.shift == nullptr) return hipErrorInvalidValue;
+  return bwd_launch<T, 2>(a, g, s);
 }
 
 }  // namespace

@@ -259,11 +259,12 @@ struct BnFwdArgs {
 };
 struct BnBwdParams {
   const float* weight; const float* mean; const float* invstd;
+  const float* scale; const float* shift;   // forward scale/shift: ReLU mask from x when y is null
   float* dweight; float* dbias;             // may be null
   float* coef_a; float* coef_b; float* coef_c;  // scratch [C] each
 };
 struct BnBwdArgs {
-  const void* dy; const void* x; const void* y;  // y: forward output (ReLU mask), used when relu
+  const void* dy; const void* x; const void* y;  // y: forward output (ReLU mask) or null: mask from x
   void* dx; void* dres;                          // dres (may be null): gradient of the residual = masked dy
   int dtype; int64_t M; int C; int relu;
   float* workspace; int* tickets;

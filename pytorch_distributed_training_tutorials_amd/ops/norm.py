@@ -51,7 +51,9 @@ class _BatchNormActFn(torch.autograd.Function):
         ctx.params = (weight, bias)
         ctx.relu = relu
         ctx.has_res = residual is not None
-        ctx.save_for_backward(x, y if relu else None, weight, stats)
+        # ReLU mask in the backward: from y with a residual; without one it is recomputed
+        # from x and the saved scale/shift (bit-exact), so y need not be read (or kept)
+        ctx.save_for_backward(x, y if (relu and residual is not None) else None, weight, stats)
         return y
 
     @staticmethod
