@@ -169,6 +169,20 @@ class DistributedDataParallel(nn.Module):
     def bucket_params(self):
         return self.reducer.buckets()
 
+    def remove_grad_sinks(self):
+        """Detach the parameters from this wrapper's buckets (also done when it is collected):
+        later backwards produce ordinary gradient tensors again."""
+        for p in getattr(self, "_sink_params", ()):
+            if getattr(p, "_ptdt_grad_sink", None) is not None:
+                del p._ptdt_grad_sink
+        self._sink_params = []
+
+    def __del__(self):
+        try:
+            self.remove_grad_sinks()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
     def zero_grad(self, set_to_none: bool = False):
         """Zero the gradient buckets in place (keeps .grad as bucket views; grad-sink
         parameters get ``None``, refilled in place by their cast's backward)."""
