@@ -27,6 +27,8 @@
 // Every configuration is a template instantiation (hidden layer / loss /
 // update+all-reduce mode) with 32-bit index math: no runtime branching on the
 // configuration in the executed path.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 #include "sampler.h"
@@ -527,24 +529,40 @@ __device__ __forceinline__ void step_body_mfma(const FusedMlpArgs& a, const Dims
   float* gW2 = gdst + d.nW1 + d.nb1;
   float* gb2 = gW2 + d.nW2;
 
-  for (int e = tid; e < Dout * H; e += kMfThreads) {
-    const int o = e / H;
-    w2p[o * la + (e - o * H)] = W2[e];
+  {  // W2 copy: all reads in flight, then the writes (Dout * H <= 4 * kMfThreads)
+    float t[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + q * kMfThreads;
+      t[q] = e < Dout * H ? W2[e] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int e = tid + q * kMfThreads;
+      if (e < Dout * H) w2p[(e / H) * la + (e % H)] = t[q];
+    }
   }
-  // ---- fwd1: wave w -> hidden tile w, both 16-row tiles (K = Din <= 32: 8 steps, masked)
+  // ---- fwd1: wave w -> hidden tile w, both 16-row tiles (K = Din: 5 steps up to 20, else 8, masked)
   if (w < HT) {
     const int h = 16 * w + c;
     const float bb = bias1 ? b1[h] : 0.f;
-    float bv[8], av0[8], av1[8];
+    mf4 z0, z1;
+    auto fwd1 = [&](auto nk) {
+      constexpr int NK = decltype(nk)::value;
+      float bv[NK], av0[NK], av1[NK];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int k = 4 * q + g;
-      const bool kin = k < Din;
-      bv[q] = kin ? W1[h * Din + k] : 0.f;
-      av0[q] = (kin && c < B) ? xs[c * Din + k] : 0.f;
-      av1[q] = (kin && 16 + c < B) ? xs[(16 + c) * Din + k] : 0.f;
-    }
-    const mf4 z0 = mfma_chain<8>(av0, bv), z1 = mfma_chain<8>(av1, bv);
+      for (int q = 0; q < NK; ++q) {
+        const int k = 4 * q + g;
+        const bool kin = k < Din;
+        bv[q] = kin ? W1[h * Din + k] : 0.f;
+        av0[q] = (kin && c < B) ? xs[c * Din + k] : 0.f;
+        av1[q] = (kin && 16 + c < B) ? xs[(16 + c) * Din + k] : 0.f;
+      }
+      z0 = mfma_chain<NK>(av0, bv);
+      z1 = mfma_chain<NK>(av1, bv);
+    };
+    if (Din <= 20) fwd1(std::integral_constant<int, 5>{});
+    else fwd1(std::integral_constant<int, 8>{});
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int r0 = 4 * g + r, r1 = 16 + 4 * g + r;
