@@ -741,7 +741,9 @@ struct Prefetch {
   }
 };
 
-template <bool HID, int LOSS, bool MF>
+// MF: 0 = LDS dot-product step body (1024 threads); 1..4 = the MFMA body for H = 16 * MF
+// (one hidden width per instantiation keeps the per-step code small in the instruction cache)
+template <bool HID, int LOSS, int MF>
 __global__ void __launch_bounds__(MF ? kMfThreads : 1024) fused_mlp_persistent_kernel(FusedMlpArgs a, PersistArgs pa) {
   extern __shared__ float lds[];
   constexpr bool FY = LOSS != kLossCEIndex;
@@ -762,7 +764,7 @@ __global__ void __launch_bounds__(MF ? kMfThreads : 1024) fused_mlp_persistent_k
   const int ystride = ylen;
   Scratch s;
   s.as = ys0 + 2 * ystride;
-  if constexpr (MF) {  // MFMA body: padded row strides, 32 rows (mlp_mfma_lds_floats)
+  if constexpr (MF != 0) {  // MFMA body: padded row strides, 32 rows
     s.zs = s.as + al4(kMfRows * kMfPad(full.H));
     s.ds = s.zs + al4(kMfRows * kMfZ);
     s.red = s.ds + al4(kMfRows * kMfPad(full.H));
@@ -832,13 +834,8 @@ __global__ void __launch_bounds__(MF ? kMfThreads : 1024) fused_mlp_persistent_k
     s.xs = xs0 + cur * xstride;
     s.ys = ys0 + cur * ystride;
     const Dims d(batch_size(j), full.Din, full.H, full.Dout, a.has_bias != 0);
-    if constexpr (MF) {
-      switch (full.H >> 4) {  // uniform: one hidden-width instantiation per launch
-        case 1: step_body_mfma<LOSS, 1>(a, d, Ps, s, gs, pa.losses + step, tid, st); break;
-        case 2: step_body_mfma<LOSS, 2>(a, d, Ps, s, gs, pa.losses + step, tid, st); break;
-        case 3: step_body_mfma<LOSS, 3>(a, d, Ps, s, gs, pa.losses + step, tid, st); break;
-        default: step_body_mfma<LOSS, 4>(a, d, Ps, s, gs, pa.losses + step, tid, st); break;
-      }
+    if constexpr (MF != 0) {
+      step_body_mfma<LOSS, MF>(a, d, Ps, s, gs, pa.losses + step, tid, st);
       lds_sync();  // grads visible; the prefetch is still in flight
     } else {
       step_body<HID, LOSS>(a, d, Ps, s, gs, false, pa.losses + step, tid, NT, st);
@@ -920,12 +917,21 @@ const void* pick_loss(int loss, int mode) {
   }
 }
 
-template <bool HID, bool MF = false>
+template <bool HID, int MF = 0>
 const void* pick_persist(int loss) {
   switch (loss) {
     case kLossCEIndex: return (const void*)fused_mlp_persistent_kernel<HID, kLossCEIndex, MF>;
     case kLossMSE: return (const void*)fused_mlp_persistent_kernel<HID, kLossMSE, MF>;
     default: return (const void*)fused_mlp_persistent_kernel<HID, kLossCESoft, MF>;
+  }
+}
+
+const void* pick_persist_mfma(int loss, int H) {
+  switch (H >> 4) {
+    case 1: return pick_persist<true, 1>(loss);
+    case 2: return pick_persist<true, 2>(loss);
+    case 3: return pick_persist<true, 3>(loss);
+    default: return pick_persist<true, 4>(loss);
   }
 }
 
@@ -1004,7 +1010,7 @@ hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hip
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const bool mf = mfma_engine(a, p);
   if (p.variant == kPersistMfma && !mf) return hipErrorInvalidValue;
-  const void* fn = mf ? pick_persist<true, true>(a.loss_kind)
+  const void* fn = mf ? pick_persist_mfma(a.loss_kind, a.H)
                       : (a.H > 0 ? pick_persist<true>(a.loss_kind) : pick_persist<false>(a.loss_kind));
   if (lds > 64 * 1024)
     PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
