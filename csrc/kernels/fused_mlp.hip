@@ -706,6 +706,18 @@ struct Prefetch {
   float x[kPf];
   float y[kPf];
   int yi[kPf];
+  int xb[kPf], xk[kPf];  // (row, column) of element tid + q * NT: fixed per thread, divided once
+  int yb[kPf], yk[kPf];
+  __device__ __forceinline__ void setup(int Din, int Dout, int tid, int NT) {
+#pragma unroll
+    for (int q = 0; q < kPf; ++q) {
+      const int e = tid + q * NT;
+      xb[q] = e / Din;
+      xk[q] = e - xb[q] * Din;
+      yb[q] = e / Dout;
+      yk[q] = e - yb[q] * Dout;
+    }
+  }
   __device__ __forceinline__ void issue(const FusedMlpArgs& a, const int* sel, int B, int Din, int Dout, int tid,
                                         int NT) {
     const auto X = gptr(a.X);
@@ -713,15 +725,9 @@ struct Prefetch {
 #pragma unroll
     for (int q = 0; q < kPf; ++q) {
       const int e = tid + q * NT;
-      if (e < B * Din) {
-        const int b = e / Din;
-        x[q] = X[(int64_t)sel[b] * ldx + (e - b * Din)];
-      }
+      if (xb[q] < B) x[q] = X[(int64_t)sel[xb[q]] * ldx + xk[q]];
       if constexpr (LOSS != kLossCEIndex) {
-        if (e < B * Dout) {
-          const int b = e / Dout;
-          y[q] = gptr(a.Yf)[(int64_t)sel[b] * Dout + (e - b * Dout)];
-        }
+        if (yb[q] < B) y[q] = gptr(a.Yf)[(int64_t)sel[yb[q]] * Dout + yk[q]];
       } else {
         if (e < B) yi[q] = (int)gptr(a.Yi)[sel[e]];
       }
@@ -805,6 +811,8 @@ __global__ void __launch_bounds__(MF ? kMfThreads : 1024) fused_mlp_persistent_k
   }
   __syncthreads();
 
+  Prefetch<LOSS> pf;
+  pf.setup(full.Din, full.Dout, tid, NT);
   Stamps st;
   st.on = pa.stamps != nullptr && tid == 0;
   const int64_t t_begin = st.on ? (int64_t)__builtin_amdgcn_s_memtime() : 0;
@@ -825,7 +833,6 @@ __global__ void __launch_bounds__(MF ? kMfThreads : 1024) fused_mlp_persistent_k
       __syncthreads();
     }
     st.tick(6);
-    Prefetch<LOSS> pf;
     const int nb = batch_size(nj);
     const bool have_next = step + 1 < pa.n_steps;
     if (pf_ok && have_next) pf.issue(a, ebuf(ne) + nj * B, nb, full.Din, full.Dout, tid, NT);
