@@ -242,10 +242,12 @@ def run_persistent(args, rank, world, dev, comm):
     losses = torch.zeros(min(chunk, max(args.steps, args.warmup, 1)), device=dev)
     eng.run_persistent(X, Y, max(args.warmup, 1), args.batch_size, sampler, cursor, losses, chunk, variant=variant)
     torch.cuda.synchronize(dev)
+    if _xgmi_failed(comm, dev, xg, "warmup"):
+        return _rccl_fallback(args, rank, world, dev, comm)
     t = _timed(comm, dev, lambda: eng.run_persistent(X, Y, args.steps, args.batch_size, sampler, cursor, losses,
                                                      chunk, variant=variant))
-    if xg is not None:
-        xg.check()
+    if _xgmi_failed(comm, dev, xg, "timed run"):
+        return _rccl_fallback(args, rank, world, dev, comm)
     in_sync = _replicas_in_sync(comm, eng.P)
     phase = None
     if args.stamps:  # diagnostic pass AFTER the timed region (timers cost a little)
@@ -270,6 +272,28 @@ def run_persistent(args, rank, world, dev, comm):
                          "workgroup; sampler shard recomputed in-kernel each epoch")}
     if phase:
         extra["phase_timers"] = phase
+    return t, extra
+
+
+def _xgmi_failed(comm, dev, xg, where: str) -> bool:
+    """True on EVERY rank if any rank's in-kernel xGMI poll timed out (a peer never
+    arrived): the run's numbers are void and all ranks must take the same fallback."""
+    if xg is None:
+        return False
+    bad = torch.tensor([float(xg.handle.error() != 0)], device=dev)
+    comm.all_reduce(bad, "max")
+    if bad.item() == 0:
+        return False
+    if comm.rank == 0:
+        print(f"[bench] xGMI poll timeout during the {where}; re-running with --engine fused --allreduce rccl",
+              flush=True)
+    return True
+
+
+def _rccl_fallback(args, rank, world, dev, comm):
+    args.allreduce = "rccl"
+    t, extra = run_fused(args, rank, world, dev, comm)
+    extra["fallback"] = "persistent xGMI engine timed out a poll; fused engine + RCCL all-reduce measured instead"
     return t, extra
 
 

@@ -129,3 +129,37 @@ def test_fake_two_node_ddp_run():
                 p.kill()
     lines = [m for o in outs for m in STATUS.findall(o)]
     assert sorted(lines) == [(str(g), "0", "32", "16") for g in (0, 0, 1, 1)]  # gpu id = LOCAL_RANK
+
+
+def test_bench_xgmi_timeout_fallback_is_agreed():
+    """bench.py: one rank's xGMI poll timeout makes EVERY rank take the RCCL fallback
+    (the flag is max-reduced); no xGMI handle means no fallback."""
+    import bench
+
+    class _X:
+        def __init__(self, e):
+            self.e = e
+
+        def error(self):
+            return self.e
+
+    class _XG:
+        def __init__(self, e):
+            self.handle = _X(e)
+
+    class _Comm:
+        rank, world = 0, 2
+
+        def __init__(self, peer_bad):
+            self.peer_bad = peer_bad
+
+        def all_reduce(self, t, op="sum"):
+            assert op == "max"
+            t.fill_(max(float(t.item()), float(self.peer_bad)))
+            return t
+
+    dev = torch.device("cpu")
+    assert not bench._xgmi_failed(_Comm(1), dev, None, "x")
+    assert not bench._xgmi_failed(_Comm(0), dev, _XG(0), "x")
+    assert bench._xgmi_failed(_Comm(1), dev, _XG(0), "x")  # a peer timed out
+    assert bench._xgmi_failed(_Comm(0), dev, _XG(1), "x")
