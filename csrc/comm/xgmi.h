@@ -45,15 +45,16 @@ __device__ __forceinline__ uint64_t* xgmi_slot(uint64_t* base, int parity, int s
 }
 
 // Push this rank's n values (vals: any memory readable by the caller's threads).
+// Peer-outer loop: no per-element division, consecutive lanes write consecutive words.
 __device__ __forceinline__ void xgmi_push(const XgmiArgs& x, uint32_t s, const float* vals, int n, int tid,
                                           int nt) {
   const int parity = (int)(s & 1u);
-  const int64_t tot = (int64_t)x.world * n;
-  for (int64_t e = tid; e < tot; e += nt) {
-    const int p = (int)(e / n), i = (int)(e % n);
-    const uint64_t w = ((uint64_t)s << 32) | (uint64_t)__float_as_uint(vals[i]);
-    __hip_atomic_store(xgmi_slot(x.peers[p], parity, x.rank, x.world, x.max_elems, i), w, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t hi = (uint64_t)s << 32;
+  for (int i = tid; i < n; i += nt) {
+    const uint64_t w = hi | (uint64_t)__float_as_uint(vals[i]);
+    for (int p = 0; p < x.world; ++p)
+      __hip_atomic_store(xgmi_slot(x.peers[p], parity, x.rank, x.world, x.max_elems, i), w, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -82,20 +83,41 @@ __device__ __forceinline__ float xgmi_gather_sum(const XgmiArgs& x, uint32_t s, 
 #endif
 
 #ifdef __HIPCC__
-// Poll every (rank, element) slot of elements [i0, i0+n) in parallel (one
-// outstanding uncached load per lane instead of W sequential round trips) and
-// stage the values in tmp[p * n + i]; the caller barriers, then sums in rank
-// order. A timed-out poll sets *x.err (and *lds_flag when given).
+// Poll every (rank, element) slot of elements [i0, i0+n) and stage the values
+// in tmp[p * n + i]; the caller barriers, then sums in rank order. Each thread
+// keeps U uncached loads in flight: one memory round trip per batch instead
+// of one per slot (W * n / nt of them: ~60 us per step for a 2K-parameter
+// bucket at W = 8). Slots whose word is not there yet are re-polled as a batch
+// (bounded; a timed-out poll sets *x.err and *lds_flag when given). U costs
+// 3 VGPRs per slot: 8 fits 1024-thread kernels, 256-thread kernels take 16.
+template <int U = 8>
 __device__ __forceinline__ void xgmi_gather_lds(const XgmiArgs& x, uint32_t s, int i0, int n, float* tmp,
                                                 int tid, int nt, int* lds_flag = nullptr) {
   const int parity = (int)(s & 1u);
+  const int tot = x.world * n;
   bool dead = false;  // after one timed-out slot this thread stops waiting: bounded total stall
-  for (int e = tid; e < x.world * n; e += nt) {
-    const int p = e / n, i = e - p * n;
-    uint64_t* slot = xgmi_slot(x.local, parity, p, x.world, x.max_elems, i0 + i);
-    uint64_t w = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (int e0 = tid; e0 < tot; e0 += U * nt) {
+    uint64_t w[U];
+    int off[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // issue the whole batch first
+      const int e = e0 + u * nt;
+      off[u] = -1;
+      w[u] = 0;
+      if (e < tot) {
+        const int p = e / n, i = e - p * n;
+        off[u] = (parity * x.world + p) * x.max_elems + i0 + i;
+        w[u] = __hip_atomic_load(x.local + off[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    // re-poll every slot still missing, all of them in flight together: a slot that
+    // arrives late costs one more round trip for the batch, not one per slot
     uint32_t polls = dead ? kXgmiMaxPolls : 0;
-    while ((uint32_t)(w >> 32) != s) {
+    for (;;) {
+      bool missing = false;
+#pragma unroll
+      for (int u = 0; u < U; ++u) missing |= off[u] >= 0 && (uint32_t)(w[u] >> 32) != s;
+      if (!missing) break;
       if (++polls > kXgmiMaxPolls) {
         __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (lds_flag) *lds_flag = 1;
@@ -103,9 +125,14 @@ __device__ __forceinline__ void xgmi_gather_lds(const XgmiArgs& x, uint32_t s, i
         break;
       }
       __builtin_amdgcn_s_sleep(1);
-      w = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (off[u] >= 0 && (uint32_t)(w[u] >> 32) != s)
+          w[u] = __hip_atomic_load(x.local + off[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    tmp[e] = __uint_as_float((uint32_t)w);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (off[u] >= 0) tmp[e0 + u * nt] = __uint_as_float((uint32_t)w[u]);
   }
 }
 

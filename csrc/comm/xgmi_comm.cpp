@@ -11,7 +11,8 @@ static void ok(hipError_t e, const char* what) {
 }
 
 XgmiComm::XgmiComm(int rank, int world, int max_elems, int device) : device_(device) {
-  if (world < 1 || world > kXgmiMaxRanks || rank < 0 || rank >= world || max_elems <= 0)
+  if (world < 1 || world > kXgmiMaxRanks || rank < 0 || rank >= world || max_elems <= 0 ||
+      (int64_t)2 * world * max_elems >= (int64_t)1 << 31)  // device slot offsets are 32-bit
     throw std::invalid_argument("XgmiComm: bad rank/world/max_elems");
   ok(hipSetDevice(device), "hipSetDevice");
   const size_t bytes = (size_t)2 * world * max_elems * sizeof(uint64_t);

@@ -355,11 +355,14 @@ __device__ __forceinline__ void step_body(const FusedMlpArgs& a, const Dims& d, 
 
 // Average `np` gradients held in LDS across ranks (in place). world == 1 is
 // the identity: DDP over one rank averages nothing.
+// PB: poll loads in flight per thread (16 for the 256-thread MFMA engine measured no
+// faster than 8 at W = 2 and 4, and costs step-body VGPRs)
+template <int PB = 8>
 __device__ __forceinline__ void allreduce_lds(const XgmiArgs& ar, uint32_t seq, float* gs, float* tmp, int np,
                                               int tid, int NT, int* lds_flag = nullptr) {
   if (ar.world <= 1) return;
   xgmi_push(ar, seq, gs, np, tid, NT);
-  xgmi_gather_lds(ar, seq, 0, np, tmp, tid, NT, lds_flag);
+  xgmi_gather_lds<PB>(ar, seq, 0, np, tmp, tid, NT, lds_flag);
   __syncthreads();
   const float inv_w = 1.f / (float)ar.world;
   for (int i = tid; i < np; i += NT) gs[i] = xgmi_sum_lds(tmp, ar.world, np, i) * inv_w;
