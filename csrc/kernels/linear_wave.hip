@@ -111,21 +111,28 @@ void linear_wave_layout(const FusedMlpArgs& a, const PersistArgs& p, int* L, int
   *kp = c.kp;
 }
 
-hipError_t linear_wave_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s) {
+hipError_t linear_wave_prepare(const FusedMlpArgs& a, const PersistArgs& p, PersistLaunch* out) {
   const Choice c = choose(a, p);
-  const void* fn = c.fn;
-  if (fn == nullptr) return hipErrorInvalidValue;
-  PersistArgs pr = p;
-  size_t lds = lds_bytes(p);
-  pr.loss_ring = 0;
-  if (c.L == 0 && lds + ring_bytes(a, p) <= 160 * 1024) {
-    pr.loss_ring = 1;
-    lds += ring_bytes(a, p);
+  if (c.fn == nullptr) return hipErrorInvalidValue;
+  out->fn = c.fn;
+  out->threads = kThreads;
+  out->a = a;
+  out->p = p;
+  out->p.loss_ring = 0;
+  out->lds = lds_bytes(p);
+  if (c.L == 0 && out->lds + ring_bytes(a, p) <= 160 * 1024) {
+    out->p.loss_ring = 1;
+    out->lds += ring_bytes(a, p);
   }
-  if (lds > 64 * 1024)
-    PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  void* args[] = {const_cast<FusedMlpArgs*>(&a), &pr};
-  return hipLaunchKernel(fn, dim3(1), dim3(kThreads), args, lds, s);
+  if (out->lds > 64 * 1024)
+    PTDT_HIP_CHECK(hipFuncSetAttribute(c.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)out->lds));
+  return hipSuccess;
+}
+
+hipError_t linear_wave_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s) {
+  PersistLaunch L;
+  PTDT_HIP_CHECK(linear_wave_prepare(a, p, &L));
+  return persistent_launch(L, p.n_steps, p.cursor_host_j, s);
 }
 
 }  // namespace ptdt

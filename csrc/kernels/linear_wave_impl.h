@@ -207,20 +207,26 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
   const int T = (int)((pos0 + n - 1) / S - pos0 / S);  // epoch transitions inside this launch
   auto list = [&](int e) { return elist + (e & 1) * estride; };
 
+  // only the first epoch's list is on the path to step 0 (stale reads past the
+  // launch are clamped below); e0+1 is built by the helpers after the barrier
+  const ListCache lc{pa.lcache, pa.ltag, estride};
   rank_epoch_indices_or(pa.idx, list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
-                     (int)threadIdx.x, kThreads);
-  if (T > 0)
-    rank_epoch_indices_or(pa.idx, list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1, pa.shuffle,
-                       (int)threadIdx.x, kThreads);
+                     (int)threadIdx.x, kThreads, lc);
   __syncthreads();
   if (wave != 0) {
     // producers: after the trainer starts prefetching epoch e0+i, the list of
     // e0+i-1 is dead; build e0+i+1 into its slot before the next transition.
+    const int ht = (int)threadIdx.x - 64;
+    if (ht == 0 && pa.idx == nullptr) list_cache_publish(lc, e0);
+    if (T > 0)
+      rank_epoch_indices_or(pa.idx, list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1,
+                            pa.shuffle, ht, kThreads - 64, lc);
     for (int i = 1; i <= T; ++i) {
       __syncthreads();
+      if (ht == 0 && pa.idx == nullptr) list_cache_publish(lc, e0 + i);
       if (i < T)
         rank_epoch_indices_or(pa.idx, list(e0 + i + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + i + 1,
-                           pa.shuffle, (int)threadIdx.x - 64, kThreads - 64);
+                           pa.shuffle, ht, kThreads - 64, lc);
     }
     return;
   }
@@ -677,13 +683,17 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   const int T = (int)((pos0 + n - 1) / S - pos0 / S);
   auto list = [&](int e) { return elist + (e & 1) * estride; };
 
-  // Both lists are built even when the launch stays in one epoch: the trainer
-  // reads (stale but valid) indices for the kNB positions past its last step,
-  // so every list entry it can touch is a valid dataset row (no clamp per load).
+  // Only the first epoch's list is on the path to step 0. The next one is
+  // zero-filled (row 0: the trainer reads stale-but-valid indices for the kNB
+  // positions past its last step, so every entry it can touch must be a valid
+  // dataset row -- no clamp per load) and built by the helper waves after the
+  // barrier, while the trainer runs epoch e0.
+  // With a list cache (pa.lcache) a launch that starts inside an already
+  // computed epoch copies its list instead of recomputing the permutation.
+  const ListCache lc{pa.lcache, pa.ltag, estride};
   rank_epoch_indices_or(pa.idx, list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
-                     (int)threadIdx.x, kThreads);
-  rank_epoch_indices_or(pa.idx, list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1, pa.shuffle,
-                     (int)threadIdx.x, kThreads);
+                     (int)threadIdx.x, kThreads, lc);
+  for (int k = (int)threadIdx.x; k < pa.num_samples; k += kThreads) list(e0 + 1)[k] = 0;
   // Loss ring (pa.loss_ring): the trainer stores each lane's scaled loss share
   // per step (one ds_write), the helper waves add the 64 shares and write
   // losses[] -- the per-step cross-lane loss reduction leaves the critical path.
@@ -702,11 +712,16 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
       }
       lo = hi > lo ? hi : lo;
     };
+    if (ht == 0 && pa.idx == nullptr) list_cache_publish(lc, e0);  // every thread's entries written (barrier)
+    if (T > 0)  // epoch e0+1, needed at the trainer's first barrier
+      rank_epoch_indices_or(pa.idx, list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1,
+                            pa.shuffle, ht, hn, lc);
     for (int i = 1; i <= T; ++i) {
       __syncthreads();
+      if (ht == 0 && pa.idx == nullptr) list_cache_publish(lc, e0 + i);  // built before barrier i
       if (i < T)
         rank_epoch_indices_or(pa.idx, list(e0 + i + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + i + 1,
-                           pa.shuffle, ht, hn);
+                           pa.shuffle, ht, hn, lc);
       // at barrier i the trainer has trained every position before (e0+i)*S - kNB
       if (ring) reduce_losses(min((int64_t)(e0 + i) * S - kNB, pos0 + n));
     }

@@ -56,22 +56,54 @@ __device__ __forceinline__ void rank_epoch_indices(int32_t* out, uint32_t N, int
                                                    uint64_t seed, int epoch, int shuffle, int tid, int nt) {
   FeistelPerm p;
   p.init(seed, epoch, N);
+  // One 64-bit remainder per thread, then the wrap is a subtraction: a
+  // remainder per entry (a software division loop) made this list ~14 us of
+  // every persistent launch's prologue.
+  uint32_t pos = (uint32_t)(((uint64_t)rank + (uint64_t)W * (uint64_t)tid) % N);  // once per thread
+  const uint32_t step = (uint32_t)(((uint64_t)W * (uint64_t)nt) % N);
   for (int i = tid; i < num_samples; i += nt) {
-    const uint32_t pos = (uint32_t)(((uint64_t)rank + (uint64_t)W * (uint64_t)i) % N);
     out[i] = (int32_t)(shuffle ? p(pos) : pos);
+    pos += step;  // both < N: one conditional subtraction
+    pos = pos >= N ? pos - N : pos;
   }
 }
 
+// Launch-to-launch cache of the epoch lists (global memory, owned by the
+// caller's launch plan, fixed sampler parameters): slot e&1 holds epoch tag[e&1].
+// A persistent launch copies a cached list instead of recomputing it, so the
+// permutation is computed once per epoch however the steps are split into
+// launches. The builder writes the tag only after every entry is written
+// (the caller publishes it after its next barrier; readers are later launches).
+struct ListCache {
+  int32_t* lists;  // [2][stride], or nullptr: no cache
+  int32_t* tag;    // [2] epoch held by each slot (-1: empty)
+  int stride;
+};
+
 // The epoch's list from a caller-provided index array (e.g. the host's torch-
-// identical DistributedSampler order) when `given` is set, else the Feistel one.
+// identical DistributedSampler order) when `given` is set, else from the cache
+// when it holds `epoch`, else the Feistel one (also written to the cache).
 __device__ __forceinline__ void rank_epoch_indices_or(const int32_t* given, int32_t* out, uint32_t N, int W, int rank,
                                                       int num_samples, uint64_t seed, int epoch, int shuffle, int tid,
-                                                      int nt) {
+                                                      int nt, const ListCache& lc = ListCache{nullptr, nullptr, 0}) {
   if (given != nullptr) {
     for (int i = tid; i < num_samples; i += nt) out[i] = given[i];
-  } else {
-    rank_epoch_indices(out, N, W, rank, num_samples, seed, epoch, shuffle, tid, nt);
+    return;
   }
+  if (lc.lists != nullptr && __builtin_amdgcn_readfirstlane(lc.tag[epoch & 1]) == epoch) {
+    const int32_t* src = lc.lists + (epoch & 1) * lc.stride;
+    for (int i = tid; i < num_samples; i += nt) out[i] = src[i];
+    return;
+  }
+  rank_epoch_indices(out, N, W, rank, num_samples, seed, epoch, shuffle, tid, nt);
+  if (lc.lists != nullptr) {
+    int32_t* dst = lc.lists + (epoch & 1) * lc.stride;
+    for (int i = tid; i < num_samples; i += nt) dst[i] = out[i];
+  }
+}
+// Publish `epoch` as cached (one thread, after every builder thread's writes).
+__device__ __forceinline__ void list_cache_publish(const ListCache& lc, int epoch) {
+  if (lc.lists != nullptr) lc.tag[epoch & 1] = epoch;
 }
 
 }  // namespace ptdt

@@ -178,6 +178,34 @@ class FusedMLPStep:
             done += n
         self._pending = False
 
+    def persistent_plan(self, X, Y, batch_size: int, sampler, cursor: torch.Tensor, losses: torch.Tensor,
+                        variant: str | None = None, idx: torch.Tensor | None = None,
+                        stamps: torch.Tensor | None = None):
+        """A :meth:`run_persistent` launch resolved once (native ``PersistentPlan``):
+        arguments validated, engine/kernel chosen, tensors held. ``plan.launch(n)``
+        runs ``n <= losses.numel()`` steps from the device cursor with nothing but a
+        ``hipLaunchKernel`` on the host; with ``idx`` (one epoch's index list)
+        ``plan.launch(n, cursor_j)`` must stay inside that epoch."""
+        if self.xgmi is None and self.comm is not None and self.comm.world > 1:
+            raise RuntimeError("the persistent engine needs the xGMI all-reduce for world > 1")
+        ce_index = self.loss_kind == LOSS_KINDS["ce_index"]
+        vid = _variant_id(variant)
+        X, padded = self._wave_input(X, batch_size, sampler, vid)
+        self._pending = False
+        # launch-to-launch cache of the epoch index lists (tags -1: empty): a launch
+        # starting inside an already computed epoch copies its list
+        stride = (sampler.num_samples + 3) // 4 * 4
+        lcache = None
+        if idx is None:
+            lcache = torch.zeros(2 * stride + 2, dtype=torch.int32, device=self.device)
+            lcache[-2:] = -1
+        return self._C.PersistentPlan(
+            X, None if ce_index else Y, Y if ce_index else None, self.P, self.G, self.mom, self.opt_step,
+            batch_size, self.Din, self.H, self.Dout, self.loss_kind, self.ignore_index, self.has_bias,
+            self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
+            self.xgmi.handle if self.xgmi is not None else None, sampler.num_replicas, sampler.rank,
+            sampler.num_samples, sampler.shuffle, sampler.seed, cursor, losses, stamps, vid, padded, idx, lcache)
+
     def _wave_input(self, X, batch_size, sampler, vid):
         """The wave engine reads whole lane chunks (L lanes x K features per row):
         when L*K > Din, hand it a zero-padded copy of X (cached per tensor version)."""

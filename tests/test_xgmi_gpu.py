@@ -107,6 +107,48 @@ def test_persistent_engine_world1_equals_per_step(dev):
         torch.testing.assert_close(res[0], res[1], rtol=1e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("kind", ["linear_mse", "mlp_workgroup", "mlp_mfma"])
+def test_persistent_plan_with_list_cache_equals_per_step(dev, kind):
+    """PersistentPlan (launch resolved once, epoch lists cached across launches):
+    irregular launch splits crossing epoch boundaries (starts mid-epoch on a
+    cached list, epochs built by the helper waves) follow the per-step trajectory."""
+    from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP, ddp_toy_model
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+
+    from ._workers import _per_step_reference
+
+    if kind == "linear_mse":
+        X, Y = torch.rand(640, 20, device=dev), torch.rand(640, 1, device=dev)
+        mk, loss, mom, variant = (lambda: ddp_toy_model()), "mse", 0.9, None
+    else:
+        X, Y = torch.randn(500, 20, device=dev), torch.randint(0, 10, (500,), device=dev)
+        mk, loss, mom = (lambda: ToyMLP(20, 64, 10)), "ce_index", 0.9
+        variant = "workgroup" if kind == "mlp_workgroup" else "mfma"
+    splits = [1, 5, 37, 3, 20, 43, 41]  # 150 steps, epochs of 20 (linear) / 16 (mlp) steps
+    res = []
+    for mode in ("plan", "per_step"):
+        torch.manual_seed(7)
+        eng = FusedMLPStep(mk().to(dev), loss=loss, lr=0.05, momentum=mom)
+        sampler = DeviceDistributedSampler(X.shape[0], 1, 0, seed=1, device=dev)
+        if mode == "plan":
+            cursor = torch.zeros(2, dtype=torch.int32, device=dev)
+            losses = torch.zeros(max(splits), device=dev)
+            plan = eng.persistent_plan(X, Y, 32, sampler, cursor, losses, variant=variant)
+            for n in splits:
+                plan.launch(n)
+            torch.cuda.synchronize()
+            S = -(-X.shape[0] // 32)
+            assert cursor.tolist() == [150 // S, 150 % S]
+        else:
+            _per_step_reference(eng, X, Y, sampler, 150, 32, dev)
+        torch.cuda.synchronize()
+        res.append(eng.P.clone())
+    assert torch.isfinite(res[0]).all()
+    tol = 1e-6 if kind != "mlp_mfma" else 1e-4
+    torch.testing.assert_close(res[0], res[1], rtol=tol, atol=tol)
+
+
 @pytest.mark.parametrize("kind", ["mlp", "linear", "linear_rows"])
 def test_persistent_engine_two_ranks_one_gpu(tmp_path, kind):
     world = 2
