@@ -80,39 +80,6 @@ def _setup(args):
     return env.rank(), env.world_size(), env.local_rank()
 
 
-class _StagedComm:
-    """Control plane for --share_gpu rehearsals: gloo collectives on host copies
-    (RCCL cannot put two ranks on one GPU). Same surface as parallel.comm.Communicator
-    for what the bench uses."""
-
-    def __init__(self, dev):
-        import torch.distributed as dist
-
-        self.dist, self.dev = dist, dev
-        self.rank, self.world = dist.get_rank(), dist.get_world_size()
-
-    def barrier(self):
-        torch.cuda.synchronize(self.dev)
-        self.dist.barrier()
-
-    def broadcast(self, t, src=0):
-        h = t.detach().cpu()
-        self.dist.broadcast(h, src)
-        t.copy_(h)
-        return t
-
-    def all_reduce(self, t, op="sum"):
-        h = t.detach().cpu()
-        self.dist.all_reduce(h, {"sum": self.dist.ReduceOp.SUM, "max": self.dist.ReduceOp.MAX}[op])
-        t.copy_(h)
-        return t
-
-    def all_gather_object(self, obj):
-        out = [None] * self.world
-        self.dist.all_gather_object(out, obj)
-        return out
-
-
 def _replicas_in_sync(comm, params: torch.Tensor) -> bool:
     """DDP invariant after training: every rank holds bit-identical parameters."""
     if comm.world == 1:
@@ -413,7 +380,7 @@ def main(argv=None):
         if args.engine not in ("persistent", "fused") or args.allreduce == "rccl":
             raise SystemExit("--share_gpu rehearses the xGMI engines only (RCCL needs one GPU per rank)")
         torch.cuda.set_device(dev)
-        comm = _StagedComm(dev)
+        comm = comm_mod.HostStagedComm(dev)
     else:
         comm = comm_mod.get_default(dev)
     runner = {"persistent": run_persistent, "fused": run_fused, "autograd": run_autograd,

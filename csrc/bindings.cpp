@@ -142,7 +142,7 @@ PersistBuild build_persistent(const Tensor& X, const c10::optional<Tensor>& Yf, 
                               int64_t num_samples, bool shuffle, int64_t seed, const Tensor& cursor,
                               const Tensor& losses, const c10::optional<Tensor>& stamps, int64_t variant,
                               bool x_zero_padded, const c10::optional<Tensor>& idx, int64_t cursor_j,
-                              const c10::optional<Tensor>& lcache = c10::nullopt) {
+                              const c10::optional<Tensor>& lcache = c10::nullopt, int64_t idx_e0 = 0) {
   TORCH_CHECK(X.is_cuda(), "X must be a GPU tensor");  // rows may be padded: checked below
   check_gpu(P, "P");
   check_gpu(G, "G");
@@ -206,14 +206,20 @@ PersistBuild build_persistent(const Tensor& X, const c10::optional<Tensor>& Yf, 
     pa.stamps = stamps->data_ptr<int64_t>();
   }
   pa.variant = (int)variant;
-  pa.cursor_host_j = -1;
+  pa.cursor_host_pos = -1;
   if (idx.has_value() && idx->defined()) {
-    TORCH_CHECK(idx->is_cuda() && idx->scalar_type() == at::kInt && idx->is_contiguous() && idx->numel() >= num_samples,
-                "persistent: idx must be a contiguous int32 GPU tensor of num_samples indices");
-    TORCH_CHECK(cursor_j >= 0 && cursor_j + n_steps <= (num_samples + B - 1) / B,
-                "persistent: with an explicit index list a launch must stay inside the epoch (pass cursor_j)");
+    // [num_samples] (one epoch: cursor_j is the step in it) or [E, num_samples]
+    // (epochs idx_e0..idx_e0+E-1: cursor_j is the absolute position epoch * S + step)
+    TORCH_CHECK(idx->is_cuda() && idx->scalar_type() == at::kInt && idx->is_contiguous() &&
+                    idx->size(-1) == num_samples && idx->dim() <= 2 && idx->device() == X.device(),
+                "persistent: idx must be a contiguous int32 GPU tensor [E,] num_samples on X's device");
+    const int64_t S = (num_samples + B - 1) / B;
     pa.idx = idx->data_ptr<int32_t>();
-    pa.cursor_host_j = (int)cursor_j;
+    pa.idx_epochs = idx->dim() == 2 ? (int)idx->size(0) : 1;
+    pa.idx_e0 = idx->dim() == 2 ? (int)idx_e0 : 0;
+    TORCH_CHECK(cursor_j >= (int64_t)pa.idx_e0 * S && cursor_j + n_steps <= (int64_t)(pa.idx_e0 + pa.idx_epochs) * S,
+                "persistent: with explicit index lists a launch must stay inside the provided epochs");
+    pa.cursor_host_pos = cursor_j;
   }
   if (lcache.has_value() && lcache->defined()) {  // [2][al4(num_samples)] lists + [2] epoch tags
     const int64_t stride = (num_samples + 3) & ~int64_t(3);
@@ -261,28 +267,31 @@ class PersistentPlan {
                  double dampening, double weight_decay, bool nesterov, std::shared_ptr<XgmiComm> ar, int64_t W,
                  int64_t rank, int64_t num_samples, bool shuffle, int64_t seed, Tensor cursor, Tensor losses,
                  c10::optional<Tensor> stamps, int64_t variant, bool x_zero_padded, c10::optional<Tensor> idx,
-                 c10::optional<Tensor> lcache)
+                 c10::optional<Tensor> lcache, int64_t idx_e0)
       : keep_{X, P, G, cursor, losses}, ar_(ar), capacity_(losses.numel()), dev_(X.device().index()) {
     for (const auto* t : {&Yf, &Yi, &mom, &opt_step, &stamps, &idx, &lcache})
       if (t->has_value() && (*t)->defined()) keep_.push_back(**t);
     const bool has_idx = idx.has_value() && idx->defined();
     steps_per_epoch_ = (num_samples + B - 1) / B;
+    const int64_t first = has_idx && idx->dim() == 2 ? idx_e0 * steps_per_epoch_ : 0;
     const PersistBuild b = build_persistent(X, Yf, Yi, P, G, mom, opt_step, B, Din, H, Dout, loss_kind, ignore_index,
                                             has_bias, lr, momentum, dampening, weight_decay, nesterov, ar, 1, W, rank,
                                             num_samples, shuffle, seed, cursor, losses, stamps, variant,
-                                            x_zero_padded, idx, has_idx ? 0 : -1, lcache);
+                                            x_zero_padded, idx, has_idx ? first : -1, lcache, idx_e0);
     c10::hip::HIPGuard guard(dev_);
     hip_check(fused_mlp_persistent_prepare(b.a, b.pa, &L_), "persistent plan");
   }
-  // n steps from the device cursor; with an explicit index list, cursor_j is
-  // the host's view of the step-in-epoch (the launch must stay in the epoch)
-  void launch(int64_t n, int64_t cursor_j) {
+  // n steps from the device cursor; with explicit index lists, cursor_pos is
+  // the host's view of the cursor (epoch * steps_per_epoch + step; one-epoch
+  // list: the step in it) and the launch must stay inside the provided epochs
+  void launch(int64_t n, int64_t cursor_pos) {
     TORCH_CHECK(n >= 0 && n <= capacity_, "persistent plan: n_steps exceeds the losses buffer");
-    TORCH_CHECK(L_.p.idx == nullptr || (cursor_j >= 0 && cursor_j + n <= steps_per_epoch_),
-                "persistent plan: with an explicit index list a launch must stay inside the epoch");
+    const int64_t S = steps_per_epoch_;
+    TORCH_CHECK(L_.p.idx == nullptr || (cursor_pos >= (int64_t)L_.p.idx_e0 * S &&
+                                        cursor_pos + n <= (int64_t)(L_.p.idx_e0 + L_.p.idx_epochs) * S),
+                "persistent plan: with explicit index lists a launch must stay inside the provided epochs");
     c10::hip::HIPGuard guard(dev_);
-    hip_check(persistent_launch(L_, (int)n, L_.p.idx ? (int)cursor_j : -1,
-                                c10::hip::getCurrentHIPStream(dev_).stream()),
+    hip_check(persistent_launch(L_, (int)n, L_.p.idx ? cursor_pos : -1, c10::hip::getCurrentHIPStream(dev_).stream()),
               "persistent launch");
   }
   int64_t capacity() const { return capacity_; }
@@ -315,6 +324,30 @@ std::string persistent_engine(int64_t B, int64_t Din, int64_t H, int64_t Dout, i
   }
   if (variant != kPersistWorkgroup && mlp_mfma_persistent_supported(a, pa)) return "workgroup:mfma";
   return "workgroup";
+}
+
+// ------------------------------------------------------------- torch-identical sampler orders
+void torch_perm_py(Tensor seeds, int64_t n, int64_t W, int64_t rank, int64_t num_samples, Tensor out,
+                   c10::optional<Tensor> ws) {
+  check_gpu(seeds, "seeds");
+  check_gpu(out, "out");
+  TORCH_CHECK(seeds.scalar_type() == at::kLong && seeds.dim() == 1, "torch_perm: seeds int64[E]");
+  TORCH_CHECK(out.scalar_type() == at::kInt && out.dim() == 2 && out.size(0) == seeds.size(0) &&
+                  out.size(1) >= num_samples && out.device() == seeds.device(),
+              "torch_perm: out int32[E, >= num_samples] on the seeds' device");
+  TORCH_CHECK(n >= 2 && n < (1ll << 31) && W > 0 && rank >= 0 && rank < W && num_samples > 0,
+              "torch_perm: bad sampler geometry");
+  int32_t* wsp = nullptr;
+  if (torch_perm_lds_bytes((int)n) + 624 * 4 > 160 * 1024) {
+    TORCH_CHECK(ws.has_value() && ws->defined() && ws->is_cuda() && ws->scalar_type() == at::kInt &&
+                    ws->is_contiguous() && ws->numel() >= seeds.size(0) * 4 * n,
+                "torch_perm: n too large for LDS, pass ws = int32[E * 4n]");
+    wsp = ws->data_ptr<int32_t>();
+  }
+  c10::hip::HIPGuard guard(out.device().index());
+  hip_check(torch_perm(seeds.data_ptr<int64_t>(), (int)seeds.size(0), (int)n, (int)W, (int)rank, (int)num_samples,
+                       out.data_ptr<int32_t>(), (int)out.size(1), wsp, cur_stream(out)),
+            "torch_perm");
 }
 
 // ------------------------------------------------------------- optimizers
@@ -963,15 +996,16 @@ PYBIND11_MODULE(_C, m) {
       .def(py::init<Tensor, c10::optional<Tensor>, c10::optional<Tensor>, Tensor, Tensor, c10::optional<Tensor>,
                     c10::optional<Tensor>, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, bool, double, double,
                     double, double, bool, std::shared_ptr<XgmiComm>, int64_t, int64_t, int64_t, bool, int64_t, Tensor,
-                    Tensor, c10::optional<Tensor>, int64_t, bool, c10::optional<Tensor>, c10::optional<Tensor>>(),
+                    Tensor, c10::optional<Tensor>, int64_t, bool, c10::optional<Tensor>, c10::optional<Tensor>,
+                    int64_t>(),
            py::arg("X"), py::arg("Yf"), py::arg("Yi"), py::arg("P"), py::arg("G"), py::arg("mom"),
            py::arg("opt_step"), py::arg("B"), py::arg("Din"), py::arg("H"), py::arg("Dout"), py::arg("loss_kind"),
            py::arg("ignore_index"), py::arg("has_bias"), py::arg("lr"), py::arg("momentum"), py::arg("dampening"),
            py::arg("weight_decay"), py::arg("nesterov"), py::arg("ar"), py::arg("W"), py::arg("rank"),
            py::arg("num_samples"), py::arg("shuffle"), py::arg("seed"), py::arg("cursor"), py::arg("losses"),
            py::arg("stamps") = py::none(), py::arg("variant") = 0, py::arg("x_zero_padded") = false,
-           py::arg("idx") = py::none(), py::arg("lcache") = py::none())
-      .def("launch", &PersistentPlan::launch, py::arg("n_steps"), py::arg("cursor_j") = -1)
+           py::arg("idx") = py::none(), py::arg("lcache") = py::none(), py::arg("idx_e0") = 0)
+      .def("launch", &PersistentPlan::launch, py::arg("n_steps"), py::arg("cursor_pos") = -1)
       .def_property_readonly("capacity", &PersistentPlan::capacity);
   m.def("persistent_engine", &persistent_engine, py::arg("B"), py::arg("Din"), py::arg("H"), py::arg("Dout"),
         py::arg("loss_kind"), py::arg("num_samples"), py::arg("world"), py::arg("variant") = 0);
@@ -1031,6 +1065,9 @@ PYBIND11_MODULE(_C, m) {
     hip_check(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()), "hipExtStreamCreateWithCUMask");
     return (uintptr_t)st;
   }, py::arg("device"), py::arg("cus"));
+  m.def("torch_perm_", &torch_perm_py, py::arg("seeds"), py::arg("n"), py::arg("W"), py::arg("rank"),
+        py::arg("num_samples"), py::arg("out"), py::arg("ws") = py::none());
+  m.def("torch_perm_needs_ws", [](int64_t n) { return torch_perm_lds_bytes((int)n) + 624 * 4 > 160 * 1024; });
   m.def("plan_buckets", &plan_buckets);
 
   py::class_<RcclComm, std::shared_ptr<RcclComm>>(m, "RcclComm")

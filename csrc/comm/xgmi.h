@@ -36,6 +36,9 @@ struct XgmiArgs {
   uint32_t* seq;                         // this rank's collective counter (device)
   int* err;                              // nonzero after a timed-out poll
   int rank, world, max_elems;            // world == 0: disabled
+  uint32_t max_polls;                    // poll budget per slot (kXgmiMaxPolls; PTDT_XGMI_MAX_POLLS)
+  uint32_t drop_push;                    // fault injection: from collective seq drop_push on (0: never) skip
+                                         // pushes to other ranks (PTDT_FAULT_XGMI_DROP_RANK / _SEQ)
 };
 
 #ifdef __HIPCC__
@@ -53,7 +56,8 @@ __device__ __forceinline__ void xgmi_push(const XgmiArgs& x, uint32_t s, const f
   for (int i = tid; i < n; i += nt) {
     const uint64_t w = hi | (uint64_t)__float_as_uint(vals[i]);
     for (int p = 0; p < x.world; ++p)
-      __hip_atomic_store(xgmi_slot(x.peers[p], parity, x.rank, x.world, x.max_elems, i), w, __ATOMIC_RELAXED,
+      if (x.drop_push == 0u || s < x.drop_push || p == x.rank)
+        __hip_atomic_store(xgmi_slot(x.peers[p], parity, x.rank, x.world, x.max_elems, i), w, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -66,9 +70,9 @@ __device__ __forceinline__ float xgmi_gather_sum(const XgmiArgs& x, uint32_t s, 
   for (int p = 0; p < x.world; ++p) {
     uint64_t* slot = xgmi_slot(x.local, parity, p, x.world, x.max_elems, i);
     uint64_t w = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    uint32_t polls = dead ? kXgmiMaxPolls : 0;
+    uint32_t polls = dead ? x.max_polls : 0;
     while ((uint32_t)(w >> 32) != s) {
-      if (++polls > kXgmiMaxPolls) {  // ~seconds: a peer is gone; fail loudly, never hang
+      if (++polls > x.max_polls) {  // ~seconds: a peer is gone; fail loudly, never hang
         __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         dead = true;
         break;
@@ -112,13 +116,13 @@ __device__ __forceinline__ void xgmi_gather_lds(const XgmiArgs& x, uint32_t s, i
     }
     // re-poll every slot still missing, all of them in flight together: a slot that
     // arrives late costs one more round trip for the batch, not one per slot
-    uint32_t polls = dead ? kXgmiMaxPolls : 0;
+    uint32_t polls = dead ? x.max_polls : 0;
     for (;;) {
       bool missing = false;
 #pragma unroll
       for (int u = 0; u < U; ++u) missing |= off[u] >= 0 && (uint32_t)(w[u] >> 32) != s;
       if (!missing) break;
-      if (++polls > kXgmiMaxPolls) {
+      if (++polls > x.max_polls) {
         __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (lds_flag) *lds_flag = 1;
         dead = true;

@@ -1,6 +1,9 @@
 // Host side of the xGMI one-shot all-reduce (see xgmi_comm.h / xgmi.h).
 #include "xgmi_comm.h"
 
+#include <algorithm>
+#include <cstdlib>
+
 #include <cstring>
 #include <stdexcept>
 
@@ -30,6 +33,19 @@ XgmiComm::XgmiComm(int rank, int world, int max_elems, int device) : device_(dev
   args_.rank = rank;
   args_.world = world;
   args_.max_elems = max_elems;
+  args_.max_polls = kXgmiMaxPolls;
+  if (const char* v = std::getenv("PTDT_XGMI_MAX_POLLS")) {  // shorter bound for fault-injection tests
+    const long n = std::strtol(v, nullptr, 10);
+    if (n > 0) args_.max_polls = (uint32_t)std::min<long>(n, (long)kXgmiMaxPolls);
+  }
+  args_.drop_push = 0u;
+  if (const char* v = std::getenv("PTDT_FAULT_XGMI_DROP_RANK")) {
+    if (std::strtol(v, nullptr, 10) == rank) {
+      const char* sq = std::getenv("PTDT_FAULT_XGMI_DROP_SEQ");
+      const long s0 = sq ? std::strtol(sq, nullptr, 10) : 64;  // after the self-test's collectives
+      args_.drop_push = (uint32_t)(s0 > 0 ? s0 : 1);
+    }
+  }
   if (world == 1) ready_ = true;
 }
 

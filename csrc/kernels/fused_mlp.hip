@@ -799,9 +799,9 @@ __global__ void __launch_bounds__(MF ? kMfThreads : 1024) fused_mlp_persistent_k
   int opt_step = a.opt_step ? *a.opt_step : 0;
   uint32_t seq = a.ar.world > 1 ? *a.ar.seq : 0u;
   const ListCache lc{pa.lcache, pa.ltag, estride};
-  rank_epoch_indices_or(pa.idx, ebuf(epoch), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch, pa.shuffle,
+  rank_epoch_indices_or(given_list(pa, epoch), ebuf(epoch), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch, pa.shuffle,
                      tid, NT, lc);
-  rank_epoch_indices_or(pa.idx, ebuf(epoch + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
+  rank_epoch_indices_or(given_list(pa, epoch + 1), ebuf(epoch + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
                      pa.shuffle, tid, NT, lc);
   __syncthreads();
   if (tid == 0 && pa.idx == nullptr) {
@@ -836,7 +836,7 @@ __global__ void __launch_bounds__(MF ? kMfThreads : 1024) fused_mlp_persistent_k
       ++ne;
     }
     if (j == 0 && step > 0) {
-      rank_epoch_indices_or(pa.idx, ebuf(epoch + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
+      rank_epoch_indices_or(given_list(pa, epoch + 1), ebuf(epoch + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, epoch + 1,
                          pa.shuffle, tid, NT, lc);
       __syncthreads();
       if (tid == 0 && pa.idx == nullptr) list_cache_publish(lc, epoch + 1);
@@ -1034,13 +1034,16 @@ hipError_t fused_mlp_persistent_prepare(const FusedMlpArgs& a, const PersistArgs
   return hipSuccess;
 }
 
-hipError_t persistent_launch(PersistLaunch& L, int n_steps, int cursor_host_j, hipStream_t s) {
+hipError_t persistent_launch(PersistLaunch& L, int n_steps, int64_t cursor_host_pos, hipStream_t s) {
   if (n_steps <= 0) return hipSuccess;
   if (L.fn == nullptr) return hipErrorInvalidValue;
-  if (L.p.idx != nullptr && cursor_host_j >= 0 && cursor_host_j + n_steps > (L.p.num_samples + L.a.B - 1) / L.a.B)
-    return hipErrorInvalidValue;  // an explicit index list covers one epoch only
+  if (L.p.idx != nullptr) {  // explicit lists cover epochs [idx_e0, idx_e0 + idx_epochs) only
+    const int64_t S = (L.p.num_samples + L.a.B - 1) / L.a.B;
+    if (cursor_host_pos < (int64_t)L.p.idx_e0 * S || cursor_host_pos + n_steps > (int64_t)(L.p.idx_e0 + L.p.idx_epochs) * S)
+      return hipErrorInvalidValue;
+  }
   L.p.n_steps = n_steps;
-  L.p.cursor_host_j = cursor_host_j;
+  L.p.cursor_host_pos = cursor_host_pos;
   void* args[] = {&L.a, &L.p};
   return hipLaunchKernel(L.fn, dim3(1), dim3(L.threads), args, L.lds, s);
 }
@@ -1049,7 +1052,7 @@ hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hip
   if (p.n_steps <= 0) return check_dims(a);
   PersistLaunch L;
   PTDT_HIP_CHECK(fused_mlp_persistent_prepare(a, p, &L));
-  return persistent_launch(L, p.n_steps, p.cursor_host_j, s);
+  return persistent_launch(L, p.n_steps, p.cursor_host_pos, s);
 }
 
 bool mlp_mfma_persistent_supported(const FusedMlpArgs& a, const PersistArgs& p) { return mfma_engine(a, p); }

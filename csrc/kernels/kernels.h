@@ -74,9 +74,11 @@ struct PersistArgs {
                          // forward, loss, backward, all-reduce, sgd+land, epoch indices, total, realtime (100 MHz)
   int variant;           // kPersistAuto / kPersistWorkgroup / kPersistWave...
   int loss_ring;         // set by the launcher: the wave engine reduces losses in helper waves
-  const int32_t* idx;    // optional [num_samples] index list of the cursor's epoch (replaces the in-kernel
-                         // Feistel permutation; the launch must then stay inside that epoch)
-  int cursor_host_j;     // the caller's view of cursor[1] (checked against n_steps when idx is set), or -1
+  const int32_t* idx;    // optional [idx_epochs][num_samples] index lists of epochs idx_e0.. (e.g. torch's
+                         // DistributedSampler orders; replace the in-kernel Feistel permutation). A launch
+                         // must stay inside those epochs; list reads past them (stale prefetches) clamp.
+  int idx_e0, idx_epochs;
+  int64_t cursor_host_pos;  // the caller's view of the cursor (epoch * steps_per_epoch + step), or -1
   int32_t* lcache;       // optional [2][al4(num_samples)] launch-to-launch epoch-list cache (sampler.h ListCache)
   int32_t* ltag;         // its [2] epoch tags (-1: empty); both null: every launch recomputes its lists
 };
@@ -94,6 +96,13 @@ enum PersistVariant : int {
   kPersistAuto = 0, kPersistWorkgroup = 1, kPersistWave = 2, kPersistWaveRows = 3, kPersistWaveF = 4,
   kPersistMfma = 5
 };
+// The caller-provided list of `epoch` (clamped into the provided range), or nullptr.
+__device__ __forceinline__ const int32_t* given_list(const PersistArgs& p, int epoch) {
+  if (p.idx == nullptr) return nullptr;
+  int k = epoch - p.idx_e0;
+  k = k < 0 ? 0 : (k >= p.idx_epochs ? p.idx_epochs - 1 : k);
+  return p.idx + (int64_t)k * p.num_samples;
+}
 hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s);
 // A persistent launch resolved once (engine choice, kernel, LDS size, argument
 // checks): relaunching it only sets n_steps (and the explicit-list cursor) and
@@ -106,7 +115,7 @@ struct PersistLaunch {
   PersistArgs p{};
 };
 hipError_t fused_mlp_persistent_prepare(const FusedMlpArgs& a, const PersistArgs& p, PersistLaunch* out);
-hipError_t persistent_launch(PersistLaunch& L, int n_steps, int cursor_host_j, hipStream_t s);
+hipError_t persistent_launch(PersistLaunch& L, int n_steps, int64_t cursor_host_pos, hipStream_t s);
 bool linear_wave_supported(const FusedMlpArgs& a, const PersistArgs& p);
 bool mlp_mfma_persistent_supported(const FusedMlpArgs& a, const PersistArgs& p);
 // lane layout the wave engine picks: L lanes per row, R rows per lane group, kp features per lane
@@ -116,6 +125,14 @@ hipError_t linear_wave_prepare(const FusedMlpArgs& a, const PersistArgs& p, Pers
 size_t fused_mlp_persistent_lds_bytes(int B, int Din, int H, int Dout, int num_samples, int world);
 // LDS bytes the step needs (host check against the 160 KiB per-CU budget).
 size_t fused_mlp_lds_bytes(int B, int Din, int H, int Dout);
+
+// torch-identical DistributedSampler epoch orders on the GPU (torch_perm.hip):
+// out[e][i] = torch.randperm(n, generator=manual_seed(seeds[e]))[(rank + W*i) % n]
+// for i < num_samples, one workgroup per epoch. ws: int32[n_epochs][4n] global
+// scratch, needed only when 4n ints exceed the LDS budget (torch_perm_lds_bytes).
+hipError_t torch_perm(const int64_t* seeds, int n_epochs, int n, int W, int rank, int num_samples, int32_t* out,
+                      int out_stride, int32_t* ws, hipStream_t s);
+size_t torch_perm_lds_bytes(int n);
 
 // --------------------------------------------------------------------------
 // Optimizers on flat buffers and multi-tensor lists (csrc/kernels/optim.hip).

@@ -132,7 +132,7 @@ hipError_t linear_wave_prepare(const FusedMlpArgs& a, const PersistArgs& p, Pers
 hipError_t linear_wave_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s) {
   PersistLaunch L;
   PTDT_HIP_CHECK(linear_wave_prepare(a, p, &L));
-  return persistent_launch(L, p.n_steps, p.cursor_host_j, s);
+  return persistent_launch(L, p.n_steps, p.cursor_host_pos, s);
 }
 
 }  // namespace ptdt

@@ -124,14 +124,16 @@ __device__ __forceinline__ bool ll_exchange(bool active, uint64_t PTDT_GLOBAL* p
                                             uint64_t PTDT_GLOBAL* poll_base, int my_rank, int peer, int world,
                                             int max_elems, uint32_t seq, int k0, int Din, bool hb, bool bias_lane,
                                             bool padded, const float (&gW)[DOUT][KP], const float (&gb)[DOUT],
-                                            float (&v)[DOUT][KP], float (&vb)[DOUT], int* err) {
+                                            float (&v)[DOUT][KP], float (&vb)[DOUT], int* err, uint32_t max_polls,
+                                            bool drop) {
   const int parity = (int)(seq & 1u);
   const int nW = DOUT * Din;
   const uint64_t hi = (uint64_t)seq << 32;
   if (!active) return true;
   uint64_t PTDT_GLOBAL* const dst = push_base + (int64_t)(parity * world + my_rank) * max_elems;
   uint64_t PTDT_GLOBAL* const src = poll_base + (int64_t)(parity * world + peer) * max_elems;
-  if (!padded) {
+  if (drop) {  // fault injection: this rank's contribution never reaches its peers
+  } else if (!padded) {
 #pragma unroll
     for (int c = 0; c < DOUT; ++c)
 #pragma unroll
@@ -147,7 +149,7 @@ __device__ __forceinline__ bool ll_exchange(bool active, uint64_t PTDT_GLOBAL* p
           __hip_atomic_store(dst + c * Din + k0 + k, hi | __float_as_uint(gW[c][k]), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  if (hb && bias_lane)
+  if (hb && bias_lane && !drop)
 #pragma unroll
     for (int c = 0; c < DOUT; ++c)
       __hip_atomic_store(dst + nW + c, hi | __float_as_uint(gb[c]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -168,7 +170,7 @@ __device__ __forceinline__ bool ll_exchange(bool active, uint64_t PTDT_GLOBAL* p
       vb[c] = hb ? __uint_as_float((uint32_t)w) : 0.f;
     }
     if (all) return true;
-    if (polls >= kXgmiMaxPolls) {  // a peer is gone: fail loudly, never hang
+    if (polls >= max_polls) {  // a peer is gone: fail loudly, never hang
       __hip_atomic_store((int PTDT_GLOBAL*)err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;
     }
@@ -210,7 +212,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
   // only the first epoch's list is on the path to step 0 (stale reads past the
   // launch are clamped below); e0+1 is built by the helpers after the barrier
   const ListCache lc{pa.lcache, pa.ltag, estride};
-  rank_epoch_indices_or(pa.idx, list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
+  rank_epoch_indices_or(given_list(pa, e0), list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
                      (int)threadIdx.x, kThreads, lc);
   __syncthreads();
   if (wave != 0) {
@@ -219,13 +221,13 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
     const int ht = (int)threadIdx.x - 64;
     if (ht == 0 && pa.idx == nullptr) list_cache_publish(lc, e0);
     if (T > 0)
-      rank_epoch_indices_or(pa.idx, list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1,
+      rank_epoch_indices_or(given_list(pa, e0 + 1), list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1,
                             pa.shuffle, ht, kThreads - 64, lc);
     for (int i = 1; i <= T; ++i) {
       __syncthreads();
       if (ht == 0 && pa.idx == nullptr) list_cache_publish(lc, e0 + i);
       if (i < T)
-        rank_epoch_indices_or(pa.idx, list(e0 + i + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + i + 1,
+        rank_epoch_indices_or(given_list(pa, e0 + i + 1), list(e0 + i + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + i + 1,
                            pa.shuffle, ht, kThreads - 64, lc);
     }
     return;
@@ -490,7 +492,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
       }
       const bool ok = ll_exchange<KP, DOUT>(j < world && j != my_rank, push_dst, poll_src, my_rank, j, world,
                                             max_elems, seq, k0, Din, hb, p == 0, L * KP != Din, gW, gb, v, vb,
-                                            ar.err);
+                                            ar.err, ar.max_polls, ar.drop_push != 0u && seq >= ar.drop_push);
       failed = !ok;
       failed = __any(failed);
 #pragma unroll
@@ -691,7 +693,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   // With a list cache (pa.lcache) a launch that starts inside an already
   // computed epoch copies its list instead of recomputing the permutation.
   const ListCache lc{pa.lcache, pa.ltag, estride};
-  rank_epoch_indices_or(pa.idx, list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
+  rank_epoch_indices_or(given_list(pa, e0), list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
                      (int)threadIdx.x, kThreads, lc);
   for (int k = (int)threadIdx.x; k < pa.num_samples; k += kThreads) list(e0 + 1)[k] = 0;
   // Loss ring (pa.loss_ring): the trainer stores each lane's scaled loss share
@@ -714,13 +716,13 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     };
     if (ht == 0 && pa.idx == nullptr) list_cache_publish(lc, e0);  // every thread's entries written (barrier)
     if (T > 0)  // epoch e0+1, needed at the trainer's first barrier
-      rank_epoch_indices_or(pa.idx, list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1,
+      rank_epoch_indices_or(given_list(pa, e0 + 1), list(e0 + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + 1,
                             pa.shuffle, ht, hn, lc);
     for (int i = 1; i <= T; ++i) {
       __syncthreads();
       if (ht == 0 && pa.idx == nullptr) list_cache_publish(lc, e0 + i);  // built before barrier i
       if (i < T)
-        rank_epoch_indices_or(pa.idx, list(e0 + i + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + i + 1,
+        rank_epoch_indices_or(given_list(pa, e0 + i + 1), list(e0 + i + 1), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0 + i + 1,
                            pa.shuffle, ht, hn, lc);
       // at barrier i the trainer has trained every position before (e0+i)*S - kNB
       if (ring) reduce_losses(min((int64_t)(e0 + i) * S - kNB, pos0 + n));
@@ -996,7 +998,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
       }
       const bool ok = ll_exchange<KP, DOUT>(i < world && i != my_rank, push_dst, poll_src, my_rank, i, world,
                                             max_elems, seq, k0, Din, hb, q == 0, 4 * KP != Din, gW, gb, v, vb,
-                                            ar.err);
+                                            ar.err, ar.max_polls, ar.drop_push != 0u && seq >= ar.drop_push);
       failed = !ok;
       failed = __any(failed);
 #pragma unroll

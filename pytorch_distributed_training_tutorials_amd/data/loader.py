@@ -91,6 +91,38 @@ class DeviceDataLoader:
             return out
         return idx
 
+    def device_epoch_indices(self, epochs, out: torch.Tensor | None = None) -> torch.Tensor:
+        """The rank's index lists of several ``epochs`` as int32 ``[len(epochs),
+        num_samples]`` on the dataset's GPU, identical to what
+        ``DistributedSampler.set_epoch(e)`` / ``iter`` yields (torch.randperm with
+        ``seed + e``, padding, ``rank::W`` striding) -- computed by one kernel
+        launch, one workgroup per epoch (csrc/kernels/torch_perm.hip), instead of a
+        host randperm + H2D copy per epoch."""
+        epochs = list(epochs)
+        ns = self._num_samples()
+        n = len(self.dataset)
+        dev = self.device
+        smp = self.sampler
+        if smp is not None:
+            W, rank, seed, shuffle = smp.num_replicas, smp.rank, smp.seed, smp.shuffle
+        else:
+            W, rank, seed, shuffle = 1, 0, self.seed, self.shuffle
+        if out is None:
+            out = torch.empty(len(epochs), ns, dtype=torch.int32, device=dev)
+        if not epochs:
+            return out
+        if not shuffle or n < 2:
+            q = (rank + W * torch.arange(ns, device=dev, dtype=torch.int64)) % max(n, 1)
+            out.copy_(q.to(torch.int32).expand(len(epochs), ns))
+            return out
+        seeds = torch.tensor([seed + e for e in epochs], dtype=torch.int64).to(dev, non_blocking=True)
+        ws = None
+        C = native()
+        if C.torch_perm_needs_ws(n):
+            ws = torch.empty(len(epochs) * 4 * n, dtype=torch.int32, device=dev)
+        C.torch_perm_(seeds, n, W, rank, ns, out, ws)
+        return out
+
     def batches(self):
         """(start, size) of each step in the epoch's index list."""
         n = self._num_samples()

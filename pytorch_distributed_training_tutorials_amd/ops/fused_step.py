@@ -180,12 +180,15 @@ class FusedMLPStep:
 
     def persistent_plan(self, X, Y, batch_size: int, sampler, cursor: torch.Tensor, losses: torch.Tensor,
                         variant: str | None = None, idx: torch.Tensor | None = None,
-                        stamps: torch.Tensor | None = None):
+                        stamps: torch.Tensor | None = None, idx_e0: int = 0):
         """A :meth:`run_persistent` launch resolved once (native ``PersistentPlan``):
         arguments validated, engine/kernel chosen, tensors held. ``plan.launch(n)``
         runs ``n <= losses.numel()`` steps from the device cursor with nothing but a
-        ``hipLaunchKernel`` on the host; with ``idx`` (one epoch's index list)
-        ``plan.launch(n, cursor_j)`` must stay inside that epoch."""
+        ``hipLaunchKernel`` on the host. ``idx``: explicit index lists instead of
+        the in-kernel permutation -- ``[num_samples]`` (one epoch; ``launch(n, j)``
+        with ``j`` the step in it) or ``[E, num_samples]`` for epochs
+        ``idx_e0 .. idx_e0+E-1`` (``launch(n, pos)`` with ``pos = epoch * S + step``,
+        the launch staying inside those epochs)."""
         if self.xgmi is None and self.comm is not None and self.comm.world > 1:
             raise RuntimeError("the persistent engine needs the xGMI all-reduce for world > 1")
         ce_index = self.loss_kind == LOSS_KINDS["ce_index"]
@@ -204,7 +207,8 @@ class FusedMLPStep:
             batch_size, self.Din, self.H, self.Dout, self.loss_kind, self.ignore_index, self.has_bias,
             self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
             self.xgmi.handle if self.xgmi is not None else None, sampler.num_replicas, sampler.rank,
-            sampler.num_samples, sampler.shuffle, sampler.seed, cursor, losses, stamps, vid, padded, idx, lcache)
+            sampler.num_samples, sampler.shuffle, sampler.seed, cursor, losses, stamps, vid, padded, idx, lcache,
+            idx_e0)
 
     def _wave_input(self, X, batch_size, sampler, vid):
         """The wave engine reads whole lane chunks (L lanes x K features per row):
@@ -231,6 +235,47 @@ class FusedMLPStep:
         "wave:L<l>R<r>K<k>" (lanes per row, rows per lane group, features per lane)."""
         return self._C.persistent_engine(batch_size, self.Din, self.H, self.Dout, self.loss_kind,
                                          sampler.num_samples, sampler.num_replicas, _variant_id(variant))
+
+    # ------------------------------------------------------------ optimizer state
+    def export_optimizer_state(self, optimizer) -> None:
+        """Write the engine's SGD state into ``optimizer`` in torch.optim.SGD layout
+        (``state[p]['momentum_buffer']``, absent before the first step), so
+        ``optimizer.state_dict()`` snapshots interchange with the autograd engine."""
+        self.flush()
+        first = int(self.opt_step.item()) == 0
+        for g in optimizer.param_groups:
+            for p in g["params"]:
+                st = optimizer.state[p]
+                st.pop("momentum_buffer", None)
+                if self.mom is not None and not first:
+                    _, off, k = self.flat.offsets[id(p)]
+                    st["momentum_buffer"] = self.mom[off:off + k].view_as(p).clone()
+
+    def import_optimizer_state(self, optimizer) -> None:
+        """Load ``optimizer``'s torch.optim.SGD state (e.g. after
+        ``optimizer.load_state_dict``) into the engine: momentum buffers into the
+        flat momentum, the first-step flag from their presence."""
+        self.flush()
+        have = False
+        for g in optimizer.param_groups:
+            for p in g["params"]:
+                buf = optimizer.state.get(p, {}).get("momentum_buffer")
+                if buf is not None and self.mom is not None:
+                    _, off, k = self.flat.offsets[id(p)]
+                    self.mom[off:off + k].copy_(buf.reshape(-1))
+                    have = True
+        self.opt_step.fill_(1 if have else 0)
+
+    def state_tensors(self) -> dict:
+        """Device copies of everything a step reads and writes (params, momentum,
+        step flag): a restore point for failure recovery."""
+        return {k: v.clone() for k, v in (("P", self.P), ("mom", self.mom), ("opt_step", self.opt_step))
+                if v is not None}
+
+    def restore(self, st: dict) -> None:
+        for k, v in st.items():
+            getattr(self, k).copy_(v)
+        self._pending = False
 
     # ------------------------------------------------------------ hipGraphs
     def state(self):

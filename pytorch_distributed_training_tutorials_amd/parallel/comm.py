@@ -264,3 +264,39 @@ def destroy_all():
             c.destroy()
         _all.clear()
         _default = None
+
+
+class HostStagedComm:
+    """Control plane for ranks that share one GPU (single-GPU rehearsals of the
+    multi-rank paths and their tests): gloo collectives on host copies, since
+    RCCL refuses two ranks on one device. Same surface as :class:`Communicator`
+    for what the engines use; nothing here is graph-capturable."""
+
+    def __init__(self, device):
+        self.device = torch.device(device)
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+
+    def barrier(self):
+        torch.cuda.synchronize(self.device)
+        dist.barrier()
+
+    def broadcast(self, t, src=0):
+        h = t.detach().cpu()
+        dist.broadcast(h, src)
+        t.copy_(h)
+        return t
+
+    def all_reduce(self, t, op="sum", stream=None):
+        h = t.detach().cpu()
+        if op == "avg":
+            dist.all_reduce(h, dist.ReduceOp.SUM)
+            h /= self.world
+        else:
+            dist.all_reduce(h, _TORCH_OPS[op])
+        t.copy_(h)
+        return t
+
+    def all_gather_object(self, obj):
+        out = [None] * self.world
+        dist.all_gather_object(out, obj)
+        return out

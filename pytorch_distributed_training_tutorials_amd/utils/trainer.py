@@ -9,11 +9,17 @@ cross_entropy -> backward -> step per batch.
 
 Engines (same observable result, different execution):
   * ``persistent`` -- GPU, Linear[-ReLU-Linear] models + SGD, one rank or a
-                    working in-kernel xGMI all-reduce: ONE kernel launch per
-                    epoch runs every DDP step of it (ops/fused_step.py
-                    run_persistent; the single-wave engine for Linear models),
-                    fed the loader's torch-identical DistributedSampler order.
-                    The default whenever available.
+                    working in-kernel xGMI all-reduce: ONE kernel launch runs
+                    every DDP step of every epoch up to the next snapshot
+                    (ops/fused_step.py persistent_plan; the single-wave engine
+                    for Linear models), fed the torch-identical
+                    DistributedSampler orders of all those epochs, computed on
+                    the GPU by one launch (data/torch_perm.py). The status lines
+                    of the launched epochs are printed before it. After it the
+                    xGMI error flag is read at the closing sync and agreed across
+                    ranks; on a timed-out poll every rank restores the launch's
+                    starting parameters and re-runs those epochs on the fused
+                    engine with RCCL. The default whenever available.
   * ``fused``    -- GPU, Linear[-ReLU-Linear] models + SGD: one fused kernel +
                     one RCCL all-reduce per step, a whole epoch captured into a
                     hipGraph and replayed (ops/fused_step.py). The default on GPU
@@ -22,7 +28,9 @@ Engines (same observable result, different execution):
                     overlapped with backward) + native kernels for Linear / loss /
                     optimizer where applicable; CPU/gloo for plumbing tests.
 Extras: rank-0 snapshots every ``save_every`` epochs with resume
-(``snapshot_path``), fault injection hooks, JSONL metrics.
+(``snapshot_path``; every engine saves its optimizer state in torch.optim.SGD
+layout, so snapshots interchange between engines), fault injection hooks,
+JSONL metrics.
 """
 from __future__ import annotations
 
@@ -96,11 +104,14 @@ class Trainer:
         self.comm = comm if comm is not None else comm_mod.get_default(self.device if self.device.type == "cuda" else None)
         model = model.to(self.device)
         self.engine_name = self._select_engine(engine, model)
+        self.xgmi = None
+        self.fallbacks = []  # (epoch range, reason) of every xGMI -> RCCL fallback
         xg = None
         if self.engine_name == "persistent" and self.world_size > 1:
             from ..parallel.xgmi import maybe_create
 
             xg = maybe_create(self.comm, self.device)  # collective: every rank takes this branch
+            self.xgmi = xg
             if xg is None:
                 if engine == "persistent":
                     raise RuntimeError("persistent engine: the in-kernel xGMI all-reduce is unavailable")
@@ -127,6 +138,9 @@ class Trainer:
     def _fusable(self, model) -> bool:
         if self.device.type != "cuda" or not isinstance(self.train_dataloader, DeviceDataLoader):
             return False
+        dl = self.train_dataloader
+        if dl.drop_last and dl._num_samples() % dl.batch_size:
+            return False  # the engines run ceil(num_samples / B) steps with a short last batch
         if self.loss_fn is not cross_entropy and getattr(self.loss_fn, "__name__", "") not in ("cross_entropy", "mse_loss"):
             return False
         if _sgd_hparams(self.optimizer) is None:
@@ -179,9 +193,7 @@ class Trainer:
         self.log(f"[GPU: {self.gpu_id} Epoch: {epoch}, Batch size: {b_sz} | Steps {len(self.train_dataloader)}]")
         self._set_epoch(epoch)
         t0 = time.perf_counter()
-        if self.engine_name == "persistent" and not self.faults.armed:
-            self._run_epoch_persistent(epoch)
-        elif self.engine_name in ("fused", "persistent"):
+        if self.engine_name in ("fused", "persistent"):
             self._run_epoch_fused()
         else:
             for xs, ys in self.train_dataloader:
@@ -208,7 +220,7 @@ class Trainer:
         batches = tuple(dl.batches())
         if self._loss_buf is None or self._loss_buf.numel() < len(batches):
             self._loss_buf = torch.zeros(len(batches), device=self.device)
-        if self.faults.armed:
+        if os.environ.get("PTDT_FAULT_RANK") is not None:  # per step on every rank (same collectives)
             for i, (s, b) in enumerate(batches):
                 self.faults.check(self.global_step + i)
                 self.engine.step(X, Y, self._idx_buf[s:s + b], b, self._loss_buf[i:i + 1])
@@ -224,42 +236,104 @@ class Trainer:
         self.global_step += len(batches)
 
     # ------------------------------------------------------------ persistent engine
-    def _run_epoch_persistent(self, epoch: int):
+    def _run_epochs_persistent(self, e0: int, e1: int):
+        """Epochs [e0, e1) in ONE persistent launch (status lines first)."""
         dl = self.train_dataloader
         X, Y = dl.dataset.tensors[0], dl.dataset.tensors[1]
         n = dl._num_samples()
-        if self._idx_buf is None:
-            self._idx_buf = torch.zeros(n, dtype=torch.int32, device=self.device)
-        dl.device_indices(out=self._idx_buf)  # torch-identical DistributedSampler order
-        steps = len(dl)
-        if self._loss_buf is None or self._loss_buf.numel() < steps:
-            self._loss_buf = torch.zeros(steps, device=self.device)
+        S = len(dl)
+        E = e1 - e0
+        b_sz = self._first_batch_size()
+        for epoch in range(e0, e1):
+            self.log(f"[GPU: {self.gpu_id} Epoch: {epoch}, Batch size: {b_sz} | Steps {S}]")
+        t0 = time.perf_counter()
+        dl.set_epoch(e1 - 1)  # the loader/sampler end where the reference's would
+        lists = dl.device_epoch_indices(range(e0, e1))  # torch-identical orders, one launch
+        if self._loss_buf is None or self._loss_buf.numel() < E * S:
+            self._loss_buf = torch.zeros(E * S, device=self.device)
         if self._cursor is None:
             self._cursor = torch.zeros(2, dtype=torch.int32, device=self.device)
-        self._cursor.copy_(torch.tensor([epoch, 0], dtype=torch.int32))
+        self._cursor.copy_(torch.tensor([e0, 0], dtype=torch.int32), non_blocking=True)
+        restore = self.engine.state_tensors() if self.xgmi is not None else None
         shard = _Shard(self.world_size, self.rank, n)
-        self.engine.run_persistent(X, Y, steps, dl.batch_size, shard, self._cursor, self._loss_buf,
-                                   idx=self._idx_buf, cursor_j=0)
-        self.global_step += steps
+        plan = self.engine.persistent_plan(X, Y, dl.batch_size, shard, self._cursor, self._loss_buf[:E * S],
+                                           idx=lists, idx_e0=e0)
+        plan.launch(E * S, e0 * S)
+        self.global_step += E * S
+        if self.xgmi is not None and self._xgmi_failed():
+            self._fallback_to_rccl(e0, e1, restore)
+        if self.metrics.enabled:
+            torch.cuda.synchronize(self.device)
+            self.metrics.write(event="epochs", first=e0, last=e1 - 1, seconds=time.perf_counter() - t0,
+                               steps=E * S, engine=self.engine_name)
+
+    def _xgmi_failed(self) -> bool:
+        """Did any rank's in-kernel all-reduce time out a poll? Read at the launch's
+        closing sync (one flag read per launch, none per step) and agreed by a
+        max-reduction, so every rank takes the same branch."""
+        bad = torch.tensor([float(self.xgmi.handle.error() != 0)], device=self.device)
+        self.comm.all_reduce(bad, "max")
+        return bad.item() != 0
+
+    def _fallback_to_rccl(self, e0: int, e1: int, restore: dict):
+        """A peer never arrived in the in-kernel all-reduce: replicas may hold
+        garbage. Every rank restores the launch's starting state, re-broadcasts
+        rank 0's parameters, drops the xGMI path and re-runs the epochs on the
+        fused engine with the RCCL all-reduce."""
+        msg = (f"[ptdt] rank {self.rank}: xGMI all-reduce timed out in epochs {e0}-{e1 - 1}; restoring their "
+               f"starting parameters and re-running them on the fused engine with RCCL")
+        print(msg, flush=True)
+        self.fallbacks.append(((e0, e1), "xgmi poll timeout"))
+        self.engine.restore(restore)
+        self.comm.broadcast(self.engine.P, 0)
+        if self.engine.mom is not None:
+            self.comm.broadcast(self.engine.mom, 0)
+        self.xgmi.handle.reset_error()
+        self.xgmi = None
+        self.engine.xgmi = None
+        self.engine.reduce = True
+        self.engine_name = "fused"
+        self._graphs = {}
+        self.global_step -= (e1 - e0) * len(self.train_dataloader)
+        for epoch in range(e0, e1):  # status lines were printed before the failed launch
+            self._set_epoch(epoch)
+            self._run_epoch_fused()
 
     def last_losses(self) -> torch.Tensor | None:
         return None if self._loss_buf is None else self._loss_buf
 
     # ------------------------------------------------------------ snapshots
     def _save_snapshot(self, epoch: int):
-        save_checkpoint(self.snapshot_path, self.model, self.optimizer if self.engine is None else None,
-                        epoch=epoch, rank=self.rank, barrier=self.comm.barrier)
+        if self.engine is not None:  # torch.optim.SGD layout: snapshots interchange between engines
+            self.engine.export_optimizer_state(self.optimizer)
+        save_checkpoint(self.snapshot_path, self.model, self.optimizer, epoch=epoch, rank=self.rank,
+                        barrier=self.comm.barrier)
 
     def _load_snapshot(self, path: str):
-        st = load_checkpoint(path, self.model, self.optimizer if self.engine is None else None,
-                             map_location=self.device)
+        st = load_checkpoint(path, self.model, self.optimizer, map_location=self.device)
+        if self.engine is not None:
+            self.engine.import_optimizer_state(self.optimizer)
         self.epochs_run = int(st.get("epoch", -1)) + 1
         self.log(f"Resuming training from snapshot at Epoch {self.epochs_run}")
 
+    def _save_due(self, epoch: int) -> bool:
+        return bool(self.snapshot_path and self.save_every and (epoch + 1) % self.save_every == 0)
+
     def train(self, max_epoch: int):
-        for epoch in range(self.epochs_run, max_epoch):
-            self._run_epoch(epoch)
-            if self.snapshot_path and self.save_every and (epoch + 1) % self.save_every == 0:
-                self._save_snapshot(epoch)
+        epoch = self.epochs_run
+        # fault injection runs per step on EVERY rank (one rank alone on another engine would desync)
+        per_step = os.environ.get("PTDT_FAULT_RANK") is not None
+        while epoch < max_epoch:
+            if self.engine_name == "persistent" and not per_step:
+                end = max_epoch
+                if self.snapshot_path and self.save_every:  # one launch per snapshot interval
+                    end = min(end, (epoch // self.save_every + 1) * self.save_every)
+                self._run_epochs_persistent(epoch, end)
+                epoch = end
+            else:
+                self._run_epoch(epoch)
+                epoch += 1
+            if self._save_due(epoch - 1):
+                self._save_snapshot(epoch - 1)
         if self.device.type == "cuda":
             torch.cuda.synchronize(self.device)

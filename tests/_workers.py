@@ -307,3 +307,47 @@ def bucket_all_reduce(rank, world, port, out_dir, numel):
            "avg0": float(t[0]), "bcast_ok": bool((b == world - 1).all())}
     torch.save(res, os.path.join(out_dir, f"r{rank}.pt"))
     destroy_process_group()
+
+
+def trainer_xgmi_fallback_one_gpu(rank, world, port, out_dir, inject):
+    """Trainer on the persistent xGMI engine, two ranks sharing cuda:0 (gloo control
+    plane). With ``inject`` rank 1 stops pushing its gradients to rank 0 from
+    collective 20 on (PTDT_FAULT_XGMI_DROP_RANK/SEQ) and the poll budget is short:
+    the in-kernel all-reduce times out, and every rank must detect it, restore
+    the launch's starting state and re-run the epochs on the fused engine."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    if inject:
+        os.environ["PTDT_FAULT_XGMI_DROP_RANK"] = "1"
+        os.environ["PTDT_FAULT_XGMI_DROP_SEQ"] = "20"
+        os.environ["PTDT_XGMI_MAX_POLLS"] = "20000"
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from pytorch_distributed_training_tutorials_amd.data import DeviceDataLoader, DeviceTensorDataset, DistributedSampler
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP
+    from pytorch_distributed_training_tutorials_amd.ops.optim import FusedSGD
+    from pytorch_distributed_training_tutorials_amd.parallel.comm import HostStagedComm
+    from pytorch_distributed_training_tutorials_amd.utils.trainer import Trainer
+
+    dev = torch.device("cuda", 0)
+    comm = HostStagedComm(dev)
+    torch.manual_seed(3)
+    ds = DeviceTensorDataset.synthetic_classification(256, 20, 4, device=dev, seed=11)
+    out = {}
+    for engine in ("persistent", "fused"):
+        torch.manual_seed(4 + rank)  # different init per rank: the Trainer broadcasts rank 0's
+        model = ToyMLP(20, 16, 4)
+        loader = DeviceDataLoader(ds, batch_size=16, sampler=DistributedSampler(ds, world, rank, seed=5))
+        t = Trainer(model, loader, FusedSGD(model.parameters(), lr=0.05, momentum=0.9), 0, engine=engine,
+                    comm=comm, graph=False, verbose=False)
+        out[engine + "_engine"] = t.engine_name
+        t.train(3)
+        torch.cuda.synchronize()
+        out[engine] = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu()
+        out[engine + "_fallbacks"] = len(t.fallbacks)
+        out[engine + "_final_engine"] = t.engine_name
+    torch.save(out, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
