@@ -36,9 +36,12 @@ import time
 
 import torch
 
-# BASELINE.md survey probe (unmodified reference loop, CPU/gloo, whole-node samples/s).
+# BASELINE.md survey probe (unmodified reference loop, CPU/gloo, whole-node samples/s) at N = 1, 2, 4.
+# N = 8 was not probed by the survey: benchmarks/reference_cpu_probe.py re-ran the same method here
+# (W=1 69.3K, W=8 55.4K samples/s on this slower container) and the W=8/W=1 ratio scales the
+# survey's W=1 figure: 99,000 * 55,383 / 69,272 = 79,150 (profiles/r2_reference_cpu_probe.md).
 # The reference publishes no GPU DDP number; see BASELINE.md.
-BASELINE_SAMPLES_PER_S = {1: 99_000.0, 2: 110_000.0, 4: 102_000.0}
+BASELINE_SAMPLES_PER_S = {1: 99_000.0, 2: 110_000.0, 4: 102_000.0, 8: 79_150.0}
 METRIC = "samples/sec (whole node) + DDP scaling eff., toy MLP at 1/2/4/8 MI355X"
 
 

@@ -1,0 +1,167 @@
+"""Worker bodies for the multi-GPU tests (one process per GPU, RCCL over xGMI).
+Importable without a GPU; every function runs in a spawned process."""
+import os
+
+import torch
+import torch.nn.functional as F
+
+
+def _init_gpu(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["LOCAL_RANK"] = str(rank)
+    from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
+    from pytorch_distributed_training_tutorials_amd.parallel import env
+
+    env.ddp_setup(rank, world, master_addr="127.0.0.1", master_port=port, backend="nccl")
+    dev = torch.device("cuda", rank)
+    torch.cuda.set_device(dev)
+    return dev, comm_mod.get_default(dev)
+
+
+def _digest_equal(comm, t: torch.Tensor) -> bool:
+    return len(set(comm.all_gather_object(t.detach().float().cpu().numpy().tobytes()))) == 1
+
+
+def ddp_gpu(rank, world, port, out_dir):
+    """Native DDP (C++ reducer, RCCL buckets on the comm stream) on cuda:rank with a
+    per-rank batch of 8 rows of a shared global batch (ddp_gpus.py:32-39)."""
+    dev, comm = _init_gpu(rank, world, port)
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP
+    from pytorch_distributed_training_tutorials_amd.ops.optim import FusedSGD
+    from pytorch_distributed_training_tutorials_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+
+    torch.manual_seed(100 + rank)  # different init per rank: DDP broadcasts rank 0's
+    model = ToyMLP(20, 16, 5).to(dev)
+    ddp = DistributedDataParallel(model, device_ids=[rank], comm=comm, bucket_cap_mb=0.0005, first_bucket_mb=0.0001)
+    opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(0)
+    X = torch.randn(4, 8 * world, 20, generator=g)
+    Y = torch.randint(0, 5, (4, 8 * world), generator=g)
+    for it in range(4):
+        xs = X[it, rank * 8:(rank + 1) * 8].to(dev)
+        ys = Y[it, rank * 8:(rank + 1) * 8].to(dev)
+        ddp.zero_grad()
+        F.cross_entropy(ddp(xs), ys).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    torch.save({"params": flat.cpu(), "in_sync": _digest_equal(comm, flat),
+                "buckets": len(ddp.bucket_sizes_bytes())}, os.path.join(out_dir, f"r{rank}.pt"))
+    destroy_process_group()
+
+
+def xgmi_gpu(rank, world, port, out_dir):
+    """In-kernel one-shot xGMI all-reduce across distinct GPUs vs RCCL ncclAvg, and the
+    persistent DDP engines (xGMI inside the kernel) vs the fused engine + RCCL."""
+    dev, comm = _init_gpu(rank, world, port)
+    from tests._workers import _per_step_reference
+
+    from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+    from pytorch_distributed_training_tutorials_amd.parallel.xgmi import XgmiAllReduce
+
+    out = {}
+    xg = XgmiAllReduce(comm, dev)
+    out["ok"] = xg.ok
+    errs = {}
+    for n in (21, 1994, 65536):
+        g = torch.Generator(device=dev).manual_seed(1000 * rank + n)
+        t = torch.randn(n, device=dev, generator=g)
+        a, b = t.clone(), t.clone()
+        if xg.ok:
+            xg.all_reduce_avg(a)
+        comm.all_reduce(b, "avg")
+        torch.cuda.synchronize()
+        errs[n] = float((a - b).abs().max()) if xg.ok else None
+        out[f"xgmi_in_sync_{n}"] = _digest_equal(comm, a)
+    out["max_err"] = errs
+    out["poll_error"] = xg.x.error() if xg.ok else None
+    X = torch.randn(2048, 20, generator=torch.Generator().manual_seed(9)).to(dev)
+    Y = torch.randint(0, 4, (2048,), generator=torch.Generator().manual_seed(10)).to(dev)
+    for kind in ("linear", "mlp"):
+        res = {}
+        for mode in ("persistent", "per_step_rccl"):
+            torch.manual_seed(5)
+            model = (ToyMLP(20, 16, 4) if kind == "mlp" else torch.nn.Linear(20, 2)).to(dev)
+            eng = FusedMLPStep(model, loss="ce_index", lr=0.05, momentum=0.9, comm=comm,
+                               xgmi=xg if (mode == "persistent" and xg.ok) else None)
+            sampler = DeviceDistributedSampler(2048, world, rank, seed=3, device=dev)
+            if mode == "persistent" and xg.ok:
+                out[f"{kind}_engine"] = eng.persistent_engine(16, sampler)
+                cursor = torch.zeros(2, dtype=torch.int32, device=dev)
+                losses = torch.zeros(64, device=dev)
+                plan = eng.persistent_plan(X, Y, 16, sampler, cursor, losses)
+                for n in (3, 40, 64, 13):  # 120 steps across epoch boundaries
+                    plan.launch(n)
+                torch.cuda.synchronize()
+                xg.check()
+            else:
+                _per_step_reference(eng, X, Y, sampler, 120, 16, dev)
+            torch.cuda.synchronize()
+            res[mode] = eng.P.clone()
+            out[f"{kind}_{mode}_in_sync"] = _digest_equal(comm, eng.P)
+        out[f"{kind}_err"] = float((res["persistent"] - res["per_step_rccl"]).abs().max()) if xg.ok else None
+    torch.save(out, os.path.join(out_dir, f"r{rank}.pt"))
+    destroy_process_group()
+
+
+def pipeline_gpu(rank, world, port, out_dir, micro):
+    """ToyModel split over two GPUs and two ranks with RCCL send/recv (NB03:440-450)."""
+    dev, comm = _init_gpu(rank, world, port)
+    import torch.nn as nn
+
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+    from pytorch_distributed_training_tutorials_amd.parallel.pipeline import PipelineStage
+
+    torch.manual_seed(0)
+    net1, net2 = nn.Linear(1000, 10), nn.Linear(10, 5)
+    stage_mod = (nn.Sequential(net1, nn.ReLU()) if rank == 0 else net2).to(dev)
+    st = PipelineStage(stage_mod, comm, loss_fn=nn.MSELoss(), micro_batches=micro)
+    opt = torch.optim.SGD(stage_mod.parameters(), lr=1e-3)
+    g = torch.Generator().manual_seed(1)
+    losses = []
+    for _ in range(3):
+        x = torch.randn(20, 1000, generator=g)
+        y = torch.randn(20, 5, generator=g)
+        opt.zero_grad()
+        l = st.train_step(x.to(dev) if rank == 0 else None, y.to(dev) if rank == 1 else None)
+        opt.step()
+        losses.append(None if l is None else float(l))
+    torch.save({"params": [p.detach().cpu() for p in stage_mod.parameters()], "losses": losses},
+               os.path.join(out_dir, f"r{rank}.pt"))
+    destroy_process_group()
+
+
+def trainer_gpu(rank, world, port, out_dir):
+    """The ddp_gpus_torchrun.py job on W GPUs through the product Trainer (persistent
+    engine, in-kernel xGMI all-reduce): status lines, steps/epoch, replicas in sync."""
+    dev, comm = _init_gpu(rank, world, port)
+    import contextlib
+    import io
+
+    from pytorch_distributed_training_tutorials_amd.data import DeviceDataLoader, DeviceTensorDataset, DistributedSampler
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+    from pytorch_distributed_training_tutorials_amd.utils.trainer import Trainer
+
+    out = {}
+    ds = DeviceTensorDataset.synthetic_classification(2048, 20, 4, device=dev, seed=1)
+    for engine in ("auto", "fused"):
+        torch.manual_seed(7 + rank)
+        model = ToyMLP(20, 32, 4)
+        loader = DeviceDataLoader(ds, batch_size=32, sampler=DistributedSampler(ds, world, rank))
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            t = Trainer(model, loader, torch.optim.SGD(model.parameters(), lr=0.05, momentum=0.9), rank,
+                        engine=engine, comm=comm)
+            t.train(3)
+        torch.cuda.synchronize()
+        flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+        out[engine] = {"engine": t.engine_name, "lines": buf.getvalue().splitlines(), "params": flat.cpu(),
+                       "in_sync": _digest_equal(comm, flat), "fallbacks": len(t.fallbacks)}
+    torch.save(out, os.path.join(out_dir, f"r{rank}.pt"))
+    destroy_process_group()
