@@ -66,6 +66,8 @@ def parse(argv=None):
     ap.add_argument("--stamps", action="store_true",
                     help="persistent engine: diagnostic run with in-kernel phase timers (separate from the timed run)")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
+    ap.add_argument("--no_mlp_side", action="store_true",
+                    help="skip the extra toy-MLP measurement (mlp_us_per_step) after the headline run")
     ap.add_argument("--share_gpu", action="store_true",
                     help="REHEARSAL ONLY: every rank on cuda:0 with a gloo control plane (RCCL refuses two ranks "
                          "per GPU), to exercise the N>1 path (xGMI self-test, in-kernel all-reduce, replica-sync "
@@ -251,7 +253,40 @@ def run_persistent(args, rank, world, dev, comm):
                          "workgroup; sampler shard recomputed in-kernel each epoch")}
     if phase:
         extra["phase_timers"] = phase
+    if args.model == "linear" and not args.no_mlp_side:
+        extra.update(_mlp_side(args, rank, world, dev, comm, xg))
     return t, extra
+
+
+def _mlp_side(args, rank, world, dev, comm, xg):
+    """Side measurement (AFTER the headline, same protocol, same K/W): the toy MLP
+    Linear(20,64)-ReLU-Linear(64,10) + CE + SGD on the persistent engine -- the
+    workload BASELINE.json's north star names; reported as extra keys only."""
+    from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+
+    side = argparse.Namespace(**vars(args))
+    side.model = "mlp"
+    model, loss = _build_model(side, dev)
+    ds = _dataset(side, dev, loss)
+    X, Y = ds.tensors
+    eng = FusedMLPStep(model, loss=loss, lr=args.lr, comm=comm, xgmi=xg)
+    if world > 1:
+        comm.broadcast(eng.P, 0)
+    sampler = DeviceDistributedSampler(len(ds), world, rank, seed=args.seed, device=dev)
+    cursor = torch.zeros(2, dtype=torch.int32, device=dev)
+    n_w, n_t = max(args.warmup, 1), args.steps
+    losses = torch.zeros(max(n_w, n_t), device=dev)
+    plan = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses)
+    plan.launch(n_w)
+    torch.cuda.synchronize(dev)
+    t = _timed(comm, dev, lambda: plan.launch(n_t))
+    failed = xg is not None and _xgmi_failed(comm, dev, xg, "MLP side measurement")
+    return {"mlp_us_per_step": None if failed else round(1e6 * t / n_t, 3),
+            "mlp_samples_per_s": None if failed else round(n_t * args.batch_size * world / t, 1),
+            "mlp_engine": eng.persistent_engine(args.batch_size, sampler),
+            "mlp_replicas_in_sync": _replicas_in_sync(comm, eng.P),
+            "mlp_final_loss": float(losses[n_t - 1].item())}
 
 
 def _xgmi_failed(comm, dev, xg, where: str) -> bool:

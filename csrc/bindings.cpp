@@ -1149,11 +1149,11 @@ PYBIND11_MODULE(_C, m) {
   py::class_<XgmiComm, std::shared_ptr<XgmiComm>>(m, "XgmiComm")
       .def(py::init<int, int, int, int>(), py::arg("rank"), py::arg("world"), py::arg("max_elems"), py::arg("device"))
       .def("handle", [](XgmiComm& c) { return py::bytes(c.handle()); })
-      .def("open", [](XgmiComm& c, std::vector<py::bytes> hs) {
+      .def("open", [](XgmiComm& c, std::vector<py::bytes> hs, std::vector<int> devices) {
         std::vector<std::string> v;
         for (auto& h : hs) v.push_back(std::string(h));
-        c.open(v);
-      })
+        c.open(v, devices);
+      }, py::arg("handles"), py::arg("devices") = std::vector<int>{})
       .def_property_readonly("ready", &XgmiComm::ready)
       .def_property_readonly("rank", &XgmiComm::rank)
       .def_property_readonly("world", &XgmiComm::world)

@@ -63,9 +63,19 @@ std::string XgmiComm::handle() const {
   return std::string(reinterpret_cast<const char*>(&h), sizeof(h));
 }
 
-void XgmiComm::open(const std::vector<std::string>& handles) {
+void XgmiComm::open(const std::vector<std::string>& handles, const std::vector<int>& devices) {
   if ((int)handles.size() != args_.world) throw std::invalid_argument("XgmiComm::open: need one handle per rank");
+  if (!devices.empty() && (int)devices.size() != args_.world)
+    throw std::invalid_argument("XgmiComm::open: need one device ordinal per rank");
   ok(hipSetDevice(device_), "hipSetDevice");
+  for (int p = 0; p < args_.world; ++p) {
+    if (p == args_.rank || devices.empty() || devices[p] == device_) continue;
+    int can = 0;
+    ok(hipDeviceCanAccessPeer(&can, device_, devices[p]), "hipDeviceCanAccessPeer");
+    if (!can)
+      throw std::runtime_error("XgmiComm::open: device " + std::to_string(device_) + " cannot access peer device " +
+                               std::to_string(devices[p]));
+  }
   for (int p = 0; p < args_.world; ++p) {
     if (p == args_.rank) continue;
     if (handles[p].size() != sizeof(hipIpcMemHandle_t)) throw std::invalid_argument("XgmiComm::open: bad handle");

@@ -21,8 +21,11 @@ class XgmiComm {
 
   // 64-byte IPC handle of this rank's buffer.
   std::string handle() const;
-  // Import every rank's handle (index = rank; own entry ignored).
-  void open(const std::vector<std::string>& handles);
+  // Import every rank's handle (index = rank; own entry ignored). `devices`
+  // (optional, index = rank): each rank's device ordinal on this node; a peer on
+  // another device this GPU cannot access directly (no xGMI/P2P path) throws, so
+  // the caller falls back to RCCL instead of faulting in the first push.
+  void open(const std::vector<std::string>& handles, const std::vector<int>& devices = {});
   bool ready() const { return ready_; }
   const XgmiArgs& args() const { return args_; }
   int error() const;  // synchronous read of the device error flag

@@ -39,8 +39,8 @@ class SinkCast(torch.autograd.Function):
     def backward(ctx, g):
         w = ctx.w
         sink = getattr(w, "_ptdt_grad_sink", None)
-        if sink is not None and w.grad is None:
-            out = sink()
+        out = sink() if (sink is not None and w.grad is None) else None  # None: slot already claimed
+        if out is not None:
             out.copy_(g)  # bf16 -> fp32 conversion straight into the bucket
             return out, None
         return g.to(w.dtype), None

@@ -23,10 +23,10 @@ from .._ext import native
 from .flat import contiguous_span, dense_like, same_layout
 
 
-def _split_by_device(params):
+def _split_by_device(params, with_grad_only: bool = True):
     out = {}
     for p in params:
-        if p.grad is None:
+        if with_grad_only and p.grad is None:
             continue
         out.setdefault((p.device, p.dtype), []).append(p)
     return out
@@ -176,6 +176,37 @@ class FusedAdam(Optimizer):
                     C.adam_multi_([p.data for p in ps], grads, ms, vs, step, group["lr"], b1, b2, group["eps"],
                                   group["weight_decay"], group["decoupled_weight_decay"], gscale)
         return loss
+
+    def state_dict(self):
+        """torch.optim.Adam layout: per parameter ``exp_avg``, ``exp_avg_sq`` and the
+        bias-correction ``step`` (a float32 scalar tensor) -- the kernels keep the step
+        as one device counter per (group, device); it is copied into the state here."""
+        for gi, group in enumerate(self.param_groups):
+            for (device, _dtype), ps in _split_by_device(group["params"], False).items():
+                step = self._steps.get((gi, device))
+                for p in ps:
+                    if p in self.state:
+                        self.state[p]["step"] = torch.tensor(float(step.item()) if step is not None else 0.0)
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict):
+        """Restores moments and the bias-correction step (a state_dict of this class or of
+        torch.optim.Adam/AdamW), so a resumed run continues the same trajectory."""
+        super().load_state_dict(state_dict)
+        self._steps = {}
+        for gi, group in enumerate(self.param_groups):
+            for (device, _dtype), ps in _split_by_device(group["params"], False).items():
+                steps = [self.state[p]["step"] for p in ps if "step" in self.state.get(p, {})]
+                if steps:
+                    self._steps[(gi, device)] = torch.full((1,), int(float(steps[0])), dtype=torch.int32,
+                                                           device=device)
+                for p in ps:  # the kernels need the flat-state layout: re-home the loaded moments
+                    st = self.state.get(p, {})
+                    if "exp_avg" in st:
+                        m, v = st.pop("exp_avg"), st.pop("exp_avg_sq")
+                        ms, vs = self._state_lists([p])
+                        ms[0].copy_(m)
+                        vs[0].copy_(v)
 
     @staticmethod
     def _cpu_step(ps, ms, vs, step, group, gscale):

@@ -67,7 +67,10 @@ class Communicator:
     def _make_native(self):
         C = native()
         _uid_counter[0] += 1
-        key = f"ptdt/rccl_uid/{self.name}/{_uid_counter[0]}"
+        # the key names the group by its global ranks: disjoint subgroups with the same
+        # communicator name never read each other's unique id
+        members = "all" if self.group is None else "-".join(map(str, dist.get_process_group_ranks(self.group)))
+        key = f"ptdt/rccl_uid/{self.name}/{members}/{_uid_counter[0]}"
         if self.world == 1:
             uid = C.RcclComm.new_unique_id()
         else:

@@ -101,6 +101,7 @@ class DistributedDataParallel(nn.Module):
         # grad sinks (ops/conv.py): weights cast through SinkCast land their gradient directly in
         # the bucket slot when .grad is None, which zero_grad arranges for exactly these params
         self._sink_params = []
+        self._forwards = 0
         if self.device.type == "cuda":
             from ..ops.conv import Conv2d
             from ..ops.linear import Linear
@@ -111,7 +112,7 @@ class DistributedDataParallel(nn.Module):
                          for t in (m.weight, m.bias) if t is not None}
             for i, p in enumerate(params):
                 if id(p) in sink_ids:
-                    p._ptdt_grad_sink = (lambda i=i, r=self.reducer: r.grad_view(i))
+                    p._ptdt_grad_sink = self._make_sink(i, p)
                     self._sink_params.append(p)
 
     # --------------------------------------------------------------- internals
@@ -122,6 +123,20 @@ class DistributedDataParallel(nn.Module):
         for r, d in enumerate(allv):
             if d != desc:
                 raise RuntimeError(f"DDP: rank {r} has a different parameter list than rank {self.comm.rank}")
+
+    def _make_sink(self, i: int, p):
+        """The bucket-slot view of parameter ``i`` for the FIRST gradient producer of
+        this forward only. A weight used twice in one forward (tied weights, a
+        module called twice) has several producers; the later ones get None and
+        return an ordinary gradient, which autograd sums into the first one's
+        slot before AccumulateGrad adopts it (writing each into the slot would
+        overwrite the earlier contribution)."""
+        def sink():
+            if getattr(p, "_ptdt_sink_forward", -1) == self._forwards:
+                return None
+            p._ptdt_sink_forward = self._forwards
+            return self.reducer.grad_view(i)
+        return sink
 
     def _make_hook(self, i: int):
         def hook(_p):
@@ -152,6 +167,7 @@ class DistributedDataParallel(nn.Module):
                 _flatten_broadcast(bufs, self.comm, 0)
         if torch.is_grad_enabled():
             self.reducer.prepare_for_backward(self.require_backward_grad_sync)
+            self._forwards += 1  # a new forward: every grad sink may be claimed once again
         return self.module(*args, **kwargs)
 
     @contextlib.contextmanager

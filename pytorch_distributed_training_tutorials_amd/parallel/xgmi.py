@@ -37,11 +37,14 @@ class XgmiAllReduce:
             handle = self.x.handle()
         except RuntimeError as e:
             print(f"[ptdt] xGMI buffer setup failed on rank {self.rank}: {e}", flush=True)
-        handles = comm.all_gather_object(handle)
+        # device ordinals travel with the handles: open() refuses a peer device with no
+        # direct access path (then every rank falls back to RCCL)
+        pairs = comm.all_gather_object((handle, self.device.index or 0))
+        handles = [h for h, _ in pairs]
         ok_open = int(all(len(h) > 0 for h in handles))
         if ok_open:
             try:
-                self.x.open(handles)
+                self.x.open(handles, [d for _, d in pairs])
             except RuntimeError as e:  # e.g. peer access unavailable
                 print(f"[ptdt] xGMI all-reduce unavailable on rank {self.rank}: {e}", flush=True)
                 ok_open = 0

@@ -22,6 +22,27 @@ def test_sink_cast_backward_writes_into_sink_and_is_adopted():
     torch.testing.assert_close(w.grad, torch.arange(12.0).view(4, 3) + 2)
 
 
+def test_sink_claimed_once_per_forward_sums_tied_uses():
+    """A weight cast twice in one forward (tied weights): the first backward claims the
+    slot, the second returns an ordinary gradient and autograd sums both (ADVICE r1:
+    writing both into the slot made the first contribution vanish)."""
+    w = nn.Parameter(torch.randn(4, 3))
+    buf = torch.full((12,), float("nan"))
+    claimed = []
+
+    def sink():  # the one-shot semantics of parallel.ddp's sinks
+        if claimed:
+            return None
+        claimed.append(1)
+        return buf.view(4, 3)
+
+    w._ptdt_grad_sink = sink
+    y1 = SinkCast.apply(w, torch.bfloat16)
+    y2 = SinkCast.apply(w, torch.bfloat16)
+    (y1.float().sum() * 1.0 + y2.float().sum() * 3.0).backward()
+    torch.testing.assert_close(w.grad, torch.full((4, 3), 4.0))
+
+
 def test_conv2d_is_a_drop_in_conv():
     a, b = Conv2d(3, 8, 3, padding=1), nn.Conv2d(3, 8, 3, padding=1)
     b.load_state_dict(a.state_dict())
@@ -107,3 +128,40 @@ def test_ddp_remove_grad_sinks_cpu_is_noop_and_gpu_detaches():
     finally:
         if own:
             dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_ddp_autocast_tied_weight_grads_are_summed():
+    """A Linear applied twice per forward under bf16 autocast with native DDP: its weight
+    gradient is the sum of both uses (the plain model's), not the last one."""
+    from pytorch_distributed_training_tutorials_amd.ops.linear import Linear
+    from pytorch_distributed_training_tutorials_amd.parallel import env
+    from pytorch_distributed_training_tutorials_amd.parallel.ddp import DistributedDataParallel
+
+    class Twice(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = Linear(16, 16)
+
+        def forward(self, x):
+            return self.lin(torch.relu(self.lin(x)))
+
+    env.init_process_group("nccl")
+    try:
+        dev = torch.device("cuda", 0)
+        torch.manual_seed(0)
+        m = Twice().to(dev)
+        ref = Twice().to(dev)
+        ref.load_state_dict(m.state_dict())
+        ddp = DistributedDataParallel(m, device_ids=[0])
+        x = torch.randn(8, 16, device=dev)
+        for _ in range(2):
+            ddp.zero_grad()
+            ref.zero_grad()
+            with torch.autocast("cuda", torch.bfloat16):
+                ddp(x).float().sum().backward()
+                ref(x).float().sum().backward()
+            torch.testing.assert_close(m.lin.weight.grad, ref.lin.weight.grad, rtol=2e-2, atol=2e-2)
+        ddp.remove_grad_sinks()
+    finally:
+        env.destroy_process_group()

@@ -149,3 +149,34 @@ def test_persistent_engine_selection():
     assert C.persistent_engine(128, 20, 0, 1, ce_soft, 2048, 1) == "workgroup"  # B > 64
     assert C.persistent_engine(32, 20, 0, 10, ce_index, 2048, 1) == "workgroup"  # Dout 10 not instantiated
     assert C.persistent_engine(32, 20, 0, 1, ce_soft, 2048, 1, 1) == "workgroup"  # forced
+
+
+def test_fused_adam_state_dict_resume_and_torch_interchange():
+    """FusedAdam's bias-correction step travels in the state_dict (torch layout): 3 steps +
+    save/load + 2 steps == 5 uninterrupted torch.optim.Adam steps, and the state loads into
+    torch.optim.Adam too (the step counter used to be dropped)."""
+    from pytorch_distributed_training_tutorials_amd.ops.optim import FusedAdam
+
+    def run(cls, steps, params, sd=None):
+        opt = cls(params, lr=1e-2)
+        if sd is not None:
+            opt.load_state_dict(sd)
+        for _ in range(steps):
+            for p in params:
+                p.grad = torch.sin(p.detach() * 3) + 0.1
+            opt.step()
+        return opt
+
+    torch.manual_seed(0)
+    p0 = [torch.nn.Parameter(torch.randn(5, 3)), torch.nn.Parameter(torch.randn(4))]
+    clone = lambda ps: [torch.nn.Parameter(t.detach().clone()) for t in ps]  # noqa: E731
+    ref = clone(p0)
+    run(torch.optim.Adam, 5, ref)
+    a = clone(p0)
+    sd = run(FusedAdam, 3, a).state_dict()
+    assert all(float(v["step"]) == 3.0 for v in sd["state"].values())
+    for cls in (FusedAdam, torch.optim.Adam):
+        b = clone(a)
+        run(cls, 2, b, sd)
+        for x, y in zip(b, ref):
+            torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
