@@ -61,7 +61,7 @@ def parse(argv=None):
                     help="gradient all-reduce of the fused engine: in-kernel one-shot xGMI (auto: if its "
                          "self-test passes on every rank) or RCCL")
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--persist", default=None, choices=["auto", "wave", "workgroup", "mfma"],
+    ap.add_argument("--persist", default=None, choices=["auto", "wave", "workgroup", "mfma", "tp"],
                     help="persistent engine variant (default: $PTDT_PERSIST or auto)")
     ap.add_argument("--stamps", action="store_true",
                     help="persistent engine: diagnostic run with in-kernel phase timers (separate from the timed run)")

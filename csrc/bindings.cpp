@@ -229,12 +229,14 @@ PersistBuild build_persistent(const Tensor& X, const c10::optional<Tensor>& Yf, 
     pa.lcache = lcache->data_ptr<int32_t>();
     pa.ltag = pa.lcache + 2 * stride;
   }
-  const bool wave = variant != kPersistWorkgroup && linear_wave_supported(a, pa);
-  const bool mfma = !wave && mlp_mfma_persistent_supported(a, pa);
-  TORCH_CHECK(wave || mfma || (variant < kPersistWave),
+  const bool wave = variant != kPersistWorkgroup && variant != kPersistMfma && variant != kPersistTp &&
+                    linear_wave_supported(a, pa);
+  const bool tp = !wave && (variant == kPersistAuto || variant == kPersistTp) && H > 0 && mlp_tp_supported(a, pa);
+  const bool mfma = !wave && !tp && mlp_mfma_persistent_supported(a, pa);
+  TORCH_CHECK(wave || mfma || tp || (variant < kPersistWave),
               "persistent: the requested engine variant does not support this configuration");
-  TORCH_CHECK(wave || fused_mlp_persistent_lds_bytes((int)B, (int)Din, (int)H, (int)Dout, (int)num_samples,
-                                                     world) <= 160 * 1024,
+  TORCH_CHECK(wave || tp || fused_mlp_persistent_lds_bytes((int)B, (int)Din, (int)H, (int)Dout, (int)num_samples,
+                                                           world) <= 160 * 1024,
               "persistent: model + epoch index list do not fit one workgroup's LDS");
   return b;
 }
@@ -317,11 +319,15 @@ std::string persistent_engine(int64_t B, int64_t Din, int64_t H, int64_t Dout, i
   PersistArgs pa{};
   pa.num_samples = (int)num_samples;
   pa.variant = (int)variant;
-  if (variant != kPersistWorkgroup && linear_wave_supported(a, pa)) {
+  pa.N = (int)std::max<int64_t>(num_samples, 1);
+  if (variant != kPersistWorkgroup && variant != kPersistMfma && variant != kPersistTp &&
+      linear_wave_supported(a, pa)) {
     int L = 0, R = 0, kp = 0;
     linear_wave_layout(a, pa, &L, &R, &kp);
     return "wave:L" + std::to_string(L) + "R" + std::to_string(R) + "K" + std::to_string(kp);
   }
+  if ((variant == kPersistAuto || variant == kPersistTp) && H > 0 && mlp_tp_supported(a, pa))
+    return "tp:" + std::to_string(H / 16) + "waves";
   if (variant != kPersistWorkgroup && mlp_mfma_persistent_supported(a, pa)) return "workgroup:mfma";
   return "workgroup";
 }

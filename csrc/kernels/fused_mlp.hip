@@ -953,7 +953,7 @@ const void* pick_persist_mfma(int loss, int H) {
 
 bool mfma_engine(const FusedMlpArgs& a, const PersistArgs& p) {
   return a.H > 0 && (p.variant == kPersistAuto || p.variant == kPersistMfma) &&
-         mlp_mfma_shape_ok(a.B, a.Din, a.H, a.Dout);
+         mlp_mfma_shape_ok(a.B, a.Din, a.H, a.Dout) && !(p.variant == kPersistAuto && mlp_tp_supported(a, p));
 }
 
 hipError_t check_dims(const FusedMlpArgs& a) {
@@ -1016,7 +1016,11 @@ hipError_t fused_mlp_persistent_prepare(const FusedMlpArgs& a, const PersistArgs
     return hipErrorInvalidValue;
   if (a.ar.world > 1 && (num_params(a) > a.ar.max_elems || a.ar.world != p.W || a.ar.rank != p.rank))
     return hipErrorInvalidValue;
-  if (p.variant != kPersistWorkgroup && linear_wave_supported(a, p)) return linear_wave_prepare(a, p, out);
+  if (p.variant != kPersistWorkgroup && p.variant != kPersistMfma && p.variant != kPersistTp &&
+      linear_wave_supported(a, p))
+    return linear_wave_prepare(a, p, out);
+  if ((p.variant == kPersistAuto || p.variant == kPersistTp) && a.H > 0 && mlp_tp_supported(a, p))
+    return mlp_tp_prepare(a, p, out);
   if (p.variant >= kPersistWave && p.variant != kPersistMfma) return hipErrorInvalidValue;
   const size_t lds = fused_mlp_persistent_lds_bytes(a.B, a.Din, a.H, a.Dout, p.num_samples, a.ar.world);
   if (lds > 160 * 1024) return hipErrorInvalidValue;

@@ -92,9 +92,13 @@ constexpr int kWavePrefetch = 3;  // batches in flight in the wave engine (regis
 // kPersistMfma: the workgroup engine with the 4-wave MFMA step body for
 // Linear-ReLU-Linear (B <= 32, Din <= 32, H in 16..64 step 16, Dout <= 16);
 // kPersistAuto picks it for those shapes.
+// kPersistTp: Linear-ReLU-Linear tensor-parallel across the waves of one
+// workgroup (mlp_tp.hip: each wave owns 16 hidden units, every product on
+// MFMA, one barrier per step); kPersistAuto picks it for B <= 32, Din <= 32,
+// H in 16..64 step 16, Dout <= 16.
 enum PersistVariant : int {
   kPersistAuto = 0, kPersistWorkgroup = 1, kPersistWave = 2, kPersistWaveRows = 3, kPersistWaveF = 4,
-  kPersistMfma = 5
+  kPersistMfma = 5, kPersistTp = 6
 };
 // The caller-provided list of `epoch` (clamped into the provided range), or nullptr.
 __device__ __forceinline__ const int32_t* given_list(const PersistArgs& p, int epoch) {
@@ -118,6 +122,8 @@ hipError_t fused_mlp_persistent_prepare(const FusedMlpArgs& a, const PersistArgs
 hipError_t persistent_launch(PersistLaunch& L, int n_steps, int64_t cursor_host_pos, hipStream_t s);
 bool linear_wave_supported(const FusedMlpArgs& a, const PersistArgs& p);
 bool mlp_mfma_persistent_supported(const FusedMlpArgs& a, const PersistArgs& p);
+bool mlp_tp_supported(const FusedMlpArgs& a, const PersistArgs& p);
+hipError_t mlp_tp_prepare(const FusedMlpArgs& a, const PersistArgs& p, PersistLaunch* out);
 // lane layout the wave engine picks: L lanes per row, R rows per lane group, kp features per lane
 void linear_wave_layout(const FusedMlpArgs& a, const PersistArgs& p, int* L, int* R, int* kp);
 hipError_t linear_wave_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s);

@@ -95,6 +95,7 @@ __device__ __forceinline__ void rank_epoch_indices_or(const int32_t* given, int3
     for (int i = tid; i < num_samples; i += nt) out[i] = src[i];
     return;
   }
+  if (lc.lists != nullptr && tid == 0) lc.tag[epoch & 1] = -1;  // slot being overwritten until published
   rank_epoch_indices(out, N, W, rank, num_samples, seed, epoch, shuffle, tid, nt);
   if (lc.lists != nullptr) {
     int32_t* dst = lc.lists + (epoch & 1) * lc.stride;

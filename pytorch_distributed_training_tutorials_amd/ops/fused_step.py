@@ -46,7 +46,7 @@ def _linears(model: nn.Module):
     raise ValueError("FusedMLPStep supports Linear or Linear-ReLU-Linear models; use the autograd engine otherwise")
 
 
-_VARIANTS = {"auto": 0, "workgroup": 1, "wave": 2, "wave_rows": 3, "wave_f": 4, "mfma": 5}
+_VARIANTS = {"auto": 0, "workgroup": 1, "wave": 2, "wave_rows": 3, "wave_f": 4, "mfma": 5, "tp": 6}
 
 
 def _variant_id(variant: str | None) -> int:

@@ -1,0 +1,123 @@
+"""Tensor-parallel MFMA engine for the toy MLP (csrc/kernels/mlp_tp.hip) against a plain
+PyTorch fp32 reference of the same DDP steps (Linear fwd, CE/MSE,
+Linear bwd, SGD with momentum), including partial last batches, epoch boundaries
+inside and across launches, and models without biases."""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(dev, N, Din, Dout, loss, seed):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    X = torch.randn(N, Din, device=dev, generator=g)
+    if loss == "ce_index":
+        Y = torch.randint(0, Dout, (N,), device=dev, generator=g)
+        Y[::7] = -100  # ignore_index rows
+    elif loss == "ce_soft":
+        Y = torch.rand(N, Dout, device=dev, generator=g)
+    else:
+        Y = torch.randn(N, Dout, device=dev, generator=g)
+    return X, Y
+
+
+def _torch_reference(model, X, Y, order, B, loss, steps, lr, mom):
+    """Plain fp32 PyTorch: the same batches (order = per-epoch index lists), SGD(momentum)."""
+    opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=mom)
+    ns = order[0].numel()
+    S = -(-ns // B)
+    losses = []
+    for k in range(steps):
+        e, j = divmod(k, S)
+        idx = order[e][j * B:(j + 1) * B].long()
+        x, y = X[idx], Y[idx]
+        opt.zero_grad()
+        out = model(x)
+        if loss == "mse":
+            l = F.mse_loss(out, y)
+        else:
+            l = F.cross_entropy(out, y)
+        l.backward()
+        opt.step()
+        losses.append(float(l))
+    return losses
+
+
+def _epoch_orders(sampler, epochs, dev):
+    out = []
+    for e in range(epochs):
+        sampler.set_epoch(e)
+        idx = torch.zeros(sampler.num_samples, dtype=torch.int32, device=dev)
+        sampler.generate(idx)
+        out.append(idx.clone())
+    sampler.set_epoch(0)
+    return out
+
+
+@pytest.mark.parametrize("B,Din,H,Dout,loss,bias", [
+    (32, 20, 64, 10, "ce_index", True),   # the BASELINE toy MLP
+    (32, 20, 64, 10, "ce_soft", True),
+    (16, 7, 32, 3, "ce_soft", True),
+    (32, 32, 16, 16, "mse", True),
+    (24, 20, 48, 1, "ce_soft", True),     # one class: the reference's zero-loss quirk shape
+    (32, 17, 64, 10, "ce_index", False),  # two input tiles, no biases
+    (8, 4, 16, 2, "mse", True),
+])
+def test_tp_engine_matches_torch_fp32(dev, B, Din, H, Dout, loss, bias):
+    from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+
+    N = 7 * B + 5  # a partial batch at every epoch end
+    X, Y = _data(dev, N, Din, Dout, loss, B + Din + H)
+    steps, lr, mom = 40, 0.05, 0.9
+    torch.manual_seed(3)
+    m_tp = nn.Sequential(nn.Linear(Din, H, bias=bias), nn.ReLU(), nn.Linear(H, Dout, bias=bias)).to(dev)
+    m_ref = nn.Sequential(nn.Linear(Din, H, bias=bias), nn.ReLU(), nn.Linear(H, Dout, bias=bias)).to(dev)
+    m_ref.load_state_dict(m_tp.state_dict())
+    eng = FusedMLPStep(m_tp, loss=loss, lr=lr, momentum=mom)
+    sampler = DeviceDistributedSampler(N, 1, 0, seed=2, device=dev)
+    assert eng.persistent_engine(B, sampler) == f"tp:{H // 16}waves"
+    order = _epoch_orders(sampler, 6, dev)
+    cursor = torch.zeros(2, dtype=torch.int32, device=dev)
+    losses = torch.zeros(steps, device=dev)
+    plan = eng.persistent_plan(X, Y, B, sampler, cursor, losses)
+    for n in (1, 12, 20, 7):  # launches start mid-epoch and cross epoch boundaries
+        plan.launch(n)
+    torch.cuda.synchronize()
+    S = -(-N // B)
+    assert cursor.tolist() == [steps // S, steps % S]
+    ref_losses = _torch_reference(m_ref, X, Y, order, B, loss, steps, lr, mom)
+    got = torch.cat([p.detach().reshape(-1) for p in m_tp.parameters()])
+    want = torch.cat([p.detach().reshape(-1) for p in m_ref.parameters()])
+    torch.testing.assert_close(got, want, rtol=2e-4, atol=2e-5)
+    # losses[i] is step i of the LAST launch (7 steps)
+    torch.testing.assert_close(losses[:7].cpu(), torch.tensor(ref_losses[-7:]), rtol=2e-4, atol=2e-5)
+    # the DDP bucket holds the last step's gradients, .grad views included
+    gref = torch.cat([p.grad.reshape(-1) for p in m_ref.parameters()])
+    torch.testing.assert_close(eng.G, gref, rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("N,B", [(32, 32), (40, 32), (300, 16)])
+def test_tp_engine_short_epochs_and_plan_splits(dev, N, B):
+    """One or two steps per epoch (list entries produced S+1 steps ahead), cached
+    epoch lists across launches: equals one long launch."""
+    from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+
+    X, Y = _data(dev, N, 20, 10, "ce_index", N)
+    out = []
+    for splits in ((37,), (1, 2, 3, 5, 26)):
+        torch.manual_seed(1)
+        eng = FusedMLPStep(ToyMLP(20, 64, 10).to(dev), loss="ce_index", lr=0.05, momentum=0.9)
+        sampler = DeviceDistributedSampler(N, 1, 0, seed=4, device=dev)
+        cursor = torch.zeros(2, dtype=torch.int32, device=dev)
+        losses = torch.zeros(37, device=dev)
+        plan = eng.persistent_plan(X, Y, B, sampler, cursor, losses)
+        for n in splits:
+            plan.launch(n)
+        torch.cuda.synchronize()
+        out.append(eng.P.clone())
+    assert torch.equal(out[0], out[1])

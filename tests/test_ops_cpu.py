@@ -142,7 +142,8 @@ def test_persistent_engine_selection():
     assert C.persistent_engine(32, 20, 0, 1, ce_soft, 256, 8).startswith("wave")  # 8 ranks
     assert C.persistent_engine(64, 16, 0, 1, ce_soft, 1000, 1).startswith("wave")
     # hidden layer: the 4-wave MFMA step body when the shape fits it, the LDS dot-product body otherwise
-    assert C.persistent_engine(32, 20, 64, 10, ce_index, 2048, 1) == "workgroup:mfma"
+    assert C.persistent_engine(32, 20, 64, 10, ce_index, 2048, 1) == "tp:4waves"  # tensor-parallel MFMA engine
+    assert C.persistent_engine(32, 20, 64, 10, ce_index, 2048, 1, 5) == "workgroup:mfma"  # forced
     assert C.persistent_engine(32, 20, 64, 10, ce_index, 2048, 1, 1) == "workgroup"  # forced
     assert C.persistent_engine(64, 20, 64, 10, ce_index, 2048, 1) == "workgroup"  # B > 32
     assert C.persistent_engine(32, 20, 100, 10, ce_index, 2048, 1) == "workgroup"  # H not a multiple of 16

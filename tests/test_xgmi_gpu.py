@@ -154,7 +154,7 @@ def test_persistent_engine_two_ranks_one_gpu(tmp_path, kind):
     world = 2
     spawn(_workers.persistent_two_procs_one_gpu, args=(world, free_port(), str(tmp_path), kind), nprocs=world)
     res = [torch.load(os.path.join(tmp_path, f"r{r}.pt"), weights_only=True) for r in range(world)]
-    assert res[0]["engine"].startswith("workgroup" if kind == "mlp" else "wave")
+    assert res[0]["engine"].startswith("tp" if kind == "mlp" else "wave")
     assert torch.equal(res[0]["persistent"], res[1]["persistent"])  # replicas in sync
     torch.testing.assert_close(res[0]["persistent"], res[0]["per_step"], rtol=1e-5, atol=1e-5)
     assert res[0]["cursor"].tolist() == [23 // 10, 23 % 10]  # 150 samples/rank / 16 -> 10 steps per epoch
