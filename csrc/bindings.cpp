@@ -629,6 +629,14 @@ Tensor relu_bwd(Tensor dy, Tensor y) {
   return dx;
 }
 
+Tensor sum_all_(Tensor x) {
+  check_gpu(x, "x");
+  auto out = torch::empty({}, x.options().dtype(at::kFloat));
+  c10::hip::HIPGuard guard(x.device().index());
+  hip_check(sum_all(x.data_ptr(), dt_of(x), x.numel(), out.data_ptr<float>(), cur_stream(x)), "sum_all");
+  return out;
+}
+
 void col_sum_(Tensor x, Tensor out, bool accumulate) {
   check_gpu(x, "x");
   TORCH_CHECK(x.dim() == 2 && out.scalar_type() == at::kFloat && out.numel() == x.size(1));
@@ -1035,6 +1043,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("tile") = 256, py::arg("split_k") = 1);
   m.def("relu_bwd", &relu_bwd);
   m.def("col_sum_", &col_sum_);
+  m.def("sum_all", &sum_all_);
   m.def("philox_", &philox_);
   m.def("one_hot", &one_hot_);
   m.def("gather_rows_", &gather_rows_);

@@ -34,6 +34,25 @@ __global__ void __launch_bounds__(kBlock) col_sum_kernel(const T* x, int64_t row
   atomicAdd(out + c, s);
 }
 
+// Sum of all elements into out[0] (fp32 accumulation, fixed order: deterministic).
+// One workgroup: the DP toy loss reduces [32, 2] (NB01:485); larger
+// inputs still run in one pass, 4 independent accumulators per thread.
+template <typename T>
+__global__ void __launch_bounds__(kBlock) sum_all_kernel(const T* x, int64_t n, float* out) {
+  __shared__ float scratch[kBlock / 64];
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int64_t i = threadIdx.x;
+  for (; i + 3 * kBlock < n; i += 4 * kBlock) {
+    a0 += Cvt<T>::load(x, i);
+    a1 += Cvt<T>::load(x, i + kBlock);
+    a2 += Cvt<T>::load(x, i + 2 * kBlock);
+    a3 += Cvt<T>::load(x, i + 3 * kBlock);
+  }
+  for (; i < n; i += kBlock) a0 += Cvt<T>::load(x, i);
+  const float s = block_sum((a0 + a1) + (a2 + a3), scratch);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
 __global__ void __launch_bounds__(kBlock) fill_kernel(float* x, float v, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * kBlock;
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += stride) x[i] = v;
@@ -90,6 +109,15 @@ hipError_t col_sum(const void* x, int dtype, int64_t rows, int64_t cols, float* 
   else
     hipLaunchKernelGGL(col_sum_kernel<uint16_t>, dim3(gx, gy), dim3(kBlock), 0, s, (const uint16_t*)x,
                        rows, cols, out, rows_per);
+  return hipGetLastError();
+}
+
+hipError_t sum_all(const void* x, int dtype, int64_t n, float* out, hipStream_t s) {
+  if (n <= 0) return hipErrorInvalidValue;
+  if (dtype == kF32)
+    hipLaunchKernelGGL(sum_all_kernel<float>, dim3(1), dim3(kBlock), 0, s, (const float*)x, n, out);
+  else
+    hipLaunchKernelGGL(sum_all_kernel<uint16_t>, dim3(1), dim3(kBlock), 0, s, (const uint16_t*)x, n, out);
   return hipGetLastError();
 }
 

@@ -31,6 +31,16 @@ def _load():
         if _mod is not None or _err is not None:
             return
         try:
+            override = os.environ.get("PTDT_EXT_PATH")  # e.g. the ASan/UBSan host build (tools/sanitize_host.py)
+            if override:
+                import importlib.util
+                import sys
+
+                spec = importlib.util.spec_from_file_location(__package__ + "._C", override)
+                _mod = importlib.util.module_from_spec(spec)
+                sys.modules[__package__ + "._C"] = _mod
+                spec.loader.exec_module(_mod)
+                return
             _mod = importlib.import_module(__package__ + "._C")
         except Exception as e:  # pragma: no cover - depends on build state
             if os.environ.get("PTDT_AUTOBUILD", "1") == "1":

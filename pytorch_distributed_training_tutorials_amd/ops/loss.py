@@ -89,3 +89,24 @@ class CrossEntropyLoss(nn.Module):
 class MSELoss(nn.Module):
     def forward(self, input, target):
         return mse_loss(input, target)
+
+
+class _SumFn(torch.autograd.Function):
+    """``x.sum()`` -> fp32 scalar by one native reduction launch; the backward is
+    the upstream scalar broadcast as a stride-0 view (no fill kernel at all)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape, ctx.dtype = x.shape, x.dtype
+        return native().sum_all(x.contiguous()).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(ctx.dtype).expand(ctx.shape)
+
+
+def sum_loss(x: torch.Tensor) -> torch.Tensor:
+    """The DP toy's ``loss = output.sum()`` (NB01:485): native on the GPU."""
+    if use_native(x) and x.dtype in (torch.float32, torch.bfloat16):
+        return _SumFn.apply(x)
+    return x.sum()

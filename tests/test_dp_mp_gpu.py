@@ -74,3 +74,16 @@ def test_mp_resnet50_matches_resnet50(dev):
         r = ref(x)
         torch.testing.assert_close(mp(x), r, rtol=1e-3, atol=1e-3)
         torch.testing.assert_close(pp(x), r, rtol=1e-3, atol=1e-3)
+
+
+def test_native_sum_loss_matches_torch(dev):
+    """K7: the DP loss ``output.sum()`` as one native reduction; backward = broadcast."""
+    from pytorch_distributed_training_tutorials_amd.ops.loss import sum_loss
+
+    for shape in ((32, 2), (7,), (1000, 33)):
+        x = torch.randn(*shape, device=dev, requires_grad=True)
+        l = sum_loss(x)
+        ref = x.detach().double().sum()
+        torch.testing.assert_close(l.double(), ref, rtol=1e-5, atol=1e-4)
+        (3.0 * l).backward()
+        torch.testing.assert_close(x.grad, torch.full_like(x, 3.0))

@@ -44,6 +44,19 @@ def test_torchrun_script_via_our_launcher_env_contract():
     assert "OMP_NUM_THREADS" in p.stderr  # torchrun's warning when nproc > 1
 
 
+@pytest.mark.parametrize("nproc", [1, 2])
+def test_torchrun_script_via_stock_torch_distributed_run(nproc):
+    """The reference invokes torchrun itself (02.ddp_toy_example.ipynb:277,318): the stock
+    launcher (python -m torch.distributed.run) drives ddp_gpus_torchrun.py unchanged."""
+    p = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(nproc),
+              "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "ddp_gpus_torchrun.py",
+              "--max_epochs", "2", "--batch_size", "32"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    steps = str(2048 // (32 * nproc))
+    assert sorted(STATUS.findall(p.stdout)) == sorted((str(r), str(e), "32", steps) for r in range(nproc)
+                                                      for e in range(2))
+
+
 def test_torchrun_default_single_worker_steps_64():
     """NB02:268-272: torchrun without --nproc-per-node -> W=1 -> Steps 64."""
     p = _run([sys.executable, "-m", "pytorch_distributed_training_tutorials_amd.launch", "--master-port",
