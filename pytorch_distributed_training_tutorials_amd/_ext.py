@@ -15,7 +15,9 @@ this package directory. Rules:
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 import threading
 
 import torch  # noqa: F401  -- must precede the extension import
@@ -33,9 +35,6 @@ def _load():
         try:
             override = os.environ.get("PTDT_EXT_PATH")  # e.g. the ASan/UBSan host build (tools/sanitize_host.py)
             if override:
-                import importlib.util
-                import sys
-
                 spec = importlib.util.spec_from_file_location(__package__ + "._C", override)
                 _mod = importlib.util.module_from_spec(spec)
                 sys.modules[__package__ + "._C"] = _mod

@@ -176,3 +176,17 @@ def test_bench_xgmi_timeout_fallback_is_agreed():
     assert not bench._xgmi_failed(_Comm(0), dev, _XG(0), "x")
     assert bench._xgmi_failed(_Comm(1), dev, _XG(0), "x")  # a peer timed out
     assert bench._xgmi_failed(_Comm(0), dev, _XG(1), "x")
+
+
+def test_native_extension_imports_without_override(monkeypatch):
+    """The in-tree _C loads through the normal path (no PTDT_EXT_PATH, no autobuild)."""
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items() if k != "PTDT_EXT_PATH"}
+    env["PTDT_AUTOBUILD"] = "0"
+    code = ("from pytorch_distributed_training_tutorials_amd._ext import native; "
+            "print(native().__file__)")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip().endswith(".so")
