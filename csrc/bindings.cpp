@@ -1067,6 +1067,13 @@ PYBIND11_MODULE(_C, m) {
   // code, dataset rows and parameters stay in that XCD's L2 (and the CU's
   // instruction cache) between launches. Returns the raw handle (wrap with
   // torch.cuda.ExternalStream); the stream lives as long as the process.
+  // hipSetDeviceFlags before the device's context exists (0 auto, 1 spin, 2 yield,
+  // 4 blocking sync): how host waits (hipDeviceSynchronize/events) poll the GPU.
+  m.def("set_device_flags", [](int device, unsigned flags) {
+    TORCH_CHECK(hipSetDevice(device) == hipSuccess, "hipSetDevice");
+    const hipError_t e = hipSetDeviceFlags(flags);
+    TORCH_CHECK(e == hipSuccess, "hipSetDeviceFlags: ", hipGetErrorString(e));
+  });
   m.def("cu_masked_stream", [](int device, std::vector<int> cus) {
     c10::hip::HIPGuard guard(device);
     int n_cu = 0;
@@ -1159,7 +1166,12 @@ PYBIND11_MODULE(_C, m) {
       .def("error", &RcclComm::error)
       .def("abort", &RcclComm::abort)
       .def_property_readonly("aborted", &RcclComm::aborted)
-      .def("fingerprints", &RcclComm::fingerprints);
+      .def("fingerprints", &RcclComm::fingerprints)
+      .def_property_readonly("captured", &RcclComm::captured)
+      .def("expect_captured", &RcclComm::expect_captured, py::arg("k"))
+      .def_property_readonly("completed_captured", &RcclComm::completed_captured)
+      .def_property_readonly("event_pool_size", &RcclComm::event_pool_size)
+      .def_property_readonly("events_created", &RcclComm::events_created);
 
   py::class_<XgmiComm, std::shared_ptr<XgmiComm>>(m, "XgmiComm")
       .def(py::init<int, int, int, int>(), py::arg("rank"), py::arg("world"), py::arg("max_elems"), py::arg("device"))

@@ -1,6 +1,8 @@
 // Native RCCL communicator (see rccl_comm.h for the design notes).
 #include "rccl_comm.h"
 
+#include "../kernels/kernels.h"
+
 #include <cstdio>
 #include <cstring>
 #include <sstream>
@@ -33,6 +35,13 @@ RcclComm::RcclComm(int rank, int world, const std::vector<uint8_t>& uid, int dev
   std::memcpy(id.internal, uid.data(), uid.size());
   hip_check(hipSetDevice(device), "hipSetDevice");
   check(ncclCommInitRank(&comm_, world, id, rank), "ncclCommInitRank");
+  hip_check(hipMalloc(&graph_ctr_dev_, sizeof(uint64_t)), "hipMalloc(graph counter)");
+  hip_check(hipMemset(graph_ctr_dev_, 0, sizeof(uint64_t)), "hipMemset(graph counter)");
+  void* mirror = nullptr;
+  hip_check(hipHostMalloc(&mirror, sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent),
+            "hipHostMalloc(graph counter mirror)");
+  graph_ctr_host_ = static_cast<volatile uint64_t*>(mirror);
+  *graph_ctr_host_ = 0;
   if (timeout_s_ > 0) watchdog_ = std::thread([this] { watchdog_loop(); });
 }
 
@@ -45,7 +54,11 @@ RcclComm::~RcclComm() {
     for (auto& r : pending_)
       if (r.done) (void)hipEventDestroy(r.done);
     pending_.clear();
+    for (auto ev : free_events_) (void)hipEventDestroy(ev);
+    free_events_.clear();
   }
+  if (graph_ctr_dev_) (void)hipFree(graph_ctr_dev_);
+  if (graph_ctr_host_) (void)hipHostFree(const_cast<uint64_t*>(graph_ctr_host_));
   if (comm_ != nullptr) {
     if (aborted_.load())
       ; // already aborted by the watchdog
@@ -76,18 +89,49 @@ void RcclComm::track(const char* op, size_t count, int dtype, hipStream_t s) {
     fp_log_.push_back(os.str());
     if (fp_log_.size() > 4096) fp_log_.erase(fp_log_.begin(), fp_log_.begin() + 2048);
   }
-  if (timeout_s_ <= 0 || group_depth_ > 0) return;
+  if (group_depth_ > 0) return;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   (void)hipStreamIsCapturing(s, &cs);
-  if (cs != hipStreamCaptureStatusNone) return;  // replayed later; not tracked
+  if (cs != hipStreamCaptureStatusNone) {
+    // part of a graph: a captured counter bump marks its completion at every replay
+    hip_check(comm_done_mark(graph_ctr_dev_, const_cast<uint64_t*>(graph_ctr_host_), s), "comm_done_mark");
+    captured_.fetch_add(1);
+    return;
+  }
+  if (timeout_s_ <= 0) return;
   hipEvent_t ev = nullptr;
-  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (!free_events_.empty()) {
+      ev = free_events_.back();
+      free_events_.pop_back();
+    }
+  }
+  if (ev == nullptr) {
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) return;
+    events_created_.fetch_add(1);
+  }
   if (hipEventRecord(ev, s) != hipSuccess) {
-    (void)hipEventDestroy(ev);
+    std::lock_guard<std::mutex> g(mu_);
+    free_events_.push_back(ev);
     return;
   }
   std::lock_guard<std::mutex> g(mu_);
   pending_.push_back(CollectiveRecord{seq, op, count, dtype, ev, std::chrono::steady_clock::now()});
+}
+
+void RcclComm::expect_captured(uint64_t k) {
+  if (k == 0) return;
+  std::lock_guard<std::mutex> g(mu_);
+  graph_expected_ += k;
+  if (timeout_s_ > 0) graph_pending_.emplace_back(graph_expected_, std::chrono::steady_clock::now());
+}
+
+uint64_t RcclComm::completed_captured() const { return *graph_ctr_host_; }
+
+size_t RcclComm::event_pool_size() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return free_events_.size();
 }
 
 void RcclComm::watchdog_loop() {
@@ -103,7 +147,7 @@ void RcclComm::watchdog_loop() {
     while (!pending_.empty()) {
       auto& r = pending_.front();
       if (hipEventQuery(r.done) == hipSuccess) {
-        (void)hipEventDestroy(r.done);
+        free_events_.push_back(r.done);  // recycled: no create/destroy per collective
         pending_.pop_front();
         continue;
       }
@@ -121,6 +165,23 @@ void RcclComm::watchdog_loop() {
         lk.lock();
       }
       break;
+    }
+    const uint64_t done = *graph_ctr_host_;
+    while (!graph_pending_.empty() && graph_pending_.front().first <= done) graph_pending_.pop_front();
+    if (!graph_pending_.empty() && !aborted_.load()) {
+      const double age = std::chrono::duration<double>(std::chrono::steady_clock::now() -
+                                                       graph_pending_.front().second).count();
+      if (age > timeout_s_) {
+        std::ostringstream os;
+        os << "watchdog: graph-captured collectives on rank " << rank_ << " completed " << done << " of "
+           << graph_pending_.front().first << " expected within " << timeout_s_ << " s";
+        error_ = os.str();
+        std::fprintf(stderr, "[ptdt] %s; aborting communicator\n", error_.c_str());
+        aborted_.store(true);
+        lk.unlock();
+        (void)ncclCommAbort(comm_);
+        lk.lock();
+      }
     }
     if (!aborted_.load() && comm_ != nullptr) {
       ncclResult_t ae = ncclSuccess;

@@ -14,7 +14,13 @@
 //     events of outstanding collectives and aborts the communicator on error
 //     or timeout instead of hanging;
 //   * an optional collective fingerprint log (op, count, dtype, seq#) for
-//     cross-rank mismatch detection.
+//     cross-rank mismatch detection;
+//   * completion tracking without per-call allocation: eager collectives take
+//     a recycled event from a pool; a collective issued under hipGraph capture
+//     is followed (in the graph) by a one-thread kernel that bumps a device
+//     counter and mirrors it into host-mapped memory, so replays are watched
+//     too -- the replaying code declares how many completions it expects
+//     (expect_captured) and the watchdog polls the mirror.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -80,6 +86,16 @@ class RcclComm {
   uint64_t seq() const { return seq_.load(); }
   std::vector<std::string> fingerprints() const;
 
+  // hipGraph-captured collectives: `captured()` counts the collectives captured
+  // so far (a graph's share is the difference around its capture); after each
+  // replay of a graph holding k of them call expect_captured(k). completed_captured()
+  // is the device counter's host mirror.
+  uint64_t captured() const { return captured_.load(); }
+  void expect_captured(uint64_t k);
+  uint64_t completed_captured() const;
+  size_t event_pool_size() const;
+  size_t events_created() const { return events_created_.load(); }
+
  private:
   void check(ncclResult_t r, const char* what);
   void track(const char* op, size_t count, int dtype, hipStream_t s);
@@ -95,6 +111,13 @@ class RcclComm {
   mutable std::mutex mu_;
   std::condition_variable cv_;
   std::deque<CollectiveRecord> pending_;
+  std::vector<hipEvent_t> free_events_;  // recycled completion events
+  std::atomic<size_t> events_created_{0};
+  uint64_t* graph_ctr_dev_ = nullptr;              // device counter (captured kernels bump it)
+  volatile uint64_t* graph_ctr_host_ = nullptr;    // host-mapped mirror read by the watchdog
+  std::atomic<uint64_t> captured_{0};
+  uint64_t graph_expected_ = 0;
+  std::deque<std::pair<uint64_t, std::chrono::steady_clock::time_point>> graph_pending_;
   std::vector<std::string> fp_log_;
   std::string error_;
   std::thread watchdog_;

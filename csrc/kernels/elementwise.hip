@@ -152,4 +152,16 @@ hipError_t bn_relu_apply(const void* x, int dtype, const float* scale, const flo
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------ comm_done_mark
+__global__ void comm_done_mark_kernel(unsigned long long* ctr, uint64_t* host_mirror) {
+  const unsigned long long v = atomicAdd(ctr, 1ull) + 1ull;
+  __hip_atomic_store(host_mirror, (uint64_t)v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t comm_done_mark(uint64_t* ctr, uint64_t* host_mirror, hipStream_t s) {
+  hipLaunchKernelGGL(comm_done_mark_kernel, dim3(1), dim3(1), 0, s, reinterpret_cast<unsigned long long*>(ctr),
+                     host_mirror);
+  return hipGetLastError();
+}
+
 }  // namespace ptdt

@@ -238,6 +238,10 @@ hipError_t gemm_bf16_big(const BigGemmArgs& g, hipStream_t s);
 hipError_t relu_backward(const void* dy, const void* y, void* dx, int dtype, int64_t n, hipStream_t s);
 // out[0] = sum of all n elements (fp32 accumulate, deterministic), one workgroup.
 hipError_t sum_all(const void* x, int dtype, int64_t n, float* out, hipStream_t s);
+
+// One-thread completion mark for a graph-captured collective (csrc/comm/rccl_comm.cpp):
+// ++*ctr (device memory), then the new value is stored to the host-mapped mirror.
+hipError_t comm_done_mark(uint64_t* ctr, uint64_t* host_mirror, hipStream_t s);
 hipError_t col_sum(const void* x, int dtype, int64_t rows, int64_t cols, float* out, int accumulate,
                    hipStream_t s);
 hipError_t fill_f32(float* x, float v, int64_t n, hipStream_t s);

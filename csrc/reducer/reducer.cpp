@@ -1,6 +1,8 @@
 // Bucketed gradient reducer (see reducer.h).
 #include "reducer.h"
 
+#include <cstdlib>
+
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -66,6 +68,10 @@ Reducer::Reducer(std::vector<at::Tensor> params, std::vector<std::vector<int64_t
     if (!comm_) throw std::invalid_argument("Reducer: GPU parameters need a RcclComm");
     device_ = params_[0].device().index();
     comm_stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/true, device_);
+    // PTDT_FORCE_COLLECTIVE=1: a one-rank job still issues every bucket all-reduce
+    // (profiling the overlap on one GPU; the average over one rank is the identity)
+    const char* fc = std::getenv("PTDT_FORCE_COLLECTIVE");
+    force_collective_ = fc != nullptr && fc[0] == '1';
     hip_ok(hipSetDevice(device_), "hipSetDevice");
     hip_ok(hipEventCreateWithFlags(&ev_ready_, hipEventDisableTiming), "hipEventCreate");
     hip_ok(hipEventCreateWithFlags(&ev_done_, hipEventDisableTiming), "hipEventCreate");
@@ -215,7 +221,7 @@ void Reducer::launch(size_t bi) {
   auto& b = buckets_[bi];
   b.launched = true;
   if (on_gpu_) {
-    if (comm_->world() == 1) return;  // the average over one rank is the bucket itself: no collective
+    if (comm_->world() == 1 && !force_collective_) return;  // the average over one rank is the bucket itself
     hipStream_t compute = c10::hip::getCurrentHIPStream(device_).stream();
     hipStream_t comm = comm_stream_->stream();
     hip_ok(hipEventRecord(ev_ready_, compute), "hipEventRecord");

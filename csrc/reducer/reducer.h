@@ -106,6 +106,7 @@ class Reducer {
   std::optional<c10::hip::HIPStream> comm_stream_;
   hipEvent_t ev_ready_ = nullptr;  // compute -> comm ordering
   hipEvent_t ev_done_ = nullptr;   // comm -> compute join
+  bool force_collective_ = false;  // PTDT_FORCE_COLLECTIVE=1: collectives even at world 1
   int device_ = -1;
 };
 

@@ -286,7 +286,7 @@ class FusedMLPStep:
         hipGraph. ``warmup_fn`` (default ``fn``) runs once eagerly first (RCCL and
         allocator warm-up); all engine state plus ``extra_state`` tensors are
         restored afterwards, so capturing never changes the training trajectory.
-        Returns a ``torch.cuda.CUDAGraph`` -- call ``.replay()``."""
+        Returns a :class:`WatchedGraph` -- call ``.replay()``."""
         tensors = self.state() + [t for t in extra_state if t is not None]
         saved = [t.clone() for t in tensors]
         pending = self._pending
@@ -300,12 +300,34 @@ class FusedMLPStep:
             t.copy_(v)
         self._pending = pending
         g = torch.cuda.CUDAGraph()
+        rc = getattr(self.comm, "handle", None)
+        before = rc.captured if rc is not None else 0
         with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):
             fn()
         self._pending = pending
         torch.cuda.synchronize(self.device)
-        return g
+        return WatchedGraph(g, rc, (rc.captured - before) if rc is not None else 0)
 
     def capture(self, X, Y, idx_buf: torch.Tensor, batches, losses: torch.Tensor | None = None):
         """Graph of :meth:`run` over ``batches``; refresh ``idx_buf`` before each replay."""
         return self.graph(lambda: self.run(X, Y, idx_buf, batches, losses), extra_state=(losses,))
+
+
+class WatchedGraph:
+    """A captured hipGraph whose RCCL collectives the communicator's watchdog
+    follows: each captured collective is followed in the graph by a device
+    completion mark (csrc/comm/rccl_comm.cpp), and every :meth:`replay` declares
+    the ``n_collectives`` marks it will produce, so a replay that stalls aborts
+    the communicator after ``PTDT_COMM_TIMEOUT`` instead of hanging."""
+
+    def __init__(self, graph, rccl, n_collectives: int):
+        self.graph, self.rccl, self.n_collectives = graph, rccl, n_collectives
+
+    def replay(self):
+        self.graph.replay()
+        if self.n_collectives and self.rccl is not None:
+            self.rccl.expect_captured(self.n_collectives)
+
+    def reset(self):
+        self.graph.reset()
+

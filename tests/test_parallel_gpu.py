@@ -178,3 +178,85 @@ def test_ddp_channels_last_grads_keep_param_layout(pg, dev):
     before = w.detach().clone()
     opt.step()
     torch.testing.assert_close(w.detach(), before - 0.1 * w.grad, rtol=1e-6, atol=1e-7)
+
+
+def test_rccl_watchdog_event_pool_recycles(pg, dev):
+    """Eager collectives under the watchdog reuse completion events (no create/destroy per call)."""
+    import time
+
+    from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
+
+    c = comm_mod.new_communicator(dev, name="evpool")  # watchdog on (PTDT_COMM_TIMEOUT, 600 s)
+    t = torch.ones(1024, device=dev)
+    for r in range(30):
+        for _ in range(10):
+            c.all_reduce(t, "sum")
+        torch.cuda.synchronize()
+        time.sleep(0.12 if r % 10 == 9 else 0.0)  # let the watchdog drain and recycle
+    time.sleep(0.3)
+    h = c.handle
+    assert h.seq == 300
+    assert h.events_created <= 120, h.events_created  # bounded by what was in flight, not by 300 calls
+    assert h.event_pool_size == h.events_created  # all completed and returned to the pool
+    torch.testing.assert_close(t, torch.ones(1024, device=dev))
+
+
+def test_graph_captured_collectives_complete_on_device_counter(pg, dev):
+    import time
+
+    from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
+
+    C = comm_mod.native()
+    rc = C.RcclComm(0, 1, C.RcclComm.new_unique_id(), dev.index or 0, 1.0, False)
+    t = torch.arange(64, dtype=torch.float32, device=dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            rc.all_reduce(t, 0, s.cuda_stream)  # warm-up outside capture
+    torch.cuda.synchronize()
+    before = rc.captured
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+        for _ in range(3):
+            t.mul_(1.0)
+            rc.all_reduce(t, 0, s.cuda_stream)
+    k = rc.captured - before
+    assert k == 3
+    for _ in range(4):
+        g.replay()
+        rc.expect_captured(k)
+    torch.cuda.synchronize()
+    assert rc.completed_captured == 12
+    time.sleep(1.3)  # past the timeout: every expectation was met, so no abort
+    assert not rc.aborted, rc.error()
+    rc.expect_captured(1)  # a completion that never comes: the watchdog aborts
+    deadline = time.time() + 5
+    while not rc.aborted and time.time() < deadline:
+        time.sleep(0.1)
+    assert rc.aborted and "graph-captured" in rc.error()
+    torch.testing.assert_close(t, torch.arange(64, dtype=torch.float32, device=dev))
+
+
+def test_force_collective_issues_bucket_allreduce_at_world_1(pg, dev, monkeypatch):
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP
+    from pytorch_distributed_training_tutorials_amd.ops.loss import cross_entropy
+    from pytorch_distributed_training_tutorials_amd.parallel.ddp import DistributedDataParallel
+
+    x = torch.randn(32, 20, device=dev)
+    y = torch.randint(0, 10, (32,), device=dev)
+    grads = []
+    for force in ("0", "1"):
+        monkeypatch.setenv("PTDT_FORCE_COLLECTIVE", force)
+        torch.manual_seed(0)
+        ddp = DistributedDataParallel(ToyMLP(20, 64, 10).to(dev), device_ids=[0], bucket_cap_mb=0.001,
+                                      first_bucket_mb=0.0001)
+        nb = len(ddp.bucket_sizes_bytes())
+        s0 = ddp.comm.handle.seq
+        ddp.zero_grad()
+        cross_entropy(ddp(x), y).backward()
+        torch.cuda.synchronize()
+        issued = ddp.comm.handle.seq - s0
+        assert issued == (nb if force == "1" else 0), (force, issued, nb)
+        grads.append(torch.cat([p.grad.reshape(-1) for p in ddp.module.parameters()]))
+    torch.testing.assert_close(grads[0], grads[1], rtol=0, atol=0)
