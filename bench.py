@@ -63,6 +63,10 @@ def parse(argv=None):
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--persist", default=None, choices=["auto", "wave", "workgroup", "mfma", "tp"],
                     help="persistent engine variant (default: $PTDT_PERSIST or auto)")
+    ap.add_argument("--sampler", default="device", choices=["device", "torch"],
+                    help="device: in-kernel Feistel permutation (DistributedSampler semantics, different order); "
+                         "torch: torch.randperm-identical order (csrc/kernels/torch_perm.hip) generated inside "
+                         "the timed region, one launch per run")
     ap.add_argument("--stamps", action="store_true",
                     help="persistent engine: diagnostic run with in-kernel phase timers (separate from the timed run)")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
@@ -212,19 +216,47 @@ def run_persistent(args, rank, world, dev, comm):
     cursor = torch.zeros(2, dtype=torch.int32, device=dev)
     chunk = 8192
     losses = torch.zeros(min(chunk, max(args.steps, args.warmup, 1)), device=dev)
-    # launch planned once (native PersistentPlan): the timed region is hipLaunchKernel(s) + the kernel
-    plan = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses, variant=variant)
     launches = [min(chunk, args.steps - d) for d in range(0, args.steps, chunk)]
-    for d in range(0, max(args.warmup, 1), chunk):
-        plan.launch(min(chunk, max(args.warmup, 1) - d))
+    n_warm = max(args.warmup, 1)
+    if args.sampler == "torch":
+        # torch-identical epoch orders: the lists of the epochs a run touches (+1 for the
+        # engine's one-position-ahead staging) come from the torch_perm kernel, enqueued
+        # right before the engine launch -- inside the timed region for the timed run
+        from pytorch_distributed_training_tutorials_amd._ext import native
+
+        C = native()
+        n, ns = len(ds), sampler.num_samples
+
+        def order_plan(pos0, steps):
+            e_a, e_b = pos0 // S, (pos0 + steps) // S + 1
+            seeds = torch.tensor([args.seed + e for e in range(e_a, e_b + 1)], dtype=torch.int64, device=dev)
+            buf = torch.empty(e_b - e_a + 1, ns, dtype=torch.int32, device=dev)
+            ws = (torch.empty((e_b - e_a + 1) * 4 * n, dtype=torch.int32, device=dev)
+                  if C.torch_perm_needs_ws(n) else None)
+            pl = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses, variant=variant, idx=buf,
+                                     idx_e0=e_a)
+
+            def run():
+                C.torch_perm_(seeds, n, world, rank, ns, buf, ws)
+                for d in range(0, steps, chunk):
+                    pl.launch(min(chunk, steps - d), pos0 + d)
+            return run
+
+        order_plan(0, n_warm)()
+        timed_steps = order_plan(n_warm, args.steps)
+    else:
+        # launch planned once (native PersistentPlan): the timed region is hipLaunchKernel(s) + the kernel
+        plan = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses, variant=variant)
+        for d in range(0, n_warm, chunk):
+            plan.launch(min(chunk, n_warm - d))
+        launch = plan.launch
+
+        def timed_steps():
+            for n in launches:
+                launch(n)
     torch.cuda.synchronize(dev)
     if _xgmi_failed(comm, dev, xg, "warmup"):
         return _rccl_fallback(args, rank, world, dev, comm)
-    launch = plan.launch
-
-    def timed_steps():
-        for n in launches:
-            launch(n)
 
     t = _timed(comm, dev, timed_steps)
     if _xgmi_failed(comm, dev, xg, "timed run"):
@@ -243,6 +275,11 @@ def run_persistent(args, rank, world, dev, comm):
                  "total_cycles_per_step": round(v[7] / args.steps, 1), "clock_GHz": round(clk / 1e9, 3)}
     last = (args.steps - 1) % chunk
     extra = {"replicas_in_sync": in_sync, "steps_per_epoch": S, "launches_timed": math.ceil(args.steps / chunk),
+             "sampler": ("torch.randperm-identical DistributedSampler order (torch_perm kernel in the timed region)"
+                         if args.sampler == "torch" else
+                         "device Feistel permutation: DistributedSampler semantics (per-epoch reshuffle, padded "
+                         "disjoint rank shards) in a different order than torch.randperm; --sampler torch runs "
+                         "the torch-identical order"),
              "final_loss": float(losses[last].item()),
              "allreduce": "xgmi-oneshot (in-kernel)" if world > 1 else "identity (world 1)",
              "persistent_engine": which,

@@ -843,7 +843,8 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> weight, c10::op
 // Backward: returns (dx, dweight, dbias, dres); dres undefined unless want_dres.
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::optional<Tensor> weight, Tensor stats,
                            bool relu, bool want_dres, bool want_dweight, c10::optional<Tensor> tickets,
-                           c10::optional<Tensor> dweight_out, c10::optional<Tensor> dbias_out) {
+                           c10::optional<Tensor> dweight_out, c10::optional<Tensor> dbias_out,
+                           c10::optional<Tensor> dy2) {
   int64_t M;
   int C;
   bn_rows(x, &M, &C);
@@ -853,6 +854,10 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::op
               "batchnorm: stats must be the [4, C] forward statistics");
   BnBwdArgs a{};
   a.dy = dy.data_ptr();
+  if (dy2.has_value() && dy2->defined()) {  // second addend (residual link), same layout as x
+    same_rows(*dy2, x, "dy2");
+    a.dy2 = dy2->data_ptr();
+  }
   a.x = x.data_ptr();
   if (relu && y.has_value() && y->defined()) {  // else: the mask is recomputed from x (no residual)
     same_rows(*y, x, "y");
@@ -1056,7 +1061,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("momentum"), py::arg("eps"), py::arg("tickets") = py::none());
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("weight"), py::arg("stats"),
         py::arg("relu"), py::arg("want_dres"), py::arg("want_dweight"), py::arg("tickets") = py::none(),
-        py::arg("dweight_out") = py::none(), py::arg("dbias_out") = py::none());
+        py::arg("dweight_out") = py::none(), py::arg("dbias_out") = py::none(), py::arg("dy2") = py::none());
   m.def("maxpool2d_fwd", &maxpool2d_fwd);
   m.def("maxpool2d_bwd", &maxpool2d_bwd);
   m.def("bn_apply", &bn_apply_, py::arg("x"), py::arg("residual"), py::arg("scale"), py::arg("shift"),

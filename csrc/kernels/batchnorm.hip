@@ -31,6 +31,9 @@
 //   dx    = k dy' - k s2 (x - mean) - k s1,   k = gamma invstd,
 //           s1 = dbeta / M, s2 = invstd^2 sum dy'(x - mean) / M
 // i.e. dx = A dy' + B x + C per channel; with a residual branch d(residual) = dy'.
+// An optional second addend dy2 (the residual gradient of the NEXT block, handed
+// over by ops/norm.py's residual link) is summed into dy on the fly, replacing a
+// separate add kernel (two reads + a write) by one extra read in each pass.
 // The ReLU mask comes from the forward output y, or -- for BNs without a residual
 // -- is recomputed from x with the forward's own fmaf(x, scale, shift), sparing
 // one of the three reads in both backward passes.
@@ -320,8 +323,9 @@ __device__ __forceinline__ float masked_dy(float g, float x, float y, float sc, 
   return g;
 }
 
-template <typename T, int MASK>
-__global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+template <typename T, int MASK, bool ADD2>
+__global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                             const T* __restrict__ x,
                                                              const T* __restrict__ y, int64_t M, int C, int TC,
                                                              int RPI, int64_t rows_per_block, float* ws,
                                                              int* tickets, BnBwdParams p) {
@@ -347,13 +351,20 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
     }
     int64_t r = r0 + rr;
     for (; r + (U - 1) * RPI < r1; r += U * RPI) {
-      float g[U][V], a[U][V], o[U][V];
+      float g[U][V], a[U][V], o[U][V], g2[ADD2 ? U : 1][V];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t off = (r + u * RPI) * C + c0;
         VecIO<T>::load(dy + off, g[u]);
+        if constexpr (ADD2) VecIO<T>::load(dy2 + off, g2[u]);
         VecIO<T>::load(x + off, a[u]);
         if constexpr (MASK == 1) VecIO<T>::load(y + off, o[u]);
+      }
+      if constexpr (ADD2) {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int v = 0; v < V; ++v) g[u][v] += g2[u][v];
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -368,6 +379,12 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
       float g[V], a[V], o[V];
       const int64_t off = r * C + c0;
       VecIO<T>::load(dy + off, g);
+      if constexpr (ADD2) {
+        float g2[V];
+        VecIO<T>::load(dy2 + off, g2);
+#pragma unroll
+        for (int v = 0; v < V; ++v) g[v] += g2[v];
+      }
       VecIO<T>::load(x + off, a);
       if constexpr (MASK == 1) VecIO<T>::load(y + off, o);
 #pragma unroll
@@ -402,8 +419,9 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
   if (tid == 0) rearm(tickets + blockIdx.y);
 }
 
-template <typename T, int MASK, bool RES>
-__global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ x,
+template <typename T, int MASK, bool RES, bool ADD2>
+__global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
+                                                                const T* __restrict__ x,
                                                                 const T* __restrict__ y, T* __restrict__ dx,
                                                                 T* __restrict__ dres, BnBwdParams p, int64_t nvec,
                                                                 int C) {
@@ -425,6 +443,12 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const T* __restr
     const int c0 = (int)(i % cv) * V;
     float g[V], a[V], o[V];
     VecIO<T>::load(dy + i * V, g);
+    if constexpr (ADD2) {
+      float g2[V];
+      VecIO<T>::load(dy2 + i * V, g2);
+#pragma unroll
+      for (int v = 0; v < V; ++v) g[v] += g2[v];
+    }
     VecIO<T>::load(x + i * V, a);
     if constexpr (MASK == 1) VecIO<T>::load(y + i * V, o);
 #pragma unroll
@@ -490,24 +514,34 @@ hipError_t apply_impl(const void* x, const void* res, void* y, const float* scal
   return hipGetLastError();
 }
 
-template <typename T, int MASK>
+template <typename T, int MASK, bool ADD2>
 hipError_t bwd_launch(const BnBwdArgs& a, const Geom& g, hipStream_t s) {
   constexpr int V = VecIO<T>::V;
   const size_t sh_red = (size_t)2 * kRed * V * sizeof(float) + 16;
   const T* dy = static_cast<const T*>(a.dy);
+  const T* dy2 = static_cast<const T*>(a.dy2);
   const T* x = static_cast<const T*>(a.x);
   const T* y = static_cast<const T*>(a.y);
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK>), dim3(g.gx, g.gy), dim3(kRed), sh_red, s, dy, x, y, a.M, a.C,
-                     g.TC, g.RPI, g.rows_per_block, a.workspace, a.tickets, a.p);
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK, ADD2>), dim3(g.gx, g.gy), dim3(kRed), sh_red, s, dy, dy2, x, y,
+                     a.M, a.C, g.TC, g.RPI, g.rows_per_block, a.workspace, a.tickets, a.p);
   PTDT_HIP_CHECK(hipGetLastError());
   const int64_t nvec = a.M * a.C / V;
   const size_t sh_ap = (size_t)(MASK == 2 ? 5 : 3) * a.C * sizeof(float);
   T* dx = static_cast<T*>(a.dx);
   T* dr = static_cast<T*>(a.dres);
   const dim3 grid(apply_grid(nvec)), blk(kThreads);
-  if (dr) hipLaunchKernelGGL((bn_bwd_apply_kernel<T, MASK, true>), grid, blk, sh_ap, s, dy, x, y, dx, dr, a.p, nvec, a.C);
-  else hipLaunchKernelGGL((bn_bwd_apply_kernel<T, MASK, false>), grid, blk, sh_ap, s, dy, x, y, dx, dr, a.p, nvec, a.C);
+  if (dr)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, MASK, true, ADD2>), grid, blk, sh_ap, s, dy, dy2, x, y, dx, dr, a.p,
+                       nvec, a.C);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, MASK, false, ADD2>), grid, blk, sh_ap, s, dy, dy2, x, y, dx, dr, a.p,
+                       nvec, a.C);
   return hipGetLastError();
+}
+
+template <typename T, int MASK>
+hipError_t bwd_launch2(const BnBwdArgs& a, const Geom& g, hipStream_t s) {
+  return a.dy2 != nullptr ? bwd_launch<T, MASK, true>(a, g, s) : bwd_launch<T, MASK, false>(a, g, s);
 }
 
 template <typename T>
@@ -515,10 +549,10 @@ hipError_t bwd_impl(const BnBwdArgs& a, hipStream_t s) {
   constexpr int V = VecIO<T>::V;
   if (a.C % V != 0) return hipErrorInvalidValue;
   const Geom g = geom<T>(a.M, a.C);
-  if (!a.relu) return bwd_launch<T, 0>(a, g, s);
-  if (a.y != nullptr) return bwd_launch<T, 1>(a, g, s);
+  if (!a.relu) return bwd_launch2<T, 0>(a, g, s);
+  if (a.y != nullptr) return bwd_launch2<T, 1>(a, g, s);
   if (a.p.scale == nullptr || a.p.shift == nullptr) return hipErrorInvalidValue;
-  return bwd_launch<T, 2>(a, g, s);
+  return bwd_launch2<T, 2>(a, g, s);
 }
 
 }  // namespace

@@ -309,6 +309,7 @@ struct BnBwdParams {
 };
 struct BnBwdArgs {
   const void* dy; const void* x; const void* y;  // y: forward output (ReLU mask) or null: mask from x
+  const void* dy2;                               // optional second gradient addend (dy + dy2), or null
   void* dx; void* dres;                          // dres (may be null): gradient of the residual = masked dy
   int dtype; int64_t M; int C; int relu;
   float* workspace; int* tickets;

@@ -3,29 +3,29 @@
 //
 // The toy MLP of BASELINE.json's north star (Linear(20,64)-ReLU-Linear(64,10),
 // CE, SGD; per-device batch 32 as in ddp_gpus.py:34-39) is ~143K MACs per step:
-// a latency problem, not a throughput one. Round 1's workgroup engine ran the
-// step as LDS-staged phases separated by workgroup barriers (~15K cycles per
-// step, MFMA ~2K of it). Here each of NW = H/16 waves owns 16 hidden units --
-// its slice of W1, b1 and the matching columns of W2, master copies + momentum
-// in its own LDS region / registers -- and runs its whole slice of the step
-// with v_mfma_f32_16x16x4_f32 (exact fp32, 32 cycles per SIMD):
+// a latency problem, not a throughput one. Each of NW = H/16 waves owns 16 hidden
+// units -- its rows of W1 (b1 folded in as input column Din against a constant-1
+// input), the matching columns of W2, their momenta -- and runs its slice of the
+// step with v_mfma_f32_16x16x4_f32 (exact fp32). Layouts are chosen so that every
+// product's result is the next product's operand or lands on the weights it
+// updates, lane for lane (D layout: lane (c = l&15, q = l>>4) holds [m = 4q+i][n = c]):
 //
-//   fwd1  HT[j][r]   = W1[j][:] . X[r][:]           (K = Din,  A: LDS W1, B: X rows)
-//   fwd2  ZT_w[c][r] = W2[c][slice] . HT[slice][r]   (K = the wave's 16 units; the
-//         MFMA D layout of HT (m on lane>>4, reg) IS the B operand with the K steps
-//         permuted to k = 4*(lane>>4) + s: no data movement)
+//   fwd1  HT[unit][row]  = W1aug . Xaug^T     A: w1r regs (unit c, input 4q+s), B: X rows (LDS)
+//   fwd2  ZT_w[cls][row] = W2[:, slice] . HT  B = HT's result layout (K permuted to unit 4q+s)
 //   ----  ONE workgroup barrier per step: the NW partial logits meet in LDS and
 //         every wave sums them in wave order (identical bits in every wave)
-//   loss  softmax / CE / MSE on the D layout: classes across the 4 lane groups
-//         (permlane16/32 swaps), rows across the 16 lanes; every wave computes it
-//   dHT   = W2[:, slice]^T . dZT                     (K = classes, same trick)
-//   dW2, dW1^T need K = rows: HT, dZT, dHT go through a wave-private LDS
-//         transpose (no barrier: one wave's LDS ops complete in order)
-//   SGD   on the wave's slice (W1/W2 in LDS, biases in registers)
+//   loss  softmax / CE / MSE on the result layout (classes across lane groups:
+//         permlane16/32 swaps; rows across the 16 lanes), in every wave
+//   dH[row][unit] = dZ . W2[:, slice]         A = dZ's result layout, B = w2t regs
+//   dW2[cls][unit] = dZ^T . H                 lands on w2t (W2[cls 4q+i][unit c])
+//   dW1aug^T[in][unit] = Xaug^T . dH          B = dH's result layout; lands on w1r
+//   SGD   in registers (padded inputs/classes have zero weights and gradients);
+//         W2 is mirrored to a wave-private LDS tile in the forward's layout
 //
-// so a step is ~50 MFMAs per wave on 4 SIMDs in parallel plus one barrier,
-// instead of phase-by-phase work over shared LDS. Batches are gathered from the
-// device-resident dataset one step ahead straight into MFMA operand registers.
+// H^T and dZ^T go through wave-private LDS tiles for the two transposed operands
+// of dW2 (no barrier: one wave's LDS ops complete in order). The next position's
+// batch is staged into LDS by all threads during each step (loads issued at the
+// top, written before the barrier; three slots), so operands are b128 LDS reads.
 // Sampler lists live in LDS (three epoch slots); the entries of each future
 // position are produced S+1 steps ahead of their use, C = min(8, S) positions at a
 // time by all threads, so epoch transitions cost nothing. With an all-reduce (world > 1) every lane
@@ -60,7 +60,7 @@ __device__ __forceinline__ float rows4_max(float v) {
 }
 
 struct TpDims {
-  int B, Din, H, Dout, NW, KS1, ld1, ld2, ldT, estride;
+  int B, Din, H, Dout, NW, estride;
   int oW1, ob1, oW2, ob2, np;
 };
 
@@ -68,10 +68,6 @@ __device__ __forceinline__ TpDims tp_dims(const FusedMlpArgs& a, const PersistAr
   TpDims d;
   d.B = a.B; d.Din = a.Din; d.H = a.H; d.Dout = a.Dout;
   d.NW = a.H / 16;
-  d.KS1 = (a.Din + 3) / 4;
-  d.ld1 = 4 * d.KS1 + 1;  // W1 slice row stride (units x padded inputs)
-  d.ld2 = 17;             // W2 slice row stride (classes x 16 units)
-  d.ldT = 33;             // transpose tiles: 16 x 32 rows
   d.estride = al4(pa.num_samples);
   const int hb = a.has_bias != 0;
   d.oW1 = 0;
@@ -80,11 +76,6 @@ __device__ __forceinline__ TpDims tp_dims(const FusedMlpArgs& a, const PersistAr
   d.ob2 = d.oW2 + a.Dout * a.H;
   d.np = d.ob2 + (hb ? a.Dout : 0);
   return d;
-}
-
-// floats of LDS per wave: W1, M1 (16 x ld1), W2, M2 (16 x ld2), 3 transpose tiles (16 x ldT)
-__host__ __device__ __forceinline__ int tp_wave_floats(int KS1) {
-  return 2 * 16 * (4 * KS1 + 1) + 2 * 16 * 17 + 3 * 16 * 33;
 }
 
 __device__ __forceinline__ float sgd1(float& w, float& m, float g, bool first, float lr, float mu, float damp, float wd,
@@ -161,30 +152,34 @@ __device__ __forceinline__ bool tp_allreduce(const XgmiArgs& x, uint32_t seq, fl
   return ok;
 }
 
-// One batch in MFMA operand registers.
+// LDS floats of one staged batch slot: X rows [32][ldx], X^T [16 MT][ldxt], targets [32][16]
 template <int MT>
-struct TpBatch {
-  float xb[2][8];   // fwd1 B operand (first KS used): X[row 16t + c][in 4s + q] (0 for in >= Din)
-  float xa[MT][8];  // dW1^T A operand: X[row 4s + q][in 16mt + c] (0 for in >= Din)
-  float yf[2][4];   // soft / MSE targets (row 16t + c, class 4q + i)
-  int yi[2];        // class labels of rows 16t + c
-  int nb;           // valid rows of this batch
+struct TpStage {
+  static constexpr int LDX = 16 * MT + 4;  // b128 reads of 4 consecutive inputs
+  static constexpr int LDXT = 36;          // b128 reads of 4 consecutive rows
+  static constexpr int XT_OFF = 32 * LDX;
+  static constexpr int Y_OFF = XT_OFF + 16 * MT * LDXT;
+  static constexpr int FLOATS = Y_OFF + 32 * 16;
 };
+constexpr int kTpLD2 = 20;  // W2 slice (classes x 16 units), b128 rows
+constexpr int kTpLDT = 36;  // per-wave transposes: 16 (class / unit) x 32 rows
+__host__ __device__ __forceinline__ int tp_wave_floats() { return 16 * kTpLD2 + 2 * 16 * kTpLDT; }
+__host__ __device__ __forceinline__ int tp_stage_floats(int MT) { return 32 * (16 * MT + 4) + 16 * MT * 36 + 32 * 16; }
 
-// KS: fwd1 K steps (4 inputs each; Din <= 4 KS, padded with zeros), MT = input tiles of dW1^T
-template <int KS, int LOSS, bool AR>
+// MT: 16-input tiles of the augmented input (Din inputs + a constant-1 column carrying b1)
+template <int MT, int LOSS, bool AR>
 __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, PersistArgs pa) {
   // No implicit FMA contraction: the compiler may contract differently in a peeled
   // first iteration than in the loop body, which made a run split into several
   // launches differ in the last bit from one long launch. Fused ops are explicit
   // (fmaf in sgd1, MFMA).
 #pragma clang fp contract(off)
-  constexpr int MT = KS > 4 ? 2 : 1;
-  constexpr int LD1 = 4 * KS + 1;  // W1 slice row stride (units x padded inputs)
-  constexpr int LD2 = 17, LDT = 33;
+  using St = TpStage<MT>;
+  constexpr int LDX = St::LDX, LDXT = St::LDXT, LD2 = kTpLD2, LDT = kTpLDT;
   extern __shared__ float lds[];
   const TpDims d = tp_dims(a, pa);
   const int tid = (int)threadIdx.x;
+  const int T = (int)blockDim.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l = tid & 63, c = l & 15, q = l >> 4;
   const int B = d.B, Din = d.Din, H = d.H, Dout = d.Dout, NW = d.NW;
@@ -197,41 +192,50 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   // [3][estride] epoch lists: a producer one epoch ahead never overwrites a list a
   // lagging wave may still read (position P's and P+1's epochs)
   int* const elist = reinterpret_cast<int*>(lds);
-  float* const xbuf = lds + 3 * d.estride;                           // [2][NW][64][8] partial logits
-  float* const wbase = xbuf + 2 * NW * 64 * 8 + tp_wave_floats(KS) * w;
-  float* const W1m = wbase;                      // [16][ld1] this wave's W1 rows (units 16w..16w+15)
-  float* const M1m = W1m + 16 * LD1;
-  float* const W2m = M1m + 16 * LD1;           // [16 classes][ld2] columns 16w..16w+15 of W2
-  float* const M2m = W2m + 16 * LD2;
-  float* const Tdz = M2m + 16 * LD2;           // [16][ldT] transposes: dZT, HT, dHT (class/unit x row)
-  float* const Th = Tdz + 16 * LDT;
-  float* const Tdh = Th + 16 * LDT;
+  float* const stage0 = lds + 3 * d.estride;                 // [3] staged batches (TpStage)
+  float* const xbuf = stage0 + 3 * St::FLOATS;               // [2][NW][64][8] partial logits
+  float* const wbase = xbuf + 2 * NW * 64 * 8 + tp_wave_floats() * w;
+  float* const W2m = wbase;                                   // [16 classes][LD2] W2[:, slice] (fwd layout)
+  float* const Th = W2m + 16 * LD2;                           // [16 units][LDT] H^T of this slice
+  float* const Tdz = Th + 16 * LDT;                           // [16 classes][LDT] dZ^T
   auto list = [&](int e) { return elist + (e % 3) * d.estride; };
+  auto stage = [&](int slot) { return stage0 + slot * St::FLOATS; };
 
   // ---- sampler lists: epoch e0 whole, epoch e0+1 up to batch j0 (entries of later
   // positions are produced S+1 steps ahead inside the loop)
   const int ns = pa.num_samples;
   const int S = (ns + B - 1) / B;
   const int e0 = pa.cursor[0], j0 = pa.cursor[1];
-  const int64_t pos0 = (int64_t)e0 * S + j0;
   const int n = pa.n_steps;
+  const uint32_t Nn = (uint32_t)pa.N;
   const ListCache lc{pa.lcache, pa.ltag, d.estride};
-  rank_epoch_indices_or(given_list(pa, e0), list(e0), (uint32_t)pa.N, pa.W, pa.rank, ns, pa.seed, e0, pa.shuffle, tid,
-                        (int)blockDim.x, lc);
+  // rank position of list entry i: (rank + W i) mod N without a 64-bit remainder
+  auto rank_pos = [&](int i) {
+    uint32_t pos = (uint32_t)pa.rank + (uint32_t)pa.W * (uint32_t)i;
+    while (pos >= Nn) pos -= Nn;
+    return pos;
+  };
+  rank_epoch_indices_or(given_list(pa, e0), list(e0), Nn, pa.W, pa.rank, ns, pa.seed, e0, pa.shuffle, tid, T, lc);
   {
     const int upto = min((j0 + 1) * B, ns);
     const int32_t* g1 = given_list(pa, e0 + 1);
     FeistelPerm fp;
-    fp.init(pa.seed, e0 + 1, (uint32_t)pa.N);
-    const uint32_t step_w = (uint32_t)pa.W;
-    for (int i = tid; i < ns; i += (int)blockDim.x) {
+    fp.init(pa.seed, e0 + 1, Nn);
+    for (int i = tid; i < ns; i += T) {
       int v = 0;  // zero-filled beyond: stale prefetches past the launch read valid rows
-      if (i < upto) {
-        const uint32_t pos = (uint32_t)(((uint64_t)pa.rank + (uint64_t)step_w * (uint64_t)i) % (uint32_t)pa.N);
-        v = g1 ? g1[i] : (int)(pa.shuffle ? fp(pos) : pos);
-      }
+      if (i < upto) v = g1 ? g1[i] : (int)(pa.shuffle ? fp(rank_pos(i)) : rank_pos(i));
       list(e0 + 1)[i] = v;
     }
+  }
+  // staged batch slots: zeros, and the constant-1 input column (b1 rides in W1's
+  // column Din) in X and X^T; the per-step writes only touch columns < Din
+  const float one = hb ? 1.f : 0.f;
+  for (int e = tid; e < 3 * St::FLOATS; e += T) {
+    const int o = e % St::FLOATS;
+    float v = 0.f;
+    if (o < St::XT_OFF) v = (o % LDX) == Din ? one : 0.f;
+    else if (o < St::Y_OFF) v = ((o - St::XT_OFF) / LDXT == Din && (o - St::XT_OFF) % LDXT < 32) ? one : 0.f;
+    stage0[e] = v;
   }
   __syncthreads();
   if (tid == 0 && pa.idx == nullptr) list_cache_publish(lc, e0);
@@ -244,7 +248,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   // the epochs still read (positions P and P+1).
   const int C = min(8, S);
   auto produce = [&](int te, int tj) {  // positions (te, tj) .. + C - 1
-    for (int idx = tid; idx < C * B; idx += (int)blockDim.x) {
+    for (int idx = tid; idx < C * B; idx += T) {
       const int o = idx / B, r = idx - o * B;
       int J = tj + o, E = te;
       if (J >= S) {
@@ -256,102 +260,117 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       int v;
       if (pa.idx != nullptr) {
         v = given_list(pa, E)[i];
+      } else if (pa.shuffle) {
+        FeistelPerm fp;
+        fp.init(pa.seed, E, Nn);
+        v = (int)fp(rank_pos(i));
       } else {
-        const uint32_t pos = (uint32_t)(((uint64_t)pa.rank + (uint64_t)pa.W * (uint64_t)i) % (uint32_t)pa.N);
-        if (pa.shuffle) {
-          FeistelPerm fp;
-          fp.init(pa.seed, E, (uint32_t)pa.N);
-          v = (int)fp(pos);
-        } else {
-          v = (int)pos;
-        }
+        v = (int)rank_pos(i);
       }
       list(E)[i] = v;
     }
   };
 
-  // ---- resident state
+  // ---- batch staging: thread (row = tid & 31, column group tid >> 5) loads its row's
+  // columns g, g + G, ... of the next position's batch into registers at the top of a
+  // step and writes them to the next LDS slot before the step's barrier, so every
+  // wave's operands are LDS reads (X rows, X^T rows, targets) instead of per-lane
+  // gathers, and the global latency hides under the step's MFMAs.
+  constexpr int JX = 16, JY = 8;  // per-thread column slots (Din <= 32, Dout <= 16, >= 2 groups)
+  const int srow = tid & 31, sgrp = tid >> 5, G = T >> 5;
+  const auto X = gptr(a.X);
+  const int ldx = a.ldx > 0 ? a.ldx : Din;
+  const int jx = (Din - sgrp + G - 1) / G;
+  const int jy = LOSS == kLossCEIndex ? (sgrp == 0 ? 1 : 0) : (Dout - sgrp + G - 1) / G;
+  float xv[JX], yv[JY];
+  int yiv = 0;
+  auto stage_issue = [&](int E, int J) {
+    if (srow >= B) return;
+    const int nb = min(B, ns - J * B);
+    const int sel = list(E)[J * B + min(srow, nb - 1)];
+    const auto xr = X + (int64_t)sel * ldx + sgrp;
+#pragma unroll
+    for (int j = 0; j < JX; ++j)
+      if (j < jx) xv[j] = xr[j * G];
+    if constexpr (LOSS == kLossCEIndex) {
+      if (jy) yiv = (int)gptr(a.Yi)[sel];
+    } else {
+      const auto yr = gptr(a.Yf) + (int64_t)sel * Dout + sgrp;
+#pragma unroll
+      for (int j = 0; j < JY; ++j)
+        if (j < jy) yv[j] = yr[j * G];
+    }
+  };
+  auto stage_write = [&](int slot) {
+    if (srow >= B) return;
+    float* const st = stage(slot);
+#pragma unroll
+    for (int j = 0; j < JX; ++j) {
+      if (j < jx) {
+        const int col = sgrp + j * G;
+        st[srow * LDX + col] = xv[j];
+        st[St::XT_OFF + col * LDXT + srow] = xv[j];
+      }
+    }
+    if constexpr (LOSS == kLossCEIndex) {
+      if (jy) reinterpret_cast<int*>(st + St::Y_OFF)[srow] = yiv;
+    } else {
+#pragma unroll
+      for (int j = 0; j < JY; ++j)
+        if (j < jy) st[St::Y_OFF + srow * 16 + sgrp + j * G] = yv[j];
+    }
+  };
+
+  // ---- resident state: this wave's W1 rows (b1 as column Din) and W2 columns in
+  // MFMA result layouts, so the gradients land on them lane for lane and SGD runs
+  // in registers:
+  //   w1r[mt][i] = W1aug[unit 16w + c][input 16 mt + 4q + i]   (= dW1^T's layout)
+  //   w2t[i]     = W2[class 4q + i][unit 16w + c]              (= dW2's layout)
   const auto P = gptr(a.P);
-  for (int e = l; e < 16 * LD1; e += 64) {
-    const int j = e / LD1, in = e - j * LD1;
-    const bool real = in < Din;
-    W1m[e] = real ? P[d.oW1 + (16 * w + j) * Din + in] : 0.f;
-    M1m[e] = (real && use_mom) ? a.mom[d.oW1 + (16 * w + j) * Din + in] : 0.f;
+  float w1r[MT][4], m1r[MT][4], w2t[4], m2t[4], b2r[4], mb2r[4];
+  const int unit = 16 * w + c;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int in = 16 * mt + 4 * q + i;
+      const int off = in < Din ? d.oW1 + unit * Din + in : (hb && in == Din ? d.ob1 + unit : -1);
+      w1r[mt][i] = off >= 0 ? P[off] : 0.f;
+      m1r[mt][i] = (off >= 0 && use_mom) ? a.mom[off] : 0.f;
+    }
   }
-  for (int e = l; e < 16 * LD2; e += 64) {
-    const int cls = e / LD2, j = e - cls * LD2;
-    const bool real = cls < Dout && j < 16;
-    W2m[e] = real ? P[d.oW2 + cls * H + 16 * w + j] : 0.f;
-    M2m[e] = (real && use_mom) ? a.mom[d.oW2 + cls * H + 16 * w + j] : 0.f;
-  }
-  float b1r[4], mb1r[4], b2r[4], mb2r[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int u = 16 * w + 4 * q + i, cls = 4 * q + i;
-    b1r[i] = hb ? P[d.ob1 + u] : 0.f;
-    mb1r[i] = (hb && use_mom) ? a.mom[d.ob1 + u] : 0.f;
-    b2r[i] = (hb && cls < Dout) ? P[d.ob2 + cls] : 0.f;
-    mb2r[i] = (hb && use_mom && cls < Dout) ? a.mom[d.ob2 + cls] : 0.f;
+    const int cls = 4 * q + i;
+    const bool real = cls < Dout;
+    w2t[i] = real ? P[d.oW2 + cls * H + unit] : 0.f;
+    m2t[i] = (real && use_mom) ? a.mom[d.oW2 + cls * H + unit] : 0.f;
+    b2r[i] = (hb && real) ? P[d.ob2 + cls] : 0.f;
+    mb2r[i] = (hb && real && use_mom) ? a.mom[d.ob2 + cls] : 0.f;
+    W2m[cls * LD2 + c] = w2t[i];  // forward layout copy: W2[class c][unit 4q + s] at c*LD2 + 4q + s
   }
   int opt_step = a.opt_step ? *a.opt_step : 0;
   uint32_t seq = AR ? *a.ar.seq : 0u;
   bool failed = AR && *a.ar.err != 0;
 
-  // ---- batch fetch (next position's rows, straight into operand registers)
-  const auto X = gptr(a.X);
-  const int ldx = a.ldx > 0 ? a.ldx : Din;
-  auto fetch = [&](TpBatch<MT>& f, int E, int J) {
-    const int nb = min(B, ns - J * B);
-    f.nb = nb;
-    const int* li = list(E) + J * B;
-    // unconditional loads (clamped indices) + selects: no per-element branches
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int sel = li[min(16 * t + c, nb - 1)];
-      const auto xr = X + (int64_t)sel * ldx;
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        const int in = 4 * s + q;
-        const float v = xr[min(in, Din - 1)];
-        f.xb[t][s] = in < Din ? v : 0.f;
-      }
-      if constexpr (LOSS == kLossCEIndex) {
-        f.yi[t] = (int)gptr(a.Yi)[sel];
-      } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int cls = 4 * q + i;
-          const float v = gptr(a.Yf)[(int64_t)sel * Dout + min(cls, Dout - 1)];
-          f.yf[t][i] = cls < Dout ? v : 0.f;
-        }
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int sel = li[min(4 * s + q, nb - 1)];
-      const auto xr = X + (int64_t)sel * ldx;
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int in = 16 * mt + c;
-        const float v = xr[min(in, Din - 1)];
-        f.xa[mt][s] = in < Din ? v : 0.f;
-      }
-    }
-  };
+  // position of step 0 staged synchronously
+  stage_issue(e0, j0);
+  stage_write(0);
+  __syncthreads();
 
   float* const losses = pa.losses;
   // last step's (averaged) gradients, written to the DDP bucket at the end
-  float lg1[MT][4], lg2[4], ldb1[4], ldb2[4];
+  float lg1[MT][4], lg2[4], ldb2[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    lg2[i] = ldb1[i] = ldb2[i] = 0.f;
+    lg2[i] = ldb2[i] = 0.f;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) lg1[mt][i] = 0.f;
   }
 
-  TpBatch<MT> cur, nxt;
-  fetch(cur, e0, j0);
   int ce = e0, cj = j0;  // current position (epoch, step in epoch): no divisions in the loop
+  int sc = 0;            // LDS slot of the current batch
+  int pc = 0;            // steps until the next production chunk
   const bool stamps = pa.stamps != nullptr && tid == 0;
   int64_t tmark = stamps ? (int64_t)__builtin_amdgcn_s_memtime() : 0;
   int64_t acc_t[6] = {0, 0, 0, 0, 0, 0};
@@ -367,71 +386,86 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     const int par = k & 1;
     const bool wrap = cj + 1 == S;
     const int ne = wrap ? ce + 1 : ce, nj = wrap ? 0 : cj + 1;
-    fetch(nxt, ne, nj);  // stale-but-valid past the launch
-    if (k % C == 0) produce(wrap ? ce + 2 : ce + 1, wrap ? 0 : cj + 1);
+    const int sn = sc == 2 ? 0 : sc + 1;
+    const int nb = min(B, ns - cj * B);
+    stage_issue(ne, nj);  // stale-but-valid past the launch
+    if (pc == 0) {
+      produce(wrap ? ce + 2 : ce + 1, wrap ? 0 : cj + 1);
+      pc = C;
+    }
+    --pc;
     tick(0);
-    const int nb = cur.nb;
+    const float* const st = stage(sc);
 
-    // ---------------- fwd1: HT = W1 . X^T (this wave's 16 units x 32 rows)
+    // ---------------- fwd1: HT = W1aug . Xaug^T (this wave's 16 units x 32 rows), ReLU
     f4 h[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const float aw = W1m[c * LD1 + 4 * s + q];
-      h[0] = mfma4(aw, cur.xb[0][s], h[0]);
-      h[1] = mfma4(aw, cur.xb[1][s], h[1]);
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const f4 xb = *reinterpret_cast<const f4*>(st + (16 * t + c) * LDX + 16 * mt + 4 * q);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) h[t] = mfma4(w1r[mt][s], xb[s], h[t]);
+      }
     }
     float ht[2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ht[t][i] = fmaxf(h[t][i] + b1r[i], 0.f);
+      for (int i = 0; i < 4; ++i) ht[t][i] = fmaxf(h[t][i], 0.f);
 
     // ---------------- fwd2 partial: ZT_w = W2[:, slice] . HT (K steps permuted: unit 4q + s)
+    const f4 a2 = *reinterpret_cast<const f4*>(W2m + c * LD2 + 4 * q);
     f4 z[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const float a2 = W2m[c * LD2 + 4 * q + s];
-      z[0] = mfma4(a2, ht[0][s], z[0]);
-      z[1] = mfma4(a2, ht[1][s], z[1]);
+      z[0] = mfma4(a2[s], ht[0][s], z[0]);
+      z[1] = mfma4(a2[s], ht[1][s], z[1]);
     }
     {
-      float4* dst = reinterpret_cast<float4*>(xbuf + ((par * NW + w) * 64 + l) * 8);
-      dst[0] = make_float4(z[0][0], z[0][1], z[0][2], z[0][3]);
-      dst[1] = make_float4(z[1][0], z[1][1], z[1][2], z[1][3]);
+      f4* dst = reinterpret_cast<f4*>(xbuf + ((par * NW + w) * 64 + l) * 8);
+      dst[0] = z[0];
+      dst[1] = z[1];
     }
-    // the transposes of HT can go out while the other waves catch up
+    // H^T of the slice for the backward's transposed reads (wave-private)
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) Th[(4 * q + i) * LDT + 16 * t + c] = ht[t][i];
+    stage_write(sn);
     tick(1);
     __syncthreads();
     float zf[2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) zf[t][i] = 0.f;
+      for (int i = 0; i < 4; ++i) zf[t][i] = b2r[i];
     for (int v = 0; v < NW; ++v) {  // wave order: identical sums in every wave
-      const float4* src = reinterpret_cast<const float4*>(xbuf + ((par * NW + v) * 64 + l) * 8);
-      const float4 p0 = src[0], p1 = src[1];
-      zf[0][0] += p0.x; zf[0][1] += p0.y; zf[0][2] += p0.z; zf[0][3] += p0.w;
-      zf[1][0] += p1.x; zf[1][1] += p1.y; zf[1][2] += p1.z; zf[1][3] += p1.w;
+      const f4* src = reinterpret_cast<const f4*>(xbuf + ((par * NW + v) * 64 + l) * 8);
+      const f4 p0 = src[0], p1 = src[1];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        zf[0][i] += p0[i];
+        zf[1][i] += p1[i];
+      }
     }
-
     tick(2);
+
     // ---------------- loss and dL/dZ (classes 4q + i across lane groups, rows 16t + c)
     float g[2][4];
-    float lsum = 0.f, cnt = 0.f;
+    float lsum = 0.f;
+    int cnt = 0;
+    const float* const ys = st + St::Y_OFF;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const bool rv = 16 * t + c < nb;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) zf[t][i] += b2r[i];
+      const int row = 16 * t + c;
+      const bool rv = row < nb;
       if constexpr (LOSS == kLossMSE) {
+        const f4 y = *reinterpret_cast<const f4*>(ys + row * 16 + 4 * q);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const bool ok = rv && 4 * q + i < Dout;
-          const float df = zf[t][i] - cur.yf[t][i];
+          const float df = zf[t][i] - y[i];
           lsum += ok ? df * df : 0.f;
           g[t][i] = ok ? 2.f * df : 0.f;
         }
@@ -440,8 +474,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 #pragma unroll
         for (int i = 0; i < 4; ++i) m = (4 * q + i < Dout) ? fmaxf(m, zf[t][i]) : m;
         m = rows4_max(m);
-        float se = 0.f;
-        float e[4];
+        float se = 0.f, e[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           e[i] = (4 * q + i < Dout) ? __expf(zf[t][i] - m) : 0.f;
@@ -450,7 +483,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         se = rows4_sum(se);
         const float lse = m + __builtin_amdgcn_logf(se) * 0.6931471805599453f;
         if constexpr (LOSS == kLossCEIndex) {
-          const int y = cur.yi[t];
+          const int y = reinterpret_cast<const int*>(ys)[row];
           const bool use = rv && y != a.ignore_index;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -459,34 +492,36 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
             g[t][i] = (use && cls < Dout) ? p - (cls == y ? 1.f : 0.f) : 0.f;
             lsum += (use && cls == y) ? lse - zf[t][i] : 0.f;
           }
-          cnt += (use && q == 0) ? 1.f : 0.f;
+          cnt += __popcll(__ballot(use && q == 0));
         } else {  // soft targets: -(t . log_softmax(z)), grad = softmax * sum(t) - t
+          const f4 y = *reinterpret_cast<const f4*>(ys + row * 16 + 4 * q);
           float ts = 0.f;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) ts += (4 * q + i < Dout) ? cur.yf[t][i] : 0.f;
+          for (int i = 0; i < 4; ++i) ts += y[i];  // classes >= Dout stage as 0
           ts = rows4_sum(ts);
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const bool ok = rv && 4 * q + i < Dout;
             const float ls = zf[t][i] - lse;
-            lsum += ok ? -cur.yf[t][i] * ls : 0.f;
-            g[t][i] = ok ? __expf(ls) * ts - cur.yf[t][i] : 0.f;
+            lsum += ok ? -y[i] * ls : 0.f;
+            g[t][i] = ok ? __expf(ls) * ts - y[i] : 0.f;
           }
         }
       }
     }
     float inv;
     if constexpr (LOSS == kLossCEIndex) {
-      cnt = wave_sum(cnt);
-      inv = 1.f / (cnt > 0.f ? cnt : 1.f);
+      cnt = __builtin_amdgcn_readfirstlane(cnt);
+      inv = 1.f / (float)(cnt > 0 ? cnt : 1);
     } else if constexpr (LOSS == kLossMSE) {
       inv = 1.f / (float)(nb * Dout);
     } else {
       inv = 1.f / (float)nb;
     }
-    lsum = wave_sum(lsum);
-    if (w == 0 && l == 0)
-      losses[k] = (LOSS == kLossCEIndex && !(cnt > 0.f)) ? NAN : lsum * inv;
+    if (w == 0) {  // the step's loss: one wave reduces and reports it
+      lsum = wave_sum(lsum);
+      if (l == 0) losses[k] = (LOSS == kLossCEIndex && cnt == 0) ? NAN : lsum * inv;
+    }
     float db2[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -498,46 +533,51 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) Tdz[(4 * q + i) * LDT + 16 * t + c] = g[t][i];
-
     tick(3);
-    // ---------------- dHT = W2[:, slice]^T . dZT (K steps permuted: class 4q + s), ReLU mask
+
+    // ---------------- dH = dZ . W2[:, slice]: dZ's result layout is the A operand
+    // (row c, class 4q + s) and w2t the B operand (class 4q + s, unit c); the result
+    // dH[row 16t + 4q + i][unit c] is dW1's B operand as it stands
     f4 dh[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const float a3 = W2m[(4 * q + s) * LD2 + c];
-      dh[0] = mfma4(a3, g[0][s], dh[0]);
-      dh[1] = mfma4(a3, g[1][s], dh[1]);
+      dh[0] = mfma4(g[0][s], w2t[s], dh[0]);
+      dh[1] = mfma4(g[1][s], w2t[s], dh[1]);
     }
-    float db1[4];
+    // transposed reads: H[row 16t + 4q + s][unit c] (ReLU mask, dW2's B) and
+    // dZ[row 16t + 4q + s][class c] (dW2's A)
+    f4 hT[2], dzT[2];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      dh[0][i] = ht[0][i] > 0.f ? dh[0][i] : 0.f;
-      dh[1][i] = ht[1][i] > 0.f ? dh[1][i] : 0.f;
-      db1[i] = group_sum<16>(dh[0][i]) + group_sum<16>(dh[1][i]);
+    for (int t = 0; t < 2; ++t) {
+      hT[t] = *reinterpret_cast<const f4*>(Th + c * LDT + 16 * t + 4 * q);
+      dzT[t] = *reinterpret_cast<const f4*>(Tdz + c * LDT + 16 * t + 4 * q);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) Tdh[(4 * q + i) * LDT + 16 * t + c] = dh[t][i];
+      for (int i = 0; i < 4; ++i) dh[t][i] = hT[t][i] > 0.f ? dh[t][i] : 0.f;
 
-    // ---------------- dW2 = dZT . H (K = rows), dW1^T = X^T . dH (K = rows)
+    // ---------------- dW2 = dZ^T . H (K = rows), dW1aug^T = Xaug^T . dH (K = rows)
     f4 gw2 = {0.f, 0.f, 0.f, 0.f};
     f4 gw1[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) gw1[mt] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int s = 0; s < 8; ++s) {
-      const int r = 4 * s + q;
-      const float adz = Tdz[c * LDT + r];
-      const float bh = Th[c * LDT + r];
-      const float bdh = Tdh[c * LDT + r];
-      gw2 = mfma4(adz, bh, gw2);
+    for (int t = 0; t < 2; ++t) {
+      f4 xa[MT];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) gw1[mt] = mfma4(cur.xa[mt][s], bdh, gw1[mt]);
+      for (int mt = 0; mt < MT; ++mt)
+        xa[mt] = *reinterpret_cast<const f4*>(st + St::XT_OFF + (16 * mt + c) * LDXT + 16 * t + 4 * q);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        gw2 = mfma4(dzT[t][s], hT[t][s], gw2);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) gw1[mt] = mfma4(xa[mt][s], dh[t][s], gw1[mt]);
+      }
     }
-
     tick(4);
-    // ---------------- all-reduce over ranks (xGMI LL), then SGD on the slice
+
+    // ---------------- all-reduce over ranks (xGMI LL), then SGD in registers
     float gv1[MT][4], gv2[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -548,7 +588,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     if constexpr (AR) {
       if (!failed) {
         seq += 1u;
-        constexpr int NV = 4 * MT + 12;
+        constexpr int NV = 4 * MT + 8;
         float v[NV];
         int idx[NV];
         bool push[NV], need[NV];
@@ -557,23 +597,19 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             const int in = 16 * mt + 4 * q + i;
-            const bool ok = in < Din;
+            const int off = in < Din ? d.oW1 + unit * Din + in : (hb && in == Din ? d.ob1 + unit : -1);
             v[mt * 4 + i] = gv1[mt][i];
-            idx[mt * 4 + i] = ok ? d.oW1 + (16 * w + c) * Din + in : 0;
-            push[mt * 4 + i] = need[mt * 4 + i] = ok;
+            idx[mt * 4 + i] = off >= 0 ? off : 0;
+            push[mt * 4 + i] = need[mt * 4 + i] = off >= 0;
           }
           const int cls = 4 * q + i;
           v[4 * MT + i] = gv2[i];
-          idx[4 * MT + i] = cls < Dout ? d.oW2 + cls * H + 16 * w + c : 0;
+          idx[4 * MT + i] = cls < Dout ? d.oW2 + cls * H + unit : 0;
           push[4 * MT + i] = need[4 * MT + i] = cls < Dout;
-          v[4 * MT + 4 + i] = db1[i];
-          idx[4 * MT + 4 + i] = hb ? d.ob1 + 16 * w + 4 * q + i : 0;
-          push[4 * MT + 4 + i] = hb && c == 0;
-          need[4 * MT + 4 + i] = hb;
-          v[4 * MT + 8 + i] = db2[i];
-          idx[4 * MT + 8 + i] = (hb && cls < Dout) ? d.ob2 + cls : 0;
-          push[4 * MT + 8 + i] = hb && cls < Dout && c == 0 && w == 0;
-          need[4 * MT + 8 + i] = hb && cls < Dout;
+          v[4 * MT + 4 + i] = db2[i];
+          idx[4 * MT + 4 + i] = (hb && cls < Dout) ? d.ob2 + cls : 0;
+          push[4 * MT + 4 + i] = hb && cls < Dout && c == 0 && w == 0;
+          need[4 * MT + 4 + i] = hb && cls < Dout;
         }
         failed = !tp_allreduce<NV>(a.ar, seq, v, idx, push, need);
 #pragma unroll
@@ -581,78 +617,55 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) gv1[mt][i] = v[mt * 4 + i];
           gv2[i] = v[4 * MT + i];
-          db1[i] = v[4 * MT + 4 + i];
-          db2[i] = v[4 * MT + 8 + i];
+          db2[i] = v[4 * MT + 4 + i];
         }
       }
     }
+    // padded inputs / classes have zero gradients and zero weights: no masks needed
     const bool first = opt_step == 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const int in = 16 * mt + 4 * q + i;
-        if (in < Din) {
-          const int e = c * LD1 + in;
-          float wv = W1m[e], mv = M1m[e];
-          sgd1(wv, mv, gv1[mt][i], first, lr, mu, damp, wd, nesterov, use_mom);
-          W1m[e] = wv;
-          M1m[e] = mv;
-        }
+        sgd1(w1r[mt][i], m1r[mt][i], gv1[mt][i], first, lr, mu, damp, wd, nesterov, use_mom);
         lg1[mt][i] = gv1[mt][i];
       }
-      const int cls = 4 * q + i;
-      if (cls < Dout) {
-        const int e = cls * LD2 + c;
-        float wv = W2m[e], mv = M2m[e];
-        sgd1(wv, mv, gv2[i], first, lr, mu, damp, wd, nesterov, use_mom);
-        W2m[e] = wv;
-        M2m[e] = mv;
-      }
-      if (hb) {
-        sgd1(b1r[i], mb1r[i], db1[i], first, lr, mu, damp, wd, nesterov, use_mom);
-        if (cls < Dout) sgd1(b2r[i], mb2r[i], db2[i], first, lr, mu, damp, wd, nesterov, use_mom);
-      }
+      sgd1(w2t[i], m2t[i], gv2[i], first, lr, mu, damp, wd, nesterov, use_mom);
+      W2m[(4 * q + i) * LD2 + c] = w2t[i];
+      if (hb) sgd1(b2r[i], mb2r[i], db2[i], first, lr, mu, damp, wd, nesterov, use_mom);
       lg2[i] = gv2[i];
-      ldb1[i] = db1[i];
       ldb2[i] = db2[i];
     }
     ++opt_step;
-    cur = nxt;
     ce = ne;
     cj = nj;
+    sc = sn;
     tick(5);
   }
 
   // ---- write back: parameters, momentum, the last step's averaged gradients (DDP bucket)
-  __syncthreads();
   float* const Pw = a.P;
   float* const Gw = a.G;
   const bool have = n > 0;
-  for (int e = l; e < 16 * Din; e += 64) {
-    const int j = e / Din, in = e - j * Din;
-    Pw[d.oW1 + (16 * w + j) * Din + in] = W1m[j * LD1 + in];
-    if (use_mom) a.mom[d.oW1 + (16 * w + j) * Din + in] = M1m[j * LD1 + in];
-  }
-  for (int e = l; e < Dout * 16; e += 64) {
-    const int cls = e / 16, j = e - cls * 16;
-    Pw[d.oW2 + cls * H + 16 * w + j] = W2m[cls * LD2 + j];
-    if (use_mom) a.mom[d.oW2 + cls * H + 16 * w + j] = M2m[cls * LD2 + j];
-  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int cls = 4 * q + i;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int in = 16 * mt + 4 * q + i;
-      if (have && in < Din) Gw[d.oW1 + (16 * w + c) * Din + in] = lg1[mt][i];
+      const int off = in < Din ? d.oW1 + unit * Din + in : (hb && in == Din ? d.ob1 + unit : -1);
+      if (off >= 0) {
+        Pw[off] = w1r[mt][i];
+        if (use_mom) a.mom[off] = m1r[mt][i];
+        if (have) Gw[off] = lg1[mt][i];
+      }
     }
-    if (have && cls < Dout) Gw[d.oW2 + cls * H + 16 * w + c] = lg2[i];
-    if (hb && c == 0) {
-      Pw[d.ob1 + 16 * w + 4 * q + i] = b1r[i];
-      if (use_mom) a.mom[d.ob1 + 16 * w + 4 * q + i] = mb1r[i];
-      if (have) Gw[d.ob1 + 16 * w + 4 * q + i] = ldb1[i];
-      if (w == 0 && cls < Dout) {
+    const int cls = 4 * q + i;
+    if (cls < Dout) {
+      const int off = d.oW2 + cls * H + unit;
+      Pw[off] = w2t[i];
+      if (use_mom) a.mom[off] = m2t[i];
+      if (have) Gw[off] = lg2[i];
+      if (hb && c == 0 && w == 0) {
         Pw[d.ob2 + cls] = b2r[i];
         if (use_mom) a.mom[d.ob2 + cls] = mb2r[i];
         if (have) Gw[d.ob2 + cls] = ldb2[i];
@@ -662,7 +675,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   if (tid == 0) {
     pa.cursor[0] = ce;
     pa.cursor[1] = cj;
-    if (stamps) {  // [0] fetch+produce [1] fwd [2] barrier+sum [3] loss [4] bwd MFMA [5] all-reduce+SGD
+    if (stamps) {  // [0] stage issue+produce [1] fwd [2] barrier+sum [3] loss [4] bwd MFMA [5] all-reduce+SGD
       for (int k = 0; k < 6; ++k) pa.stamps[k] += acc_t[k];
       pa.stamps[7] += (int64_t)__builtin_amdgcn_s_memtime() - t_begin;
       pa.stamps[8] += (int64_t)__builtin_amdgcn_s_memrealtime() - r_begin;
@@ -672,30 +685,26 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   }
 }
 
-int tp_ks(int Din) { return Din <= 8 ? 2 : Din <= 16 ? 4 : Din <= 20 ? 5 : 8; }
+int tp_mt(const FusedMlpArgs& a) { return a.Din + (a.has_bias ? 1 : 0) <= 16 ? 1 : 2; }
 
 template <int LOSS, bool AR>
-const void* pick_ks(int ks) {
-  switch (ks) {
-    case 2: return (const void*)mlp_tp_kernel<2, LOSS, AR>;
-    case 4: return (const void*)mlp_tp_kernel<4, LOSS, AR>;
-    case 5: return (const void*)mlp_tp_kernel<5, LOSS, AR>;
-    default: return (const void*)mlp_tp_kernel<8, LOSS, AR>;
-  }
+const void* pick_mt(int mt) {
+  return mt == 1 ? (const void*)mlp_tp_kernel<1, LOSS, AR> : (const void*)mlp_tp_kernel<2, LOSS, AR>;
 }
 
 template <bool AR>
-const void* pick_loss_tp(int loss, int ks) {
+const void* pick_loss_tp(int loss, int mt) {
   switch (loss) {
-    case kLossCEIndex: return pick_ks<kLossCEIndex, AR>(ks);
-    case kLossMSE: return pick_ks<kLossMSE, AR>(ks);
-    default: return pick_ks<kLossCESoft, AR>(ks);
+    case kLossCEIndex: return pick_mt<kLossCEIndex, AR>(mt);
+    case kLossMSE: return pick_mt<kLossMSE, AR>(mt);
+    default: return pick_mt<kLossCESoft, AR>(mt);
   }
 }
 
 size_t tp_lds_bytes(const FusedMlpArgs& a, const PersistArgs& p) {
   const int NW = a.H / 16;
-  const size_t fl = (size_t)3 * al4(p.num_samples) + (size_t)2 * NW * 64 * 8 + (size_t)NW * tp_wave_floats(tp_ks(a.Din));
+  const size_t fl = (size_t)3 * al4(p.num_samples) + (size_t)3 * tp_stage_floats(tp_mt(a)) +
+                    (size_t)2 * NW * 64 * 8 + (size_t)NW * tp_wave_floats();
   return fl * sizeof(float);
 }
 
@@ -703,7 +712,8 @@ size_t tp_lds_bytes(const FusedMlpArgs& a, const PersistArgs& p) {
 
 bool mlp_tp_supported(const FusedMlpArgs& a, const PersistArgs& p) {
   if (a.H < 16 || a.H > 64 || a.H % 16 != 0) return false;
-  if (a.B < 1 || a.B > 32 || a.Din < 1 || a.Din > 32 || a.Dout < 1 || a.Dout > 16) return false;
+  if (a.B < 1 || a.B > 32 || a.Din < 1 || a.Din + (a.has_bias ? 1 : 0) > 32 || a.Dout < 1 || a.Dout > 16)
+    return false;
   if (a.ar.world > kXgmiMaxRanks) return false;
   if (p.N <= 0 || p.num_samples <= 0) return false;
   return tp_lds_bytes(a, p) <= 160 * 1024;
@@ -711,8 +721,8 @@ bool mlp_tp_supported(const FusedMlpArgs& a, const PersistArgs& p) {
 
 hipError_t mlp_tp_prepare(const FusedMlpArgs& a, const PersistArgs& p, PersistLaunch* out) {
   if (!mlp_tp_supported(a, p)) return hipErrorInvalidValue;
-  const int ks = tp_ks(a.Din);
-  const void* fn = a.ar.world > 1 ? pick_loss_tp<true>(a.loss_kind, ks) : pick_loss_tp<false>(a.loss_kind, ks);
+  const int mt = tp_mt(a);
+  const void* fn = a.ar.world > 1 ? pick_loss_tp<true>(a.loss_kind, mt) : pick_loss_tp<false>(a.loss_kind, mt);
   const size_t lds = tp_lds_bytes(a, p);
   if (lds > 64 * 1024) PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   out->fn = fn;

@@ -25,10 +25,12 @@ from ..ops.linear import Linear
 from ..ops.norm import BatchNorm2d, MaxPool2d
 
 
-def bn_act(bn: nn.Module, x: torch.Tensor, residual: torch.Tensor | None = None, relu: bool = False):
-    """``ReLU?(bn(x) + residual)``: fused for ops.norm.BatchNorm2d, composed for any other norm layer."""
+def bn_act(bn: nn.Module, x: torch.Tensor, residual: torch.Tensor | None = None, relu: bool = False,
+           link: bool = False):
+    """``ReLU?(bn(x) + residual)``: fused for ops.norm.BatchNorm2d, composed for any other norm layer.
+    ``link``: the residual is an identity shortcut from another fused BN (ops.norm.ResidualLink)."""
     if isinstance(bn, BatchNorm2d):
-        return bn(x, residual, relu)
+        return bn(x, residual, relu, link)
     y = bn(x)
     if residual is not None:
         y = y + residual
@@ -66,7 +68,8 @@ class Bottleneck(nn.Module):
         identity = x if self.downsample is None else self.downsample(x)
         out = bn_act(self.bn1, self.conv1(x), relu=True)
         out = bn_act(self.bn2, self.conv2(out), relu=True)
-        return bn_act(self.bn3, self.conv3(out), residual=identity, relu=True)
+        # identity shortcut: the residual gradient goes straight into the producing BN's backward
+        return bn_act(self.bn3, self.conv3(out), residual=identity, relu=True, link=self.downsample is None)
 
 
 class ResNet(nn.Module):

@@ -41,16 +41,37 @@ def _like(t: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     return t.contiguous(memory_format=torch.channels_last) if x.dim() == 4 else t.contiguous()
 
 
+class ResidualLink:
+    """Hand-over of a residual gradient between two fused BNs (a ResNet identity
+    shortcut): the BN that adds ``residual`` (block k+1's bn3) stores the
+    residual's gradient here instead of returning it to autograd, and the BN that
+    produced ``residual`` (block k's bn3) adds it to its incoming gradient inside
+    its backward kernels -- replacing autograd's separate add of the two
+    gradients of the shared activation (two reads and a write of it).
+
+    Ordering is autograd's own: the producer's backward runs only after every
+    consumer of its output, the linking BN included, has run its backward."""
+
+    __slots__ = ("dres", "armed")
+
+    def __init__(self):
+        self.dres = None
+        self.armed = False
+
+
 class _BatchNormActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, relu: bool, momentum: float,
-                eps: float, tickets):
+                eps: float, tickets, link_in, link_out):
         y, stats = native().bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, residual, relu, momentum,
                                          eps, tickets)
         ctx.tickets = tickets
         ctx.params = (weight, bias)
         ctx.relu = relu
         ctx.has_res = residual is not None
+        ctx.link_in, ctx.link_out = link_in, link_out
+        if link_in is not None:
+            link_in.armed = True
         # ReLU mask in the backward: from y with a residual; without one it is recomputed
         # from x and the saved scale/shift (bit-exact), so y need not be read (or kept)
         ctx.save_for_backward(x, y if (relu and residual is not None) else None, weight, stats)
@@ -60,16 +81,27 @@ class _BatchNormActFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, y, weight, stats = ctx.saved_tensors
         want_dw = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
-        want_dres = ctx.has_res and ctx.needs_input_grad[3]
+        link_in, link_out = ctx.link_in, ctx.link_out
+        want_dres = ctx.has_res and (ctx.needs_input_grad[3] or link_in is not None)
+        dy = _like(dy, x)
+        dy2 = None
+        if link_out is not None and link_out.armed:  # a later block's residual gradient of our output
+            # (None: that block's backward did not run -- its output does not reach the loss)
+            dy2, link_out.dres, link_out.armed = link_out.dres, None, False
+            if dy2 is not None and dy2.stride() != dy.stride():
+                dy, dy2 = dy + dy2, None
         sinks = [None, None]
         if want_dw:  # DDP grad sinks (ops/conv.py): write dweight/dbias straight into the bucket slots
             for k, p in enumerate(ctx.params):
                 if p is not None and p.grad is None and getattr(p, "_ptdt_grad_sink", None) is not None:
                     sinks[k] = p._ptdt_grad_sink()
-        dx, dw, db, dres = native().bn_bwd(_like(dy, x), x, y, weight, stats, ctx.relu, want_dres, want_dw,
-                                           ctx.tickets, sinks[0], sinks[1])
+        dx, dw, db, dres = native().bn_bwd(dy, x, y, weight, stats, ctx.relu, want_dres, want_dw,
+                                           ctx.tickets, sinks[0], sinks[1], dy2)
+        if link_in is not None:  # delivered to the residual's producer instead of autograd
+            link_in.dres, dres = dres, None
         return (dx if ctx.needs_input_grad[0] else None, dw if want_dw else None, db if want_dw else None,
-                dres if want_dres else None, None, None, None, None, None, None, None)
+                dres if ctx.has_res and ctx.needs_input_grad[3] else None, None, None, None, None, None, None, None,
+                None, None)
 
 
 def _tickets_of(bn, x):
@@ -81,17 +113,27 @@ def _tickets_of(bn, x):
 
 
 def batch_norm_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: torch.Tensor | None = None,
-                   relu: bool = False) -> torch.Tensor:
-    """``ReLU?(bn(x) + residual)`` with ``bn``'s parameters, buffers and train/eval mode."""
+                   relu: bool = False, link: bool = False) -> torch.Tensor:
+    """``ReLU?(bn(x) + residual)`` with ``bn``'s parameters, buffers and train/eval mode.
+
+    ``link=True``: when ``residual`` is the output of another fused BN, its gradient
+    is handed to that BN's backward kernels (:class:`ResidualLink`) instead of being
+    added to the residual's other gradients by autograd. Only for a residual whose
+    producer is a fused BN (a ResNet identity shortcut)."""
     fast = _rows_layout_ok(x) and (residual is None or (residual.dtype == x.dtype and residual.shape == x.shape
                                                         and residual.stride() == x.stride()
                                                         and residual.data_ptr() % 16 == 0))
     use_batch_stats = bn.training or not bn.track_running_stats
     if fast and use_batch_stats and bn.momentum is not None:
         track = bn.training and bn.track_running_stats
-        return _BatchNormActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean if track else None,
-                                     bn.running_var if track else None, bn.num_batches_tracked if track else None,
-                                     relu, float(bn.momentum), float(bn.eps), _tickets_of(bn, x))
+        link_in = getattr(residual, "_ptdt_res_link", None) if (link and residual is not None) else None
+        link_out = ResidualLink() if torch.is_grad_enabled() else None
+        y = _BatchNormActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean if track else None,
+                                  bn.running_var if track else None, bn.num_batches_tracked if track else None,
+                                  relu, float(bn.momentum), float(bn.eps), _tickets_of(bn, x), link_in, link_out)
+        if link_out is not None:
+            y._ptdt_res_link = link_out
+        return y
     needs_grad = torch.is_grad_enabled() and (x.requires_grad or (residual is not None and residual.requires_grad))
     if fast and not use_batch_stats and not needs_grad:  # eval: one launch with the running statistics
         scale = torch.rsqrt(bn.running_var.float() + bn.eps)
@@ -126,9 +168,9 @@ class BatchNorm2d(nn.BatchNorm2d):
         self.register_buffer("_bn_tickets", torch.zeros(max(1, -(-num_features // 32)), dtype=torch.int32),
                              persistent=False)
 
-    def forward(self, x, residual=None, relu: bool = False):
+    def forward(self, x, residual=None, relu: bool = False, link: bool = False):
         self._check_input_dim(x)
-        return batch_norm_act(x, self, residual, relu)
+        return batch_norm_act(x, self, residual, relu, link)
 
 
 # ----------------------------------------------------------------------------- pooling
