@@ -37,6 +37,8 @@ def main(argv=None):
     ap.add_argument("--bucket_cap_mb", type=float, default=None)
     ap.add_argument("--impl", default="native", choices=["native", "torch"],
                     help="native DDP reducer + fused optimizer, or stock torch DDP + torch.optim.SGD (comparator)")
+    ap.add_argument("--no_shadow", action="store_true",
+                    help="cast the fp32 weights in every forward instead of using FusedSGD's bf16 shadows")
     ap.add_argument("--no_cudnn_benchmark", action="store_true",
                     help="keep MIOpen's heuristic solver choice (default: exhaustive find per conv shape)")
     a = ap.parse_args(argv)
@@ -60,7 +62,8 @@ def main(argv=None):
         model = model.to(memory_format=torch.channels_last)
     if a.impl == "native":
         ddp = DistributedDataParallel(model, device_ids=[dev.index], comm=comm, bucket_cap_mb=a.bucket_cap_mb)
-        opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+        opt = FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4,
+                       bf16_shadow=a.dtype == "bf16" and not a.no_shadow)
     else:
         from torch.nn.parallel import DistributedDataParallel as TorchDDP
 

@@ -388,9 +388,11 @@ void for_tensor_chunks(size_t n, F&& f) {
 
 void sgd_multi_(std::vector<Tensor> ps, std::vector<Tensor> gs, std::vector<Tensor> moms,
                 c10::optional<Tensor> step, double lr, double momentum, double dampening, double wd,
-                bool nesterov, double grad_scale) {
+                bool nesterov, double grad_scale, std::vector<Tensor> shadows) {
   if (ps.empty()) return;
   TORCH_CHECK(ps.size() == gs.size() && (moms.empty() || moms.size() == ps.size()));
+  TORCH_CHECK(shadows.empty() || (shadows.size() == ps.size() && ps[0].scalar_type() == at::kFloat),
+              "sgd_multi_: bf16 shadows need one per (f32) param");
   const int dt = dt_of(ps[0]);
   c10::hip::HIPGuard guard(ps[0].device().index());
   for_tensor_chunks(ps.size(), [&](size_t a, size_t b) {
@@ -406,6 +408,12 @@ void sgd_multi_(std::vector<Tensor> ps, std::vector<Tensor> gs, std::vector<Tens
       tl.g[i - a] = gs[i].data_ptr();
       tl.s1[i - a] = moms.empty() ? nullptr : moms[i].data_ptr<float>();
       tl.s2[i - a] = nullptr;
+      if (!shadows.empty()) {
+        TORCH_CHECK(shadows[i].scalar_type() == at::kBFloat16 && shadows[i].numel() == ps[i].numel(),
+                    "sgd_multi_: shadow must be a bf16 tensor of the param's size");
+        check_dense_like(ps[i], shadows[i], "bf16 shadow");
+        tl.s2[i - a] = reinterpret_cast<float*>(shadows[i].data_ptr());
+      }
     }
     hip_check(sgd_multi(tl, dt, ptr_or_null<int32_t>(step), (float)lr, (float)momentum, (float)dampening,
                         (float)wd, nesterov, (float)grad_scale, cur_stream(ps[0])),
@@ -1031,7 +1039,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("fused_mlp_lds_bytes", [](int B, int Din, int H, int Dout) { return fused_mlp_lds_bytes(B, Din, H, Dout); });
   m.def("sgd_flat_", &sgd_flat_);
   m.def("adam_flat_", &adam_flat_);
-  m.def("sgd_multi_", &sgd_multi_);
+  m.def("sgd_multi_", &sgd_multi_, py::arg("ps"), py::arg("gs"), py::arg("moms"), py::arg("step"), py::arg("lr"),
+        py::arg("momentum"), py::arg("dampening"), py::arg("wd"), py::arg("nesterov"), py::arg("grad_scale"),
+        py::arg("shadows") = std::vector<Tensor>{});
   m.def("adam_multi_", &adam_multi_);
   m.def("bucket_copy", &bucket_copy);
   m.def("scale_", &scale_);

@@ -159,7 +159,8 @@ struct TensorList {
   void* p[kMaxTensorsPerLaunch];           // param (f32 or bf16, see dtype)
   const void* g[kMaxTensorsPerLaunch];     // grad (same dtype as param)
   float* s1[kMaxTensorsPerLaunch];         // momentum / exp_avg (f32) or nullptr
-  float* s2[kMaxTensorsPerLaunch];         // exp_avg_sq (f32) or nullptr
+  float* s2[kMaxTensorsPerLaunch];         // exp_avg_sq (f32) or nullptr; SGD on f32 params: optional bf16
+                                           // shadow of the updated param (uint16_t*), the autocast weight copy
 };
 hipError_t sgd_multi(const TensorList& tl, int dtype, int32_t* step, float lr, float momentum,
                      float dampening, float weight_decay, int nesterov, float grad_scale,

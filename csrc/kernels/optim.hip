@@ -11,6 +11,8 @@
 //  * *_multi: a kernel-argument tensor list (<= 32 tensors per launch, no
 //    device-side metadata, so it is hipGraph-capturable); blocks are mapped
 //    to (tensor, chunk) by a prefix search over chunk counts.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -118,10 +120,14 @@ __global__ void __launch_bounds__(kBlock) sgd_multi_kernel(TensorList tl, int32_
   T* p = static_cast<T*>(tl.p[t]);
   const T* g = static_cast<const T*>(tl.g[t]);
   float* mom = tl.s1[t];
+  // f32 params: the bf16 autocast copy of the updated weight, written in the same pass
+  uint16_t* shadow = std::is_same<T, float>::value ? reinterpret_cast<uint16_t*>(tl.s2[t]) : nullptr;
   const int64_t end = min(start + (int64_t)kChunk, tl.numel[t]);
   for (int64_t i = start + threadIdx.x; i < end; i += kBlock) {
     const float pv = Cvt<T>::load(p, i);
-    Cvt<T>::store(p, i, sgd_update(pv, Cvt<T>::load(g, i), mom, i, first, h));
+    const float nv = sgd_update(pv, Cvt<T>::load(g, i), mom, i, first, h);
+    Cvt<T>::store(p, i, nv);
+    if (shadow) shadow[i] = f32_to_bf16(nv);
   }
 }
 

@@ -31,9 +31,9 @@ class SinkCast(torch.autograd.Function):
     """``w.to(dtype)`` whose backward can land the gradient in ``w``'s DDP bucket slot."""
 
     @staticmethod
-    def forward(ctx, w, dtype):
+    def forward(ctx, w, dtype, shadow=None):
         ctx.w = w
-        return w.to(dtype)
+        return shadow.detach() if shadow is not None else w.to(dtype)
 
     @staticmethod
     def backward(ctx, g):
@@ -42,8 +42,8 @@ class SinkCast(torch.autograd.Function):
         out = sink() if (sink is not None and w.grad is None) else None  # None: slot already claimed
         if out is not None:
             out.copy_(g)  # bf16 -> fp32 conversion straight into the bucket
-            return out, None
-        return g.to(w.dtype), None
+            return out, None, None
+        return g.to(w.dtype), None, None
 
 
 def cast_weight(w: torch.Tensor) -> torch.Tensor:
@@ -53,9 +53,13 @@ def cast_weight(w: torch.Tensor) -> torch.Tensor:
     dt = torch.get_autocast_dtype("cuda")
     if dt not in (torch.bfloat16, torch.float16):
         return w
+    # the optimizer's bf16 copy of the current weight (FusedSGD(bf16_shadow=True)), if still current
+    sh = getattr(w, "_ptdt_bf16", None)
+    if sh is not None and (dt != torch.bfloat16 or getattr(w, "_ptdt_bf16_version", -1) != w._version):
+        sh = None
     if w.requires_grad and torch.is_grad_enabled():
-        return SinkCast.apply(w, dt)
-    return w.to(dt)
+        return SinkCast.apply(w, dt, sh)
+    return sh if sh is not None else w.to(dt)
 
 
 class Conv2d(nn.Conv2d):

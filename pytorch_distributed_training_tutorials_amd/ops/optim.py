@@ -32,9 +32,23 @@ def _split_by_device(params, with_grad_only: bool = True):
     return out
 
 
+def _bf16_shadow(p: torch.Tensor) -> torch.Tensor:
+    sh = getattr(p, "_ptdt_bf16", None)
+    if sh is None or sh.shape != p.shape or sh.stride() != p.stride() or sh.device != p.device:
+        sh = torch.empty_like(p, dtype=torch.bfloat16)
+        p._ptdt_bf16 = sh
+    return sh
+
+
 class FusedSGD(Optimizer):
+    """``bf16_shadow=True``: every f32 GPU parameter also gets a bf16 copy of its
+    updated value, written by the same update kernel (``p._ptdt_bf16``); under bf16
+    autocast :func:`ops.conv.cast_weight` uses it instead of casting the weight in
+    every forward (one cast kernel per conv per step)."""
+
     def __init__(self, params, lr: float = 1e-3, momentum: float = 0.0, dampening: float = 0.0,
-                 weight_decay: float = 0.0, nesterov: bool = False, maximize: bool = False):
+                 weight_decay: float = 0.0, nesterov: bool = False, maximize: bool = False,
+                 bf16_shadow: bool = False):
         if lr < 0.0:
             raise ValueError(f"Invalid learning rate: {lr}")
         if nesterov and (momentum <= 0 or dampening != 0):
@@ -44,6 +58,7 @@ class FusedSGD(Optimizer):
         super().__init__(params, defaults)
         self._counters: dict = {}
         self._flat_mom: dict = {}
+        self.bf16_shadow = bf16_shadow
 
     def _counter(self, gi: int, device) -> torch.Tensor:
         key = (gi, device)
@@ -96,13 +111,16 @@ class FusedSGD(Optimizer):
                 mflat = contiguous_span(moms) if moms else None
                 pdata = [p.data for p in ps]
                 aligned = same_layout(pdata, grads) and (not moms or same_layout(pdata, moms))
+                shadows = [_bf16_shadow(p) for p in ps] if (self.bf16_shadow and dtype == torch.float32) else []
                 if (dtype == torch.float32 and aligned and pflat is not None and gflat is not None
-                        and (not moms or mflat is not None)):
+                        and (not moms or mflat is not None) and not shadows):
                     # one launch for the whole group (also increments the device counter)
                     C.sgd_flat_(pflat, gflat, mflat, step, lr, mu, damp, wd, nest, gscale)
                 else:
-                    C.sgd_multi_([p.data for p in ps], grads, moms, step, lr, mu, damp, wd, nest, gscale)
+                    C.sgd_multi_(pdata, grads, moms, step, lr, mu, damp, wd, nest, gscale, shadows)
                     step.add_(1)
+                for p in ps if shadows else ():
+                    p._ptdt_bf16_version = p._version  # the shadow is current until p changes
         return loss
 
     def _cpu_step(self, ps, lr, mu, damp, wd, nest, gscale):
