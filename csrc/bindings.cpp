@@ -310,9 +310,10 @@ class PersistentPlan {
 // Which persistent engine fused_mlp_persistent would run for this configuration
 // ("workgroup", or "wave:L<lanes per row>R<rows per lane group>K<features per lane>").
 std::string persistent_engine(int64_t B, int64_t Din, int64_t H, int64_t Dout, int64_t loss_kind, int64_t num_samples,
-                              int64_t world, int64_t variant) {
+                              int64_t world, int64_t variant, bool has_bias) {
   FusedMlpArgs a{};
   a.B = (int)B; a.Din = (int)Din; a.H = (int)H; a.Dout = (int)Dout; a.loss_kind = (int)loss_kind;
+  a.has_bias = has_bias ? 1 : 0;
   a.ar.world = (int)world;
   a.ldx = 1 << 20;  // the caller zero-pads X rows to the layout's width when needed
   a.x_padded = 1;
@@ -1035,7 +1036,8 @@ PYBIND11_MODULE(_C, m) {
       .def("launch", &PersistentPlan::launch, py::arg("n_steps"), py::arg("cursor_pos") = -1)
       .def_property_readonly("capacity", &PersistentPlan::capacity);
   m.def("persistent_engine", &persistent_engine, py::arg("B"), py::arg("Din"), py::arg("H"), py::arg("Dout"),
-        py::arg("loss_kind"), py::arg("num_samples"), py::arg("world"), py::arg("variant") = 0);
+        py::arg("loss_kind"), py::arg("num_samples"), py::arg("world"), py::arg("variant") = 0,
+        py::arg("has_bias") = true);
   m.def("fused_mlp_lds_bytes", [](int B, int Din, int H, int Dout) { return fused_mlp_lds_bytes(B, Din, H, Dout); });
   m.def("sgd_flat_", &sgd_flat_);
   m.def("adam_flat_", &adam_flat_);

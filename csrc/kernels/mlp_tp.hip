@@ -44,6 +44,18 @@ using f4 = __attribute__((ext_vector_type(4))) float;
 
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 
+// Wait states between the end of an MFMA chain and the first VALU read of its result,
+// padded explicitly: with a (uniform) branch between the last v_mfma_f32_16x16x4_f32
+// and the read, hipcc's hazard recognizer padded only for the fall-through path
+// (s_nop 1 before reading the 4th result register on the taken one), and the read
+// returned a stale value (the 4th register of the dW1^T tile, only when no other MFMA
+// chain followed). 8-pass XDL -> VALU read needs 11; scheduling is fenced on both sides.
+__device__ __forceinline__ void mfma_settle() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_nop 7\n\ts_nop 4" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // across the 4 lane groups (DPP rows) of a column: permlane16 then permlane32
 // swaps, symmetric pairing -> every lane gets the same bits
 __device__ __forceinline__ float rows4_sum(float v) {
@@ -166,8 +178,9 @@ constexpr int kTpLDT = 36;  // per-wave transposes: 16 (class / unit) x 32 rows
 __host__ __device__ __forceinline__ int tp_wave_floats() { return 16 * kTpLD2 + 2 * 16 * kTpLDT; }
 __host__ __device__ __forceinline__ int tp_stage_floats(int MT) { return 32 * (16 * MT + 4) + 16 * MT * 36 + 32 * 16; }
 
-// MT: 16-input tiles of the augmented input (Din inputs + a constant-1 column carrying b1)
-template <int MT, int LOSS, bool AR>
+// MT: 16-input tiles of the augmented input (Din inputs + a constant-1 column carrying b1);
+// VX: X rows staged as float4 chunks (Din and the row stride multiples of 4, X 16-B aligned)
+template <int MT, int LOSS, bool AR, bool VX>
 __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, PersistArgs pa) {
   // No implicit FMA contraction: the compiler may contract differently in a peeled
   // first iteration than in the loop body, which made a run split into several
@@ -271,54 +284,79 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     }
   };
 
-  // ---- batch staging: thread (row = tid & 31, column group tid >> 5) loads its row's
-  // columns g, g + G, ... of the next position's batch into registers at the top of a
-  // step and writes them to the next LDS slot before the step's barrier, so every
-  // wave's operands are LDS reads (X rows, X^T rows, targets) instead of per-lane
-  // gathers, and the global latency hides under the step's MFMAs.
-  constexpr int JX = 16, JY = 8;  // per-thread column slots (Din <= 32, Dout <= 16, >= 2 groups)
-  const int srow = tid & 31, sgrp = tid >> 5, G = T >> 5;
+  // ---- batch staging: the next position's batch tile (32 rows of X, the targets) is
+  // loaded by ALL threads at the top of a step and written to the next LDS slot (rows,
+  // and X^T) before the step's barrier, so every wave's operands are LDS reads and the
+  // global latency hides under the step's MFMAs. Item e = tid + k T of the tile (float4
+  // chunks when VX, else single floats) for k below a count that is uniform across the
+  // workgroup; the last item is repeated past the end (identical writes) and rows past
+  // the batch read clamped rows: no divergent branches, no per-step divisions.
+  constexpr int KX = VX ? 4 : 16, KY = 8;
   const auto X = gptr(a.X);
   const int ldx = a.ldx > 0 ? a.ldx : Din;
-  const int jx = (Din - sgrp + G - 1) / G;
-  const int jy = LOSS == kLossCEIndex ? (sgrp == 0 ? 1 : 0) : (Dout - sgrp + G - 1) / G;
-  float xv[JX], yv[JY];
-  int yiv = 0;
+  const int xper = VX ? Din / 4 : Din;  // items per row
+  const int nkx = (32 * xper + T - 1) / T;
+  int xrow[KX], xcol[KX];
+#pragma unroll
+  for (int k = 0; k < KX; ++k) {
+    const int e = min(tid + k * T, 32 * xper - 1);
+    xrow[k] = e / xper;
+    xcol[k] = e - xrow[k] * xper;
+  }
+  constexpr bool YI = LOSS == kLossCEIndex;
+  const int yper = YI ? 1 : Dout;
+  const int nky = (32 * yper + T - 1) / T;
+  int yrow[KY], ycol[KY];
+#pragma unroll
+  for (int k = 0; k < KY; ++k) {
+    const int e = min(tid + k * T, 32 * yper - 1);
+    yrow[k] = e / yper;
+    ycol[k] = e - yrow[k] * yper;
+  }
+  f4 xv[KX];
+  float yv[KY];
   auto stage_issue = [&](int E, int J) {
-    if (srow >= B) return;
     const int nb = min(B, ns - J * B);
-    const int sel = list(E)[J * B + min(srow, nb - 1)];
-    const auto xr = X + (int64_t)sel * ldx + sgrp;
+    const int* const li = list(E) + J * B;
 #pragma unroll
-    for (int j = 0; j < JX; ++j)
-      if (j < jx) xv[j] = xr[j * G];
-    if constexpr (LOSS == kLossCEIndex) {
-      if (jy) yiv = (int)gptr(a.Yi)[sel];
-    } else {
-      const auto yr = gptr(a.Yf) + (int64_t)sel * Dout + sgrp;
+    for (int k = 0; k < KX; ++k) {
+      if (k < nkx) {
+        const int sel = li[min(xrow[k], nb - 1)];
+        if constexpr (VX) {
+          xv[k] = *reinterpret_cast<const f4*>(a.X + (int64_t)sel * ldx + 4 * xcol[k]);
+        } else {
+          xv[k][0] = X[(int64_t)sel * ldx + xcol[k]];
+        }
+      }
+    }
 #pragma unroll
-      for (int j = 0; j < JY; ++j)
-        if (j < jy) yv[j] = yr[j * G];
+    for (int k = 0; k < KY; ++k) {
+      if (k < nky) {
+        const int sel = li[min(yrow[k], nb - 1)];
+        if constexpr (YI) yv[k] = __int_as_float((int)gptr(a.Yi)[sel]);
+        else yv[k] = gptr(a.Yf)[(int64_t)sel * Dout + ycol[k]];
+      }
     }
   };
   auto stage_write = [&](int slot) {
-    if (srow >= B) return;
     float* const st = stage(slot);
 #pragma unroll
-    for (int j = 0; j < JX; ++j) {
-      if (j < jx) {
-        const int col = sgrp + j * G;
-        st[srow * LDX + col] = xv[j];
-        st[St::XT_OFF + col * LDXT + srow] = xv[j];
+    for (int k = 0; k < KX; ++k) {
+      if (k < nkx) {
+        const int row = xrow[k];
+        if constexpr (VX) {
+          *reinterpret_cast<f4*>(st + row * LDX + 4 * xcol[k]) = xv[k];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) st[St::XT_OFF + (4 * xcol[k] + i) * LDXT + row] = xv[k][i];
+        } else {
+          st[row * LDX + xcol[k]] = xv[k][0];
+          st[St::XT_OFF + xcol[k] * LDXT + row] = xv[k][0];
+        }
       }
     }
-    if constexpr (LOSS == kLossCEIndex) {
-      if (jy) reinterpret_cast<int*>(st + St::Y_OFF)[srow] = yiv;
-    } else {
 #pragma unroll
-      for (int j = 0; j < JY; ++j)
-        if (j < jy) st[St::Y_OFF + srow * 16 + sgrp + j * G] = yv[j];
-    }
+    for (int k = 0; k < KY; ++k)
+      if (k < nky) st[St::Y_OFF + (YI ? yrow[k] : yrow[k] * 16 + ycol[k])] = yv[k];
   };
 
   // ---- resident state: this wave's W1 rows (b1 as column Din) and W2 columns in
@@ -371,7 +409,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   int ce = e0, cj = j0;  // current position (epoch, step in epoch): no divisions in the loop
   int sc = 0;            // LDS slot of the current batch
   int pc = 0;            // steps until the next production chunk
-  const bool stamps = pa.stamps != nullptr && tid == 0;
+  const bool stamps = pa.stamps != nullptr;  // uniform: s_memtime is scalar, thread 0 reports
   int64_t tmark = stamps ? (int64_t)__builtin_amdgcn_s_memtime() : 0;
   int64_t acc_t[6] = {0, 0, 0, 0, 0, 0};
   const int64_t t_begin = tmark, r_begin = stamps ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
@@ -408,6 +446,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         for (int s = 0; s < 4; ++s) h[t] = mfma4(w1r[mt][s], xb[s], h[t]);
       }
     }
+    mfma_settle();
     float ht[2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -422,6 +461,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       z[0] = mfma4(a2[s], ht[0][s], z[0]);
       z[1] = mfma4(a2[s], ht[1][s], z[1]);
     }
+    mfma_settle();
     {
       f4* dst = reinterpret_cast<f4*>(xbuf + ((par * NW + w) * 64 + l) * 8);
       dst[0] = z[0];
@@ -544,6 +584,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       dh[0] = mfma4(g[0][s], w2t[s], dh[0]);
       dh[1] = mfma4(g[1][s], w2t[s], dh[1]);
     }
+    mfma_settle();
     // transposed reads: H[row 16t + 4q + s][unit c] (ReLU mask, dW2's B) and
     // dZ[row 16t + 4q + s][class c] (dW2's A)
     f4 hT[2], dzT[2];
@@ -575,6 +616,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         for (int mt = 0; mt < MT; ++mt) gw1[mt] = mfma4(xa[mt][s], dh[t][s], gw1[mt]);
       }
     }
+    mfma_settle();
     tick(4);
 
     // ---------------- all-reduce over ranks (xGMI LL), then SGD in registers
@@ -687,18 +729,23 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 
 int tp_mt(const FusedMlpArgs& a) { return a.Din + (a.has_bias ? 1 : 0) <= 16 ? 1 : 2; }
 
-template <int LOSS, bool AR>
+template <int LOSS, bool AR, bool VX>
 const void* pick_mt(int mt) {
-  return mt == 1 ? (const void*)mlp_tp_kernel<1, LOSS, AR> : (const void*)mlp_tp_kernel<2, LOSS, AR>;
+  return mt == 1 ? (const void*)mlp_tp_kernel<1, LOSS, AR, VX> : (const void*)mlp_tp_kernel<2, LOSS, AR, VX>;
 }
 
-template <bool AR>
+template <bool AR, bool VX>
 const void* pick_loss_tp(int loss, int mt) {
   switch (loss) {
-    case kLossCEIndex: return pick_mt<kLossCEIndex, AR>(mt);
-    case kLossMSE: return pick_mt<kLossMSE, AR>(mt);
-    default: return pick_mt<kLossCESoft, AR>(mt);
+    case kLossCEIndex: return pick_mt<kLossCEIndex, AR, VX>(mt);
+    case kLossMSE: return pick_mt<kLossMSE, AR, VX>(mt);
+    default: return pick_mt<kLossCESoft, AR, VX>(mt);
   }
+}
+
+bool tp_vec_x(const FusedMlpArgs& a) {
+  const int ldx = a.ldx > 0 ? a.ldx : a.Din;
+  return a.Din % 4 == 0 && ldx % 4 == 0 && reinterpret_cast<uintptr_t>(a.X) % 16 == 0;
 }
 
 size_t tp_lds_bytes(const FusedMlpArgs& a, const PersistArgs& p) {
@@ -722,7 +769,9 @@ bool mlp_tp_supported(const FusedMlpArgs& a, const PersistArgs& p) {
 hipError_t mlp_tp_prepare(const FusedMlpArgs& a, const PersistArgs& p, PersistLaunch* out) {
   if (!mlp_tp_supported(a, p)) return hipErrorInvalidValue;
   const int mt = tp_mt(a);
-  const void* fn = a.ar.world > 1 ? pick_loss_tp<true>(a.loss_kind, mt) : pick_loss_tp<false>(a.loss_kind, mt);
+  const bool vx = tp_vec_x(a);
+  const void* fn = a.ar.world > 1 ? (vx ? pick_loss_tp<true, true>(a.loss_kind, mt) : pick_loss_tp<true, false>(a.loss_kind, mt))
+                                  : (vx ? pick_loss_tp<false, true>(a.loss_kind, mt) : pick_loss_tp<false, false>(a.loss_kind, mt));
   const size_t lds = tp_lds_bytes(a, p);
   if (lds > 64 * 1024) PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   out->fn = fn;

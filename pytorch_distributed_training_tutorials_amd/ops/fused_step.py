@@ -214,7 +214,7 @@ class FusedMLPStep:
         """The wave engine reads whole lane chunks (L lanes x K features per row):
         when L*K > Din, hand it a zero-padded copy of X (cached per tensor version)."""
         eng = self._C.persistent_engine(batch_size, self.Din, self.H, self.Dout, self.loss_kind,
-                                        sampler.num_samples, sampler.num_replicas, vid)
+                                        sampler.num_samples, sampler.num_replicas, vid, self.has_bias)
         if not eng.startswith("wave"):
             return X, False
         lanes, kp = int(eng.split("L")[1].split("R")[0]), int(eng.split("K")[1])
@@ -234,7 +234,8 @@ class FusedMLPStep:
         """Which persistent engine :meth:`run_persistent` runs: "workgroup" or
         "wave:L<l>R<r>K<k>" (lanes per row, rows per lane group, features per lane)."""
         return self._C.persistent_engine(batch_size, self.Din, self.H, self.Dout, self.loss_kind,
-                                         sampler.num_samples, sampler.num_replicas, _variant_id(variant))
+                                         sampler.num_samples, sampler.num_replicas, _variant_id(variant),
+                                         self.has_bias)
 
     # ------------------------------------------------------------ optimizer state
     def export_optimizer_state(self, optimizer) -> None:

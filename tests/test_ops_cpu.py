@@ -143,6 +143,9 @@ def test_persistent_engine_selection():
     assert C.persistent_engine(64, 16, 0, 1, ce_soft, 1000, 1).startswith("wave")
     # hidden layer: the 4-wave MFMA step body when the shape fits it, the LDS dot-product body otherwise
     assert C.persistent_engine(32, 20, 64, 10, ce_index, 2048, 1) == "tp:4waves"  # tensor-parallel MFMA engine
+    # b1 rides in W1 as input column Din: Din + bias <= 32
+    assert C.persistent_engine(32, 32, 64, 10, ce_index, 2048, 1, 0, False) == "tp:4waves"
+    assert C.persistent_engine(32, 32, 64, 10, ce_index, 2048, 1, 0, True) == "workgroup:mfma"
     assert C.persistent_engine(32, 20, 64, 10, ce_index, 2048, 1, 5) == "workgroup:mfma"  # forced
     assert C.persistent_engine(32, 20, 64, 10, ce_index, 2048, 1, 1) == "workgroup"  # forced
     assert C.persistent_engine(64, 20, 64, 10, ce_index, 2048, 1) == "workgroup"  # B > 32
