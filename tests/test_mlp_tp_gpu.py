@@ -60,10 +60,12 @@ def _epoch_orders(sampler, epochs, dev):
     (32, 20, 64, 10, "ce_index", True),   # the BASELINE toy MLP
     (32, 20, 64, 10, "ce_soft", True),
     (16, 7, 32, 3, "ce_soft", True),
-    (32, 32, 16, 16, "mse", True),
+    (32, 32, 16, 16, "mse", False),     # 32 inputs: two full tiles (b1 needs a free column: Din <= 31)
+    (32, 31, 16, 16, "mse", True),
     (24, 20, 48, 1, "ce_soft", True),     # one class: the reference's zero-loss quirk shape
     (32, 17, 64, 10, "ce_index", False),  # two input tiles, no biases
     (8, 4, 16, 2, "mse", True),
+    (32, 12, 64, 10, "ce_index", True),  # one 16-input tile, float4 staging
 ])
 def test_tp_engine_matches_torch_fp32(dev, B, Din, H, Dout, loss, bias):
     from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler

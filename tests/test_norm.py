@@ -221,23 +221,30 @@ def test_maxpool_cpu_falls_back():
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_residual_link_matches_autograd_add(dtype):
     """Identity shortcut between two fused BNs: the residual gradient handed to the
-    producer's backward kernels (dy + dy2 in-kernel) equals autograd's add."""
+    producer's backward kernels (dy + dy2 in-kernel) equals autograd's add (fp32), and
+    in bf16 is at least as close to the fp32 result as autograd's bf16 add."""
     from pytorch_distributed_training_tutorials_amd.ops.norm import BatchNorm2d
 
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    x0 = torch.randn(4, 64, 9, 7, device=dev, dtype=dtype).contiguous(memory_format=torch.channels_last)
-    w = torch.randn(64, 64, 1, 1, device=dev, dtype=dtype).contiguous(memory_format=torch.channels_last) * 0.2
-    grads = []
-    for link in (False, True):
+    x0 = torch.randn(4, 64, 9, 7, device=dev).contiguous(memory_format=torch.channels_last)
+    w0 = torch.randn(64, 64, 1, 1, device=dev).contiguous(memory_format=torch.channels_last) * 0.2
+
+    def grads(dt, link):
         torch.manual_seed(1)
         bn_a, bn_b = BatchNorm2d(64).to(dev), BatchNorm2d(64).to(dev)
-        x = x0.clone().requires_grad_(True)
-        y1 = bn_a(x, relu=True)                            # producer
-        h = torch.nn.functional.conv2d(y1, w)              # the block's conv path
-        y2 = bn_b(h, residual=y1, relu=True, link=link)    # consumer: identity shortcut
+        x = x0.to(dt).clone().requires_grad_(True)
+        y1 = bn_a(x, relu=True)                              # producer
+        h = torch.nn.functional.conv2d(y1, w0.to(dt))        # the block's conv path
+        y2 = bn_b(h, residual=y1, relu=True, link=link)      # consumer: identity shortcut
         (y2.float() * torch.linspace(-1, 1, y2.numel(), device=dev).view_as(y2)).sum().backward()
-        grads.append([t.grad.float().clone() for t in (x, bn_a.weight, bn_a.bias, bn_b.weight, bn_b.bias)])
-    tol = dict(rtol=1e-4, atol=1e-5) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
-    for g0, g1 in zip(*grads):
-        torch.testing.assert_close(g1, g0, **tol)
+        return [t.grad.float().clone() for t in (x, bn_a.weight, bn_a.bias, bn_b.weight, bn_b.bias)]
+
+    if dtype == torch.float32:
+        for g0, g1 in zip(grads(dtype, False), grads(dtype, True)):
+            torch.testing.assert_close(g1, g0, rtol=1e-4, atol=1e-5)
+    else:
+        truth = grads(torch.float32, False)
+        for gt, g0, g1 in zip(truth, grads(dtype, False), grads(dtype, True)):
+            e0, e1 = (g0 - gt).norm().item(), (g1 - gt).norm().item()
+            assert e1 <= 1.5 * e0 + 1e-3 * gt.norm().item(), (e1, e0)
