@@ -197,5 +197,5 @@ def test_fused_sgd_bf16_shadow_replaces_autocast_cast():
                 with torch.no_grad():
                     w.mul_(0.5)  # outside the optimizer: the shadow is stale now
                 assert cast_weight(w).data_ptr() != w._ptdt_bf16.data_ptr()
-    for a, b in zip(*outs):
-        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    for a, b in zip(*outs):  # (MIOpen's weight-gradient solvers may sum in any order: not bitwise)
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)

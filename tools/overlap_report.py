@@ -20,7 +20,7 @@ import argparse
 import re
 import sqlite3
 
-COMM = re.compile(r"nccl|rccl", re.I)
+COMM = re.compile(r"nccl|rccl|oneRankReduce", re.I)  # oneRankReduce: RCCL at world 1
 OPT = re.compile(r"sgd_multi|sgd_flat")
 
 
@@ -52,6 +52,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("db")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--table", type=int, default=0, help="also print the top-N kernels of those iterations")
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = c.execute("select name, start, end, stream_id from kernels order by start").fetchall()
@@ -81,6 +82,20 @@ def main():
         bk = ", ".join(f"{(s - t0) / 1e6:.2f}-{(e - t0) / 1e6:.2f}" for s, e in comm)
         step = (rows[hi][1] - t0) / 1e6
         print(f"| {it} | {step:.2f} | {busy / 1e6:.3f} | {100 * conc / max(busy, 1):.0f}% | {tail / 1e3:.0f} | {bk} |")
+    if a.table and len(bounds) > a.steps:
+        lo, hi = bounds[len(bounds) - a.steps - 1] + 1, bounds[-1] + 1
+        agg = {}
+        for name, s0, e0, _ in rows[lo:hi]:
+            n, t = agg.get(name, (0, 0))
+            agg[name] = (n + 1, t + e0 - s0)
+        tot = sum(t for _, t in agg.values())
+        print(f"\nkernels of the last {a.steps} iterations (busy {tot / 1e6 / a.steps:.2f} ms per iteration)\n")
+        print("| kernel | calls/iter | us/iter | % |")
+        print("|---|---|---|---|")
+        for name, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.table]:
+            short = name.replace("void ", "").replace("(anonymous namespace)::", "")
+            short = re.sub(r"\(.*$", "", short)[:90]
+            print(f"| `{short}` | {n / a.steps:.0f} | {t / 1e3 / a.steps:.0f} | {100 * t / tot:.1f} |")
 
 
 if __name__ == "__main__":
