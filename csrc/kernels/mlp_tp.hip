@@ -175,12 +175,13 @@ struct TpStage {
 };
 constexpr int kTpLD2 = 20;  // W2 slice (classes x 16 units), b128 rows
 constexpr int kTpLDT = 36;  // per-wave transposes: 16 (class / unit) x 32 rows
-__host__ __device__ __forceinline__ int tp_wave_floats() { return 16 * kTpLD2 + 2 * 16 * kTpLDT; }
+__host__ __device__ __forceinline__ int tp_wave_floats() { return 16 * kTpLD2 + 2 * 16 * kTpLDT + 16; }
 __host__ __device__ __forceinline__ int tp_stage_floats(int MT) { return 32 * (16 * MT + 4) + 16 * MT * 36 + 32 * 16; }
 
 // MT: 16-input tiles of the augmented input (Din inputs + a constant-1 column carrying b1);
-// VX: X rows staged as float4 chunks (Din and the row stride multiples of 4, X 16-B aligned)
-template <int MT, int LOSS, bool AR, bool VX>
+// VX: X rows staged as float4 chunks (Din and the row stride multiples of 4, X 16-B aligned);
+// ST: phase timers compiled in (diagnostic build: uniform branches around s_memtime)
+template <int MT, int LOSS, bool AR, bool VX, bool ST>
 __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, PersistArgs pa) {
   // No implicit FMA contraction: the compiler may contract differently in a peeled
   // first iteration than in the loop body, which made a run split into several
@@ -211,6 +212,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   float* const W2m = wbase;                                   // [16 classes][LD2] W2[:, slice] (fwd layout)
   float* const Th = W2m + 16 * LD2;                           // [16 units][LDT] H^T of this slice
   float* const Tdz = Th + 16 * LDT;                           // [16 classes][LDT] dZ^T
+  float* const B2m = Tdz + 16 * LDT;                          // [16] b2 (the forward's class-4q+i reads)
   auto list = [&](int e) { return elist + (e % 3) * d.estride; };
   auto stage = [&](int slot) { return stage0 + slot * St::FLOATS; };
 
@@ -365,7 +367,8 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   //   w1r[mt][i] = W1aug[unit 16w + c][input 16 mt + 4q + i]   (= dW1^T's layout)
   //   w2t[i]     = W2[class 4q + i][unit 16w + c]              (= dW2's layout)
   const auto P = gptr(a.P);
-  float w1r[MT][4], m1r[MT][4], w2t[4], m2t[4], b2r[4], mb2r[4];
+  // b2c = b2[class c] (= db2's layout: the column sums of dZ^T), mirrored to LDS for the forward
+  float w1r[MT][4], m1r[MT][4], w2t[4], m2t[4], b2c, mb2c;
   const int unit = 16 * w + c;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -383,10 +386,11 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     const bool real = cls < Dout;
     w2t[i] = real ? P[d.oW2 + cls * H + unit] : 0.f;
     m2t[i] = (real && use_mom) ? a.mom[d.oW2 + cls * H + unit] : 0.f;
-    b2r[i] = (hb && real) ? P[d.ob2 + cls] : 0.f;
-    mb2r[i] = (hb && real && use_mom) ? a.mom[d.ob2 + cls] : 0.f;
     W2m[cls * LD2 + c] = w2t[i];  // forward layout copy: W2[class c][unit 4q + s] at c*LD2 + 4q + s
   }
+  b2c = (hb && c < Dout) ? P[d.ob2 + c] : 0.f;
+  mb2c = (hb && c < Dout && use_mom) ? a.mom[d.ob2 + c] : 0.f;
+  if (q == 0) B2m[c] = b2c;
   int opt_step = a.opt_step ? *a.opt_step : 0;
   uint32_t seq = AR ? *a.ar.seq : 0u;
   bool failed = AR && *a.ar.err != 0;
@@ -398,10 +402,10 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 
   float* const losses = pa.losses;
   // last step's (averaged) gradients, written to the DDP bucket at the end
-  float lg1[MT][4], lg2[4], ldb2[4];
+  float lg1[MT][4], lg2[4], ldb2 = 0.f;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    lg2[i] = ldb2[i] = 0.f;
+    lg2[i] = 0.f;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) lg1[mt][i] = 0.f;
   }
@@ -409,7 +413,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   int ce = e0, cj = j0;  // current position (epoch, step in epoch): no divisions in the loop
   int sc = 0;            // LDS slot of the current batch
   int pc = 0;            // steps until the next production chunk
-  const bool stamps = pa.stamps != nullptr;  // uniform: s_memtime is scalar, thread 0 reports
+  constexpr bool stamps = ST;  // s_memtime is scalar: every wave times, thread 0 reports
   int64_t tmark = stamps ? (int64_t)__builtin_amdgcn_s_memtime() : 0;
   int64_t acc_t[6] = {0, 0, 0, 0, 0, 0};
   const int64_t t_begin = tmark, r_begin = stamps ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
@@ -446,7 +450,6 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         for (int s = 0; s < 4; ++s) h[t] = mfma4(w1r[mt][s], xb[s], h[t]);
       }
     }
-    mfma_settle();
     float ht[2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -461,7 +464,6 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       z[0] = mfma4(a2[s], ht[0][s], z[0]);
       z[1] = mfma4(a2[s], ht[1][s], z[1]);
     }
-    mfma_settle();
     {
       f4* dst = reinterpret_cast<f4*>(xbuf + ((par * NW + w) * 64 + l) * 8);
       dst[0] = z[0];
@@ -476,10 +478,11 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     tick(1);
     __syncthreads();
     float zf[2][4];
+    const f4 b2v = *reinterpret_cast<const f4*>(B2m + 4 * q);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) zf[t][i] = b2r[i];
+      for (int i = 0; i < 4; ++i) zf[t][i] = b2v[i];
     for (int v = 0; v < NW; ++v) {  // wave order: identical sums in every wave
       const f4* src = reinterpret_cast<const f4*>(xbuf + ((par * NW + v) * 64 + l) * 8);
       const f4 p0 = src[0], p1 = src[1];
@@ -521,16 +524,19 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
           se += e[i];
         }
         se = rows4_sum(se);
-        const float lse = m + __builtin_amdgcn_logf(se) * 0.6931471805599453f;
+        const float rse = 1.f / se;  // softmax = e / se; the log only feeds the reported loss
         if constexpr (LOSS == kLossCEIndex) {
           const int y = reinterpret_cast<const int*>(ys)[row];
           const bool use = rv && y != a.ignore_index;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int cls = 4 * q + i;
-            const float p = __expf(zf[t][i] - lse);
-            g[t][i] = (use && cls < Dout) ? p - (cls == y ? 1.f : 0.f) : 0.f;
-            lsum += (use && cls == y) ? lse - zf[t][i] : 0.f;
+            g[t][i] = (use && cls < Dout) ? e[i] * rse - (cls == y ? 1.f : 0.f) : 0.f;
+          }
+          if (w == 0) {
+            const float lse = m + __builtin_amdgcn_logf(se) * 0.6931471805599453f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lsum += (use && 4 * q + i == y) ? lse - zf[t][i] : 0.f;
           }
           cnt += __popcll(__ballot(use && q == 0));
         } else {  // soft targets: -(t . log_softmax(z)), grad = softmax * sum(t) - t
@@ -539,12 +545,16 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 #pragma unroll
           for (int i = 0; i < 4; ++i) ts += y[i];  // classes >= Dout stage as 0
           ts = rows4_sum(ts);
+          const float sc = ts * rse;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const bool ok = rv && 4 * q + i < Dout;
-            const float ls = zf[t][i] - lse;
-            lsum += ok ? -y[i] * ls : 0.f;
-            g[t][i] = ok ? __expf(ls) * ts - y[i] : 0.f;
+            g[t][i] = ok ? e[i] * sc - y[i] : 0.f;
+          }
+          if (w == 0) {
+            const float lse = m + __builtin_amdgcn_logf(se) * 0.6931471805599453f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) lsum += (rv && 4 * q + i < Dout) ? -y[i] * (zf[t][i] - lse) : 0.f;
           }
         }
       }
@@ -562,12 +572,10 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       lsum = wave_sum(lsum);
       if (l == 0) losses[k] = (LOSS == kLossCEIndex && cnt == 0) ? NAN : lsum * inv;
     }
-    float db2[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       g[0][i] *= inv;
       g[1][i] *= inv;
-      db2[i] = group_sum<16>(g[0][i]) + group_sum<16>(g[1][i]);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -578,13 +586,19 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     // ---------------- dH = dZ . W2[:, slice]: dZ's result layout is the A operand
     // (row c, class 4q + s) and w2t the B operand (class 4q + s, unit c); the result
     // dH[row 16t + 4q + i][unit c] is dW1's B operand as it stands
+    // X^T operands of dW1 (read now: their latency hides under the dH MFMAs)
+    f4 xa[2][MT];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+        xa[t][mt] = *reinterpret_cast<const f4*>(st + St::XT_OFF + (16 * mt + c) * LDXT + 16 * t + 4 * q);
     f4 dh[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       dh[0] = mfma4(g[0][s], w2t[s], dh[0]);
       dh[1] = mfma4(g[1][s], w2t[s], dh[1]);
     }
-    mfma_settle();
     // transposed reads: H[row 16t + 4q + s][unit c] (ReLU mask, dW2's B) and
     // dZ[row 16t + 4q + s][class c] (dW2's A)
     f4 hT[2], dzT[2];
@@ -597,6 +611,9 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) dh[t][i] = hT[t][i] > 0.f ? dh[t][i] : 0.f;
+    // db2[class c] = column sum of dZ^T: this lane's 8 rows, then the 4 lane groups
+    float db2 = ((dzT[0][0] + dzT[0][1]) + (dzT[0][2] + dzT[0][3])) + ((dzT[1][0] + dzT[1][1]) + (dzT[1][2] + dzT[1][3]));
+    db2 = rows4_sum(db2);
 
     // ---------------- dW2 = dZ^T . H (K = rows), dW1aug^T = Xaug^T . dH (K = rows)
     f4 gw2 = {0.f, 0.f, 0.f, 0.f};
@@ -605,18 +622,14 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     for (int mt = 0; mt < MT; ++mt) gw1[mt] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      f4 xa[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-        xa[mt] = *reinterpret_cast<const f4*>(st + St::XT_OFF + (16 * mt + c) * LDXT + 16 * t + 4 * q);
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         gw2 = mfma4(dzT[t][s], hT[t][s], gw2);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) gw1[mt] = mfma4(xa[mt][s], dh[t][s], gw1[mt]);
+        for (int mt = 0; mt < MT; ++mt) gw1[mt] = mfma4(xa[t][mt][s], dh[t][s], gw1[mt]);
       }
     }
-    mfma_settle();
+    mfma_settle();  // uniform branches follow (hb, tick, the all-reduce's failed check)
     tick(4);
 
     // ---------------- all-reduce over ranks (xGMI LL), then SGD in registers
@@ -630,7 +643,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     if constexpr (AR) {
       if (!failed) {
         seq += 1u;
-        constexpr int NV = 4 * MT + 8;
+        constexpr int NV = 4 * MT + 5;
         float v[NV];
         int idx[NV];
         bool push[NV], need[NV];
@@ -648,19 +661,19 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
           v[4 * MT + i] = gv2[i];
           idx[4 * MT + i] = cls < Dout ? d.oW2 + cls * H + unit : 0;
           push[4 * MT + i] = need[4 * MT + i] = cls < Dout;
-          v[4 * MT + 4 + i] = db2[i];
-          idx[4 * MT + 4 + i] = (hb && cls < Dout) ? d.ob2 + cls : 0;
-          push[4 * MT + 4 + i] = hb && cls < Dout && c == 0 && w == 0;
-          need[4 * MT + 4 + i] = hb && cls < Dout;
         }
+        v[4 * MT + 4] = db2;  // b2[class c]: one lane per class pushes
+        idx[4 * MT + 4] = (hb && c < Dout) ? d.ob2 + c : 0;
+        push[4 * MT + 4] = hb && c < Dout && q == 0 && w == 0;
+        need[4 * MT + 4] = hb && c < Dout;
         failed = !tp_allreduce<NV>(a.ar, seq, v, idx, push, need);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) gv1[mt][i] = v[mt * 4 + i];
           gv2[i] = v[4 * MT + i];
-          db2[i] = v[4 * MT + 4 + i];
         }
+        db2 = v[4 * MT + 4];
       }
     }
     // padded inputs / classes have zero gradients and zero weights: no masks needed
@@ -674,10 +687,13 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       }
       sgd1(w2t[i], m2t[i], gv2[i], first, lr, mu, damp, wd, nesterov, use_mom);
       W2m[(4 * q + i) * LD2 + c] = w2t[i];
-      if (hb) sgd1(b2r[i], mb2r[i], db2[i], first, lr, mu, damp, wd, nesterov, use_mom);
       lg2[i] = gv2[i];
-      ldb2[i] = db2[i];
     }
+    if (hb) {
+      sgd1(b2c, mb2c, db2, first, lr, mu, damp, wd, nesterov, use_mom);
+      if (q == 0) B2m[c] = b2c;
+    }
+    ldb2 = db2;
     ++opt_step;
     ce = ne;
     cj = nj;
@@ -707,12 +723,12 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       Pw[off] = w2t[i];
       if (use_mom) a.mom[off] = m2t[i];
       if (have) Gw[off] = lg2[i];
-      if (hb && c == 0 && w == 0) {
-        Pw[d.ob2 + cls] = b2r[i];
-        if (use_mom) a.mom[d.ob2 + cls] = mb2r[i];
-        if (have) Gw[d.ob2 + cls] = ldb2[i];
-      }
     }
+  }
+  if (hb && q == 0 && w == 0 && c < Dout) {
+    Pw[d.ob2 + c] = b2c;
+    if (use_mom) a.mom[d.ob2 + c] = mb2c;
+    if (have) Gw[d.ob2 + c] = ldb2;
   }
   if (tid == 0) {
     pa.cursor[0] = ce;
@@ -730,16 +746,19 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 int tp_mt(const FusedMlpArgs& a) { return a.Din + (a.has_bias ? 1 : 0) <= 16 ? 1 : 2; }
 
 template <int LOSS, bool AR, bool VX>
-const void* pick_mt(int mt) {
-  return mt == 1 ? (const void*)mlp_tp_kernel<1, LOSS, AR, VX> : (const void*)mlp_tp_kernel<2, LOSS, AR, VX>;
+const void* pick_mt(int mt, bool st) {
+  if (st && !AR)  // phase timers: world-1 diagnostic builds only
+    return mt == 1 ? (const void*)mlp_tp_kernel<1, LOSS, false, VX, true>
+                   : (const void*)mlp_tp_kernel<2, LOSS, false, VX, true>;
+  return mt == 1 ? (const void*)mlp_tp_kernel<1, LOSS, AR, VX, false> : (const void*)mlp_tp_kernel<2, LOSS, AR, VX, false>;
 }
 
 template <bool AR, bool VX>
-const void* pick_loss_tp(int loss, int mt) {
+const void* pick_loss_tp(int loss, int mt, bool st) {
   switch (loss) {
-    case kLossCEIndex: return pick_mt<kLossCEIndex, AR, VX>(mt);
-    case kLossMSE: return pick_mt<kLossMSE, AR, VX>(mt);
-    default: return pick_mt<kLossCESoft, AR, VX>(mt);
+    case kLossCEIndex: return pick_mt<kLossCEIndex, AR, VX>(mt, st);
+    case kLossMSE: return pick_mt<kLossMSE, AR, VX>(mt, st);
+    default: return pick_mt<kLossCESoft, AR, VX>(mt, st);
   }
 }
 
@@ -770,8 +789,10 @@ hipError_t mlp_tp_prepare(const FusedMlpArgs& a, const PersistArgs& p, PersistLa
   if (!mlp_tp_supported(a, p)) return hipErrorInvalidValue;
   const int mt = tp_mt(a);
   const bool vx = tp_vec_x(a);
-  const void* fn = a.ar.world > 1 ? (vx ? pick_loss_tp<true, true>(a.loss_kind, mt) : pick_loss_tp<true, false>(a.loss_kind, mt))
-                                  : (vx ? pick_loss_tp<false, true>(a.loss_kind, mt) : pick_loss_tp<false, false>(a.loss_kind, mt));
+  const bool st = p.stamps != nullptr;
+  const void* fn = a.ar.world > 1
+                       ? (vx ? pick_loss_tp<true, true>(a.loss_kind, mt, st) : pick_loss_tp<true, false>(a.loss_kind, mt, st))
+                       : (vx ? pick_loss_tp<false, true>(a.loss_kind, mt, st) : pick_loss_tp<false, false>(a.loss_kind, mt, st));
   const size_t lds = tp_lds_bytes(a, p);
   if (lds > 64 * 1024) PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   out->fn = fn;
