@@ -204,6 +204,7 @@ PersistBuild build_persistent(const Tensor& X, const c10::optional<Tensor>& Yf, 
   if (stamps.has_value() && stamps->defined()) {
     TORCH_CHECK(stamps->is_cuda() && stamps->scalar_type() == at::kLong && stamps->numel() >= 9, "stamps: int64[9]");
     pa.stamps = stamps->data_ptr<int64_t>();
+    pa.stamps_n = (int)stamps->numel();
   }
   pa.variant = (int)variant;
   pa.cursor_host_pos = -1;

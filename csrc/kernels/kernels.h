@@ -70,6 +70,7 @@ struct PersistArgs {
   uint64_t seed;
   int32_t* cursor;       // device [epoch, step_in_epoch]; advanced by the kernel
   float* losses;         // [n_steps] per-step mean loss
+  int stamps_n;          // elements of stamps (the TP engine adds per-wave barrier waits at [9 + w])
   int64_t* stamps;       // optional [9] diagnostic phase timers (s_memtime cycles, thread 0): prefetch issue,
                          // forward, loss, backward, all-reduce, sgd+land, epoch indices, total, realtime (100 MHz)
   int variant;           // kPersistAuto / kPersistWorkgroup / kPersistWave...

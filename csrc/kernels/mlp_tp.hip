@@ -207,8 +207,10 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   // lagging wave may still read (position P's and P+1's epochs)
   int* const elist = reinterpret_cast<int*>(lds);
   float* const stage0 = lds + 3 * d.estride;                 // [3] staged batches (TpStage)
-  float* const xbuf = stage0 + 3 * St::FLOATS;               // [2][NW][64][8] partial logits
+  float* const xbuf = stage0 + 3 * St::FLOATS;               // [2][NW][2 tiles][64 lanes][4] partial logits
   float* const wbase = xbuf + 2 * NW * 64 * 8 + tp_wave_floats() * w;
+  // Feistel keys of epochs e (slot e & 3: key[4], mask, half, n, epoch), after the wave regions
+  int* const fkeys = reinterpret_cast<int*>(xbuf + 2 * NW * 64 * 8 + tp_wave_floats() * NW);
   float* const W2m = wbase;                                   // [16 classes][LD2] W2[:, slice] (fwd layout)
   float* const Th = W2m + 16 * LD2;                           // [16 units][LDT] H^T of this slice
   float* const Tdz = Th + 16 * LDT;                           // [16 classes][LDT] dZ^T
@@ -242,6 +244,32 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       list(e0 + 1)[i] = v;
     }
   }
+  // Feistel keys of the epochs the producer will need (computed by one thread, one
+  // epoch ahead of use: a produce call reads te, te + 1 and prepares te + 2)
+  const bool feistel = pa.idx == nullptr && pa.shuffle;
+  auto keys_store = [&](int e) {
+    int* const k = fkeys + (e & 3) * 8;
+    FeistelPerm fp;
+    fp.init(pa.seed, e, Nn);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) k[r] = (int)fp.key[r];
+    k[4] = (int)fp.mask;
+    k[5] = fp.half;
+    k[6] = (int)fp.n;
+    k[7] = e;
+  };
+  auto keys_load = [&](int e) {
+    const int* const k = fkeys + (e & 3) * 8;
+    FeistelPerm fp;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) fp.key[r] = (uint32_t)k[r];
+    fp.mask = (uint32_t)k[4];
+    fp.half = k[5];
+    fp.n = (uint32_t)k[6];
+    return fp;
+  };
+  if (feistel && tid == 0)
+    for (int e = e0 + 1; e <= e0 + 3; ++e) keys_store(e);
   // staged batch slots: zeros, and the constant-1 input column (b1 rides in W1's
   // column Din) in X and X^T; the per-step writes only touch columns < Din
   const float one = hb ? 1.f : 0.f;
@@ -262,9 +290,20 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   // computed whole by a prologue); three LDS slots keep any produced epoch clear of
   // the epochs still read (positions P and P+1).
   const int C = min(8, S);
-  auto produce = [&](int te, int tj) {  // positions (te, tj) .. + C - 1
+  const int o0 = tid / B, r0 = tid - o0 * B;  // this thread's first chunk entry (position offset, row)
+  auto produce = [&](int te, int tj) {  // positions (te, tj) .. + C - 1: they span epochs te, te + 1
+    FeistelPerm fa, fb;
+    if (feistel) {
+      fa = keys_load(te);
+      fb = keys_load(te + 1);
+      if (tid == 0 && fkeys[((te + 2) & 3) * 8 + 7] != te + 2) keys_store(te + 2);
+    }
     for (int idx = tid; idx < C * B; idx += T) {
-      const int o = idx / B, r = idx - o * B;
+      int o = o0, r = r0;
+      if (idx != tid) {  // only when the chunk outnumbers the threads (small workgroups)
+        o = idx / B;
+        r = idx - o * B;
+      }
       int J = tj + o, E = te;
       if (J >= S) {
         J -= S;
@@ -275,10 +314,8 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       int v;
       if (pa.idx != nullptr) {
         v = given_list(pa, E)[i];
-      } else if (pa.shuffle) {
-        FeistelPerm fp;
-        fp.init(pa.seed, E, Nn);
-        v = (int)fp(rank_pos(i));
+      } else if (feistel) {
+        v = (int)(E == te ? fa : fb)(rank_pos(i));
       } else {
         v = (int)rank_pos(i);
       }
@@ -317,26 +354,35 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   }
   f4 xv[KX];
   float yv[KY];
-  auto stage_issue = [&](int E, int J) {
+  // the dataset rows of a position's items, read from the LDS list one step before
+  // their loads are issued (after a barrier: the producer's writes are visible)
+  int xsel[KX], ysel[KY];
+  auto stage_sel = [&](int E, int J) {
     const int nb = min(B, ns - J * B);
     const int* const li = list(E) + J * B;
 #pragma unroll
+    for (int k = 0; k < KX; ++k)
+      if (k < nkx) xsel[k] = li[min(xrow[k], nb - 1)];
+#pragma unroll
+    for (int k = 0; k < KY; ++k)
+      if (k < nky) ysel[k] = li[min(yrow[k], nb - 1)];
+  };
+  auto stage_issue = [&]() {
+#pragma unroll
     for (int k = 0; k < KX; ++k) {
       if (k < nkx) {
-        const int sel = li[min(xrow[k], nb - 1)];
         if constexpr (VX) {
-          xv[k] = *reinterpret_cast<const f4*>(a.X + (int64_t)sel * ldx + 4 * xcol[k]);
+          xv[k] = *reinterpret_cast<const f4*>(a.X + (int64_t)xsel[k] * ldx + 4 * xcol[k]);
         } else {
-          xv[k][0] = X[(int64_t)sel * ldx + xcol[k]];
+          xv[k][0] = X[(int64_t)xsel[k] * ldx + xcol[k]];
         }
       }
     }
 #pragma unroll
     for (int k = 0; k < KY; ++k) {
       if (k < nky) {
-        const int sel = li[min(yrow[k], nb - 1)];
-        if constexpr (YI) yv[k] = __int_as_float((int)gptr(a.Yi)[sel]);
-        else yv[k] = gptr(a.Yf)[(int64_t)sel * Dout + ycol[k]];
+        if constexpr (YI) yv[k] = __int_as_float((int)gptr(a.Yi)[ysel[k]]);
+        else yv[k] = gptr(a.Yf)[(int64_t)ysel[k] * Dout + ycol[k]];
       }
     }
   };
@@ -396,9 +442,14 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   bool failed = AR && *a.ar.err != 0;
 
   // position of step 0 staged synchronously
-  stage_issue(e0, j0);
+  stage_sel(e0, j0);
+  stage_issue();
   stage_write(0);
   __syncthreads();
+  {  // the rows of position 1 (epoch e0 + 1's list is filled up to batch j0)
+    const bool w1 = j0 + 1 == S;
+    stage_sel(w1 ? e0 + 1 : e0, w1 ? 0 : j0 + 1);
+  }
 
   float* const losses = pa.losses;
   // last step's (averaged) gradients, written to the DDP bucket at the end
@@ -415,7 +466,8 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   int pc = 0;            // steps until the next production chunk
   constexpr bool stamps = ST;  // s_memtime is scalar: every wave times, thread 0 reports
   int64_t tmark = stamps ? (int64_t)__builtin_amdgcn_s_memtime() : 0;
-  int64_t acc_t[6] = {0, 0, 0, 0, 0, 0};
+  int64_t acc_t[7] = {0, 0, 0, 0, 0, 0, 0};
+  int64_t acc_bar = 0;
   const int64_t t_begin = tmark, r_begin = stamps ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   auto tick = [&](int ph) {
     if (stamps) {
@@ -430,13 +482,14 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     const int ne = wrap ? ce + 1 : ce, nj = wrap ? 0 : cj + 1;
     const int sn = sc == 2 ? 0 : sc + 1;
     const int nb = min(B, ns - cj * B);
-    stage_issue(ne, nj);  // stale-but-valid past the launch
+    stage_issue();  // position k + 1 (rows read last step); stale-but-valid past the launch
+    tick(0);
     if (pc == 0) {
       produce(wrap ? ce + 2 : ce + 1, wrap ? 0 : cj + 1);
       pc = C;
     }
     --pc;
-    tick(0);
+    tick(6);
     const float* const st = stage(sc);
 
     // ---------------- fwd1: HT = W1aug . Xaug^T (this wave's 16 units x 32 rows), ReLU
@@ -465,9 +518,10 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       z[1] = mfma4(a2[s], ht[1][s], z[1]);
     }
     {
-      f4* dst = reinterpret_cast<f4*>(xbuf + ((par * NW + w) * 64 + l) * 8);
+      // tile-major planes: consecutive lanes read consecutive 16 B (no bank conflicts)
+      f4* dst = reinterpret_cast<f4*>(xbuf + (par * NW + w) * 512 + l * 4);
       dst[0] = z[0];
-      dst[1] = z[1];
+      dst[64] = z[1];
     }
     // H^T of the slice for the backward's transposed reads (wave-private)
 #pragma unroll
@@ -477,19 +531,39 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     stage_write(sn);
     tick(1);
     __syncthreads();
+    {  // the rows of position k + 2 (its list entries were produced before this barrier)
+      const bool w2 = nj + 1 == S;
+      stage_sel(w2 ? ne + 1 : ne, w2 ? 0 : nj + 1);
+    }
+    if constexpr (ST) {  // the barrier alone (per wave, stamps[13 + w])
+      const int64_t t = (int64_t)__builtin_amdgcn_s_memtime();
+      acc_bar += t - tmark;
+      tmark = t;
+    }
     float zf[2][4];
     const f4 b2v = *reinterpret_cast<const f4*>(B2m + 4 * q);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) zf[t][i] = b2v[i];
-    for (int v = 0; v < NW; ++v) {  // wave order: identical sums in every wave
-      const f4* src = reinterpret_cast<const f4*>(xbuf + ((par * NW + v) * 64 + l) * 8);
-      const f4 p0 = src[0], p1 = src[1];
+    // all partial reads in flight before the first add (a runtime-count loop waited on each)
+    f4 pz[4][2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        zf[0][i] += p0[i];
-        zf[1][i] += p1[i];
+    for (int v = 0; v < 4; ++v) {
+      if (v < NW) {
+        const f4* src = reinterpret_cast<const f4*>(xbuf + (par * NW + v) * 512 + l * 4);
+        pz[v][0] = src[0];
+        pz[v][1] = src[64];
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {  // wave order: identical sums in every wave
+      if (v < NW) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          zf[0][i] += pz[v][0][i];
+          zf[1][i] += pz[v][1][i];
+        }
       }
     }
     tick(2);
@@ -520,11 +594,11 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         float se = 0.f, e[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          e[i] = (4 * q + i < Dout) ? __expf(zf[t][i] - m) : 0.f;
+          e[i] = (4 * q + i < Dout) ? __builtin_amdgcn_exp2f((zf[t][i] - m) * 1.4426950408889634f) : 0.f;
           se += e[i];
         }
         se = rows4_sum(se);
-        const float rse = 1.f / se;  // softmax = e / se; the log only feeds the reported loss
+        const float rse = __builtin_amdgcn_rcpf(se);  // softmax = e / se (v_rcp_f32); the log only feeds the loss
         if constexpr (LOSS == kLossCEIndex) {
           const int y = reinterpret_cast<const int*>(ys)[row];
           const bool use = rv && y != a.ignore_index;
@@ -730,11 +804,15 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     if (use_mom) a.mom[d.ob2 + c] = mb2c;
     if (have) Gw[d.ob2 + c] = ldb2;
   }
+  if (stamps && l == 0 && pa.stamps_n >= 13 + NW) {  // each wave's logit-sum phase and barrier wait
+    pa.stamps[9 + w] += acc_t[2];
+    pa.stamps[13 + w] += acc_bar;
+  }
   if (tid == 0) {
     pa.cursor[0] = ce;
     pa.cursor[1] = cj;
     if (stamps) {  // [0] stage issue+produce [1] fwd [2] barrier+sum [3] loss [4] bwd MFMA [5] all-reduce+SGD
-      for (int k = 0; k < 6; ++k) pa.stamps[k] += acc_t[k];
+      for (int k = 0; k < 7; ++k) pa.stamps[k] += acc_t[k];
       pa.stamps[7] += (int64_t)__builtin_amdgcn_s_memtime() - t_begin;
       pa.stamps[8] += (int64_t)__builtin_amdgcn_s_memrealtime() - r_begin;
     }
@@ -770,7 +848,7 @@ bool tp_vec_x(const FusedMlpArgs& a) {
 size_t tp_lds_bytes(const FusedMlpArgs& a, const PersistArgs& p) {
   const int NW = a.H / 16;
   const size_t fl = (size_t)3 * al4(p.num_samples) + (size_t)3 * tp_stage_floats(tp_mt(a)) +
-                    (size_t)2 * NW * 64 * 8 + (size_t)NW * tp_wave_floats();
+                    (size_t)2 * NW * 64 * 8 + (size_t)NW * tp_wave_floats() + 32;
   return fl * sizeof(float);
 }
 
