@@ -264,7 +264,7 @@ def run_persistent(args, rank, world, dev, comm):
     in_sync = _replicas_in_sync(comm, eng.P)
     phase = None
     if args.stamps:  # diagnostic pass AFTER the timed region (timers cost a little)
-        st = torch.zeros(17, dtype=torch.int64, device=dev)
+        st = torch.zeros(32, dtype=torch.int64, device=dev)
         eng.run_persistent(X, Y, args.steps, args.batch_size, sampler, cursor, losses, chunk, stamps=st,
                            variant=variant)
         v = st.tolist()
@@ -276,9 +276,9 @@ def run_persistent(args, rank, world, dev, comm):
         phase = {"cycles_per_step": {n: round(v[k] / args.steps, 1) for k, n in enumerate(names)},
                  "total_cycles_per_step": round(v[7] / args.steps, 1), "clock_GHz": round(clk / 1e9, 3)}
         if which.startswith("tp"):  # each wave's barrier + logit-sum phase (load balance)
-            nw = int(which[3])
+            nw = int(which.split(":")[1].split("w")[0])
             phase["logit_sum_per_wave"] = [round(x / args.steps, 1) for x in v[9:9 + nw]]
-            phase["barrier_wait_per_wave"] = [round(x / args.steps, 1) for x in v[13:13 + nw]]
+            phase["barrier_wait_per_wave"] = [round(x / args.steps, 1) for x in v[9 + nw:9 + 2 * nw]]
     last = (args.steps - 1) % chunk
     extra = {"replicas_in_sync": in_sync, "steps_per_epoch": S, "launches_timed": math.ceil(args.steps / chunk),
              "sampler": ("torch.randperm-identical DistributedSampler order (torch_perm kernel in the timed region)"
