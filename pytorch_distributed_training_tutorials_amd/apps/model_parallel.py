@@ -90,6 +90,9 @@ def benchmark(repeat: int = 10, devs=("cuda:0", "cuda:1"), split_sizes=(20,), ch
               "Single GPU": lambda: cl(resnet50(num_classes=NUM_CLASSES).to(devs[0]))}
     for ss in split_sizes:
         setups[f"Pipeline split={ss}"] = (lambda ss=ss: cl(PipelineParallelResNet50(ss, NUM_CLASSES, devs[0], devs[1])))
+        if devs[0] != devs[1]:  # stage streams: two GPUs only
+            setups[f"Pipeline split={ss} stage streams"] = (
+                lambda ss=ss: cl(PipelineParallelResNet50(ss, NUM_CLASSES, devs[0], devs[1], streams=True)))
     for name, mk in setups.items():
         model = mk()
         in_dev = torch.device(devs[0])

@@ -210,3 +210,28 @@ def test_mp_resnet50_two_gpus_train_step_matches_single_gpu():
     torch.testing.assert_close(mp.fc.weight.detach().cpu(), ref.fc.weight.detach().cpu(), rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(mp.conv1.weight.detach().cpu(), ref.conv1.weight.detach().cpu(), rtol=1e-4,
                                atol=1e-6)
+
+
+@needs(2)
+def test_stream_pipeline_two_gpus_matches_single_queue_pipeline():
+    """Stage streams across cuda:0/cuda:1 (stage 0 of micro-batch i+1 overlapping stage 1
+    of micro-batch i, backward on the forward's streams) compute the same training step
+    as the reference's single-queue pipeline schedule."""
+    from pytorch_distributed_training_tutorials_amd.models.mp_resnet import PipelineParallelResNet50
+
+    torch.manual_seed(3)
+    a = PipelineParallelResNet50(split_size=4, num_classes=10, dev0="cuda:0", dev1="cuda:1", streams=True)
+    b = PipelineParallelResNet50(split_size=4, num_classes=10, dev0="cuda:0", dev1="cuda:1", streams=False)
+    b.load_state_dict(a.state_dict())
+    x = torch.randn(12, 3, 64, 64, device="cuda:0")
+    outs = []
+    for m in (a, b):
+        m.train()
+        y = m(x)
+        y.square().mean().backward()
+        torch.cuda.synchronize("cuda:0")
+        torch.cuda.synchronize("cuda:1")
+        outs.append((y.detach().cpu(), [p.grad.detach().cpu() for p in m.parameters()]))
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-4, atol=1e-5)
+    for ga, gb in zip(outs[0][1], outs[1][1]):
+        torch.testing.assert_close(ga, gb, rtol=1e-3, atol=1e-5)
