@@ -730,6 +730,67 @@ Tensor int8_linear(Tensor x, Tensor q, Tensor scale, c10::optional<Tensor> bias)
   return y;
 }
 
+// LLM.int8 pieces
+Tensor int8_col_outliers_(Tensor x, double threshold) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "int8_col_outliers: contiguous [M, K]");
+  c10::hip::HIPGuard guard(x.device().index());
+  Tensor mask = at::empty({x.size(1)}, x.options().dtype(at::kByte));
+  hip_check(int8_col_outliers(x.data_ptr(), dt_of(x), (int)x.size(0), (int)x.size(1), (float)threshold,
+                              mask.data_ptr<uint8_t>(), cur_stream(x)),
+            "int8_col_outliers");
+  return mask;
+}
+
+std::vector<Tensor> int8_quant_rows_(Tensor x, c10::optional<Tensor> mask) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "int8_quant_rows: contiguous [M, K]");
+  const uint8_t* mp = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->numel() == x.size(1) && mask->is_cuda());
+    mp = mask->data_ptr<uint8_t>();
+  }
+  c10::hip::HIPGuard guard(x.device().index());
+  Tensor q = at::empty(x.sizes(), x.options().dtype(at::kChar));
+  Tensor s = at::empty({x.size(0)}, x.options().dtype(at::kFloat));
+  hip_check(int8_quant_rows(x.data_ptr(), dt_of(x), (int)x.size(0), (int)x.size(1), mp, q.data_ptr<int8_t>(),
+                            s.data_ptr<float>(), cur_stream(x)),
+            "int8_quant_rows");
+  return {q, s};
+}
+
+Tensor int8_mm_(Tensor A, Tensor sa, Tensor B, Tensor sb, c10::optional<Tensor> addend, c10::optional<Tensor> bias,
+                bool out_bf16) {
+  check_gpu(A, "A");
+  check_gpu(B, "B");
+  TORCH_CHECK(A.scalar_type() == at::kChar && B.scalar_type() == at::kChar && A.dim() == 2 && B.dim() == 2 &&
+                  A.is_contiguous() && B.is_contiguous() && A.size(1) == B.size(1),
+              "int8_mm: contiguous int8 A[M,K], B[N,K]");
+  const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
+  TORCH_CHECK(K % 16 == 0, "int8_mm: K must be a multiple of 16");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(A.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(B.data_ptr()) % 16 == 0,
+              "int8_mm: 16-byte aligned operands");
+  TORCH_CHECK(sa.scalar_type() == at::kFloat && sa.numel() == M && sb.scalar_type() == at::kFloat && sb.numel() == N);
+  const float* ad = nullptr;
+  if (addend.has_value() && addend->defined()) {
+    TORCH_CHECK(addend->scalar_type() == at::kFloat && addend->is_contiguous() && addend->numel() == M * N);
+    ad = addend->data_ptr<float>();
+  }
+  const void* bp = nullptr;
+  int bias_bf16 = 0;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->numel() == N && (bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16));
+    bp = bias->data_ptr();
+    bias_bf16 = bias->scalar_type() == at::kBFloat16;
+  }
+  c10::hip::HIPGuard guard(A.device().index());
+  Tensor y = at::empty({M, N}, A.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  hip_check(int8_mm(A.data_ptr<int8_t>(), sa.data_ptr<float>(), B.data_ptr<int8_t>(), sb.data_ptr<float>(), ad, bp,
+                    bias_bf16, (int)M, (int)N, (int)K, y.data_ptr(), dt_of(y), cur_stream(A)),
+            "int8_mm");
+  return y;
+}
+
 Tensor bn_relu(Tensor x, Tensor scale, Tensor shift, bool relu) {
   check_gpu(x, "x");
   TORCH_CHECK(x.dim() >= 2);
@@ -1068,6 +1129,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("device_sampler_", &device_sampler_);
   m.def("quantize_int8", &quantize_int8);
   m.def("int8_linear", &int8_linear);
+  m.def("int8_col_outliers", &int8_col_outliers_, py::arg("x"), py::arg("threshold"));
+  m.def("int8_quant_rows", &int8_quant_rows_, py::arg("x"), py::arg("mask") = py::none());
+  m.def("int8_mm", &int8_mm_, py::arg("A"), py::arg("sa"), py::arg("B"), py::arg("sb"), py::arg("addend") = py::none(),
+        py::arg("bias") = py::none(), py::arg("out_bf16") = false);
   m.def("bn_relu", &bn_relu);
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("num_batches_tracked"), py::arg("residual"), py::arg("relu"),

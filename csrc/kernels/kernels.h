@@ -281,6 +281,15 @@ hipError_t int8_weight_gemm(const void* x, int x_dtype, const int8_t* q, const f
                             const void* bias, int M, int N, int K, void* y, int y_dtype,
                             hipStream_t s);
 
+// LLM.int8 (csrc/kernels/int8_mm.hip): outlier columns (|x| > threshold), row-wise
+// activation quantisation with them zeroed, int8 x int8 -> int32 MFMA GEMM with the
+// dequantisation, the caller's outlier product (addend, f32 [M,N]) and bias in the epilogue.
+hipError_t int8_col_outliers(const void* x, int dtype, int M, int K, float threshold, uint8_t* mask, hipStream_t s);
+hipError_t int8_quant_rows(const void* x, int dtype, int M, int K, const uint8_t* mask, int8_t* q, float* scale,
+                           hipStream_t s);
+hipError_t int8_mm(const int8_t* A, const float* sa, const int8_t* B, const float* sb, const float* addend,
+                   const void* bias, int bias_bf16, int M, int N, int K, void* y, int y_dtype, hipStream_t s);
+
 // BatchNorm(train stats applied) + ReLU fused epilogue over NCHW (csrc/kernels/elementwise.hip)
 hipError_t bn_relu_apply(const void* x, int dtype, const float* scale, const float* shift, int64_t N,
                          int64_t C, int64_t HW, int relu, void* y, hipStream_t s);

@@ -7,9 +7,16 @@ when moved to the GPU; RMSNorm, embeddings and lm_head stay in 16-bit.
 :class:`Int8Linear` stores ``weight_q`` (int8 ``[out, in]``) and per-row
 ``weight_scale`` (fp32); on GPU the forward is the native
 ``int8_weight_gemm`` kernel (int8 tile widened to bf16 in LDS, MFMA, scale in
-the fp32 epilogue -- 1 byte per weight read from HBM). bitsandbytes' fp16
-outlier decomposition is not reproduced: activations stay bf16/fp32, so no
-activation quantisation error exists to decompose.
+the fp32 epilogue -- 1 byte per weight read from HBM).
+
+``llm_int8=True`` reproduces bitsandbytes' LLM.int8 matmul instead: the input
+features with an activation above ``threshold`` (6.0, bitsandbytes' default) in
+the batch are outliers and stay in 16/32-bit against the dequantised weight
+columns; every other feature is quantised row-wise (absmax per token) to int8
+and multiplied int8 x int8 -> int32 on MFMA (``v_mfma_i32_16x16x64_i8``,
+csrc/kernels/int8_mm.hip), dequantised in the epilogue where the outlier product
+and the bias are added. (Gathering the outlier columns reads their indices on
+the host, as bitsandbytes does.)
 """
 from __future__ import annotations
 
@@ -30,10 +37,32 @@ def quantize_rowwise(w: torch.Tensor):
     return q, scale
 
 
+def llm_int8_reference(x: torch.Tensor, q: torch.Tensor, scale: torch.Tensor, bias: torch.Tensor | None,
+                       threshold: float) -> torch.Tensor:
+    """The LLM.int8 product in plain PyTorch (fp32 math, exact int32 products):
+    the CPU path and the numerics reference of the native kernels."""
+    xf = x.float()
+    out_cols = xf.abs().amax(dim=0) > threshold
+    xin = xf.masked_fill(out_cols[None, :], 0.0)
+    amax = xin.abs().amax(dim=1)
+    sx = torch.where(amax > 0, amax / 127.0, torch.ones_like(amax))
+    xq = torch.clamp(torch.round(xin / sx[:, None]), -127, 127)
+    prod = (xq.long().cpu() @ q.long().cpu().t()).to(torch.float32).to(x.device)
+    y = prod * sx[:, None] * scale.float()[None, :]
+    if bool(out_cols.any()):
+        wdq = q[:, out_cols].float() * scale.float()[:, None]
+        y = y + xf[:, out_cols] @ wdq.t()
+    if bias is not None:
+        y = y + bias.float()
+    return y.to(x.dtype)
+
+
 class Int8Linear(nn.Module):
-    def __init__(self, in_features: int, out_features: int, bias: bool = True, dtype=torch.bfloat16, device=None):
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, dtype=torch.bfloat16, device=None,
+                 llm_int8: bool = False, threshold: float = 6.0):
         super().__init__()
         self.in_features, self.out_features = in_features, out_features
+        self.llm_int8, self.threshold = llm_int8, float(threshold)
         self.register_buffer("weight_q", torch.zeros(out_features, in_features, dtype=torch.int8, device=device))
         self.register_buffer("weight_scale", torch.ones(out_features, dtype=torch.float32, device=device))
         if bias:
@@ -42,9 +71,9 @@ class Int8Linear(nn.Module):
             self.bias = None
 
     @classmethod
-    def from_linear(cls, lin: nn.Linear) -> "Int8Linear":
+    def from_linear(cls, lin: nn.Linear, llm_int8: bool = False, threshold: float = 6.0) -> "Int8Linear":
         m = cls(lin.in_features, lin.out_features, lin.bias is not None, dtype=lin.weight.dtype,
-                device=lin.weight.device)
+                device=lin.weight.device, llm_int8=llm_int8, threshold=threshold)
         q, s = quantize_rowwise(lin.weight.detach())
         m.weight_q.copy_(q)
         m.weight_scale.copy_(s)
@@ -55,9 +84,26 @@ class Int8Linear(nn.Module):
     def dequantized_weight(self) -> torch.Tensor:
         return self.weight_q.float() * self.weight_scale[:, None]
 
+    def _llm_int8(self, x2: torch.Tensor) -> torch.Tensor:
+        C = native()
+        b = self.bias
+        if not (use_native(x2) and x2.dtype in (torch.float32, torch.bfloat16) and self.in_features % 16 == 0):
+            return llm_int8_reference(x2, self.weight_q, self.weight_scale, b, self.threshold)
+        x2 = x2.contiguous()
+        mask = C.int8_col_outliers(x2, self.threshold)
+        cols = mask.nonzero().flatten()  # host read: usually a handful of features
+        xq, sx = C.int8_quant_rows(x2, mask if cols.numel() else None)
+        addend = None
+        if cols.numel():
+            wdq = self.weight_q.index_select(1, cols).float() * self.weight_scale[:, None]
+            addend = (x2.index_select(1, cols).float() @ wdq.t()).contiguous()
+        return C.int8_mm(xq, sx, self.weight_q, self.weight_scale, addend, b, x2.dtype == torch.bfloat16)
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
+        if self.llm_int8:
+            return self._llm_int8(x2).reshape(*shape[:-1], self.out_features)
         if use_native(x2) and x2.dtype in (torch.float32, torch.bfloat16):
             b = self.bias if self.bias is None or self.bias.dtype == x2.dtype else self.bias.to(x2.dtype)
             y = native().int8_linear(x2.contiguous(), self.weight_q, self.weight_scale, b)
@@ -68,14 +114,16 @@ class Int8Linear(nn.Module):
         return y.reshape(*shape[:-1], self.out_features)
 
     def extra_repr(self) -> str:
-        return f"in_features={self.in_features}, out_features={self.out_features}, int8 row-wise"
+        mode = f"LLM.int8 threshold={self.threshold}" if self.llm_int8 else "int8 row-wise weights"
+        return f"in_features={self.in_features}, out_features={self.out_features}, {mode}"
 
 
-def quantize_int8_(model: nn.Module, skip=("lm_head",)) -> nn.Module:
-    """Replace every ``nn.Linear`` (except names ending in ``skip``) by Int8Linear, in place."""
+def quantize_int8_(model: nn.Module, skip=("lm_head",), llm_int8: bool = False, threshold: float = 6.0) -> nn.Module:
+    """Replace every ``nn.Linear`` (except names ending in ``skip``) by Int8Linear, in place
+    (``llm_int8``: bitsandbytes' LLM.int8 matmul with outlier decomposition)."""
     for name, mod in list(model.named_modules()):
         for cname, child in list(mod.named_children()):
             full = f"{name}.{cname}" if name else cname
             if isinstance(child, nn.Linear) and not any(full.endswith(s) for s in skip):
-                setattr(mod, cname, Int8Linear.from_linear(child))
+                setattr(mod, cname, Int8Linear.from_linear(child, llm_int8=llm_int8, threshold=threshold))
     return model

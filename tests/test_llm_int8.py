@@ -1,0 +1,73 @@
+"""LLM.int8 (bitsandbytes' load_in_8bit matmul; reference NB03:52-56):
+outlier features in 16/32-bit, the rest int8 x int8 -> int32 on MFMA."""
+import pytest
+import torch
+
+
+def _lin(K=64, N=48, seed=0):
+    torch.manual_seed(seed)
+    return torch.nn.Linear(K, N)
+
+
+def test_llm_int8_reference_cpu_tracks_fp32_and_handles_outliers():
+    from pytorch_distributed_training_tutorials_amd.ops.quant import Int8Linear
+
+    lin = _lin()
+    m = Int8Linear.from_linear(lin, llm_int8=True, threshold=6.0)
+    x = torch.randn(9, 64)
+    x[:, 5] *= 40.0  # an outlier feature: kept out of the int8 product
+    y, ref = m(x), lin(x)
+    assert (y - ref).abs().max() <= 0.02 * ref.abs().max()
+    # without the decomposition the outlier column would dominate every row's absmax
+    m_plain = Int8Linear.from_linear(lin, llm_int8=True, threshold=1e9)
+    assert (m_plain(x) - ref).abs().max() > 2 * (y - ref).abs().max()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(70, 50, 128), (64, 64, 64), (5, 130, 48), (129, 17, 256)])
+def test_int8_mm_exact_integer_products(dev, M, N, K):
+    """v_mfma_i32_16x16x64_i8 operand map: exact int32 products (scales 1, f32 out)."""
+    from pytorch_distributed_training_tutorials_amd._ext import native
+
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randint(-127, 128, (M, K), generator=g, dtype=torch.int8)
+    B = torch.randint(-127, 128, (N, K), generator=g, dtype=torch.int8)
+    ref = (A.long() @ B.long().t()).float()
+    y = native().int8_mm(A.to(dev), torch.ones(M, device=dev), B.to(dev), torch.ones(N, device=dev))
+    assert torch.equal(y.cpu(), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("outliers", [0, 3])
+def test_llm_int8_linear_matches_reference(dev, dtype, outliers):
+    from pytorch_distributed_training_tutorials_amd.ops.quant import Int8Linear, llm_int8_reference
+
+    lin = _lin(K=256, N=96, seed=outliers).to(dev).to(dtype)
+    m = Int8Linear.from_linear(lin, llm_int8=True)
+    x = torch.randn(4, 33, 256, device=dev, dtype=dtype)
+    for j in range(outliers):
+        x[..., 7 + 50 * j] *= 30.0
+    y = m(x)
+    ref = llm_int8_reference(x.reshape(-1, 256), m.weight_q, m.weight_scale, m.bias, m.threshold).reshape(y.shape)
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(y, ref, **tol)
+    full = lin(x).float()
+    assert (y.float() - full).abs().max() <= 0.03 * full.abs().max()
+
+
+@pytest.mark.gpu
+def test_tiny_llama_llm_int8_logits_track_bf16(dev):
+    """load_in_8bit-style model: every projection LLM.int8 (lm_head kept 16-bit)."""
+    from pytorch_distributed_training_tutorials_amd.models.llama import build_llama
+    from pytorch_distributed_training_tutorials_amd.ops.quant import Int8Linear, quantize_int8_
+
+    ref = build_llama("tiny", dtype=torch.float32).to(dev).eval()
+    q = build_llama("tiny", dtype=torch.float32).to(dev).eval()
+    quantize_int8_(q, llm_int8=True)
+    n8 = sum(isinstance(m, Int8Linear) for m in q.modules())
+    assert n8 == 7 * 4 and q.lm_head.weight.dtype == torch.float32
+    ids = torch.randint(0, 512, (2, 24), device=dev)
+    with torch.no_grad():
+        a, b = ref(ids).logits, q(ids).logits
+    assert (a - b).norm() <= 0.05 * a.norm()
