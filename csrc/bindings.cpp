@@ -1268,6 +1268,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("rank", &XgmiComm::rank)
       .def_property_readonly("world", &XgmiComm::world)
       .def_property_readonly("max_elems", &XgmiComm::max_elems)
+      .def_property("max_polls", &XgmiComm::max_polls, &XgmiComm::set_max_polls)
       .def("error", &XgmiComm::error)
       .def("reset_error", &XgmiComm::reset_error)
       .def("all_reduce_avg", [](XgmiComm& c, Tensor t) {

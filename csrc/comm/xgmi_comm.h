@@ -33,6 +33,10 @@ class XgmiComm {
   int rank() const { return args_.rank; }
   int world() const { return args_.world; }
   int max_elems() const { return args_.max_elems; }
+  // poll budget of later launches (the self-test runs with the full budget whatever
+  // PTDT_XGMI_MAX_POLLS says; fault-injection tests shorten it for the training)
+  uint32_t max_polls() const { return args_.max_polls; }
+  void set_max_polls(uint32_t n) { args_.max_polls = n == 0u ? 1u : n; }
 
  private:
   XgmiArgs args_{};

@@ -209,7 +209,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   float* const stage0 = lds + 3 * d.estride;                 // [3] staged batches (TpStage)
   float* const xbuf = stage0 + 3 * St::FLOATS;               // [2][NW][2 tiles][64 lanes][4] partial logits
   float* const wbase = xbuf + 2 * NW * 64 * 8 + tp_wave_floats() * w;
-  // Feistel keys of epochs e (slot e & 3: key[4], mask, half, n, epoch), after the wave regions
+  // Feistel keys of epochs e (slot e & 3, 12 ints: key[4], maskL, maskR, hb, n, epoch), after the wave regions
   int* const fkeys = reinterpret_cast<int*>(xbuf + 2 * NW * 64 * 8 + tp_wave_floats() * NW);
   float* const W2m = wbase;                                   // [16 classes][LD2] W2[:, slice] (fwd layout)
   float* const Th = W2m + 16 * LD2;                           // [16 units][LDT] H^T of this slice
@@ -248,24 +248,26 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   // epoch ahead of use: a produce call reads te, te + 1 and prepares te + 2)
   const bool feistel = pa.idx == nullptr && pa.shuffle;
   auto keys_store = [&](int e) {
-    int* const k = fkeys + (e & 3) * 8;
+    int* const k = fkeys + (e & 3) * 12;
     FeistelPerm fp;
     fp.init(pa.seed, e, Nn);
 #pragma unroll
     for (int r = 0; r < 4; ++r) k[r] = (int)fp.key[r];
-    k[4] = (int)fp.mask;
-    k[5] = fp.half;
-    k[6] = (int)fp.n;
-    k[7] = e;
+    k[4] = (int)fp.maskL;
+    k[5] = (int)fp.maskR;
+    k[6] = fp.hb;
+    k[7] = (int)fp.n;
+    k[8] = e;
   };
   auto keys_load = [&](int e) {
-    const int* const k = fkeys + (e & 3) * 8;
+    const int* const k = fkeys + (e & 3) * 12;
     FeistelPerm fp;
 #pragma unroll
     for (int r = 0; r < 4; ++r) fp.key[r] = (uint32_t)k[r];
-    fp.mask = (uint32_t)k[4];
-    fp.half = k[5];
-    fp.n = (uint32_t)k[6];
+    fp.maskL = (uint32_t)k[4];
+    fp.maskR = (uint32_t)k[5];
+    fp.hb = k[6];
+    fp.n = (uint32_t)k[7];
     return fp;
   };
   if (feistel && tid == 0)
@@ -296,7 +298,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     if (feistel) {
       fa = keys_load(te);
       fb = keys_load(te + 1);
-      if (tid == 0 && fkeys[((te + 2) & 3) * 8 + 7] != te + 2) keys_store(te + 2);
+      if (tid == 0 && fkeys[((te + 2) & 3) * 12 + 8] != te + 2) keys_store(te + 2);
     }
     for (int idx = tid; idx < C * B; idx += T) {
       int o = o0, r = r0;
@@ -848,7 +850,7 @@ bool tp_vec_x(const FusedMlpArgs& a) {
 size_t tp_lds_bytes(const FusedMlpArgs& a, const PersistArgs& p) {
   const int NW = a.H / 16;
   const size_t fl = (size_t)3 * al4(p.num_samples) + (size_t)3 * tp_stage_floats(tp_mt(a)) +
-                    (size_t)2 * NW * 64 * 8 + (size_t)NW * tp_wave_floats() + 32;
+                    (size_t)2 * NW * 64 * 8 + (size_t)NW * tp_wave_floats() + 48;
   return fl * sizeof(float);
 }
 

@@ -20,32 +20,34 @@ __device__ __forceinline__ uint64_t feistel_splitmix64(uint64_t x) {
   return x ^ (x >> 31);
 }
 
+// Keyed 4-round Feistel bijection of [0, 2^bits), bits = ceil(log2 N), cycle-walked
+// into [0, N). Unbalanced split (L: bits - hb, R: hb = bits / 2 bits; the rounds
+// alternate L ^= F(R), R ^= F(L)) so the domain is the next power of two of N, not
+// the next even power: at most half the draws walk again (none for N = 2^k), which
+// bounds the divergence of a wave's cycle walks.
 struct FeistelPerm {
   uint32_t key[4];
-  uint32_t mask, n;
-  int half;
+  uint32_t maskL, maskR, n;
+  int hb;
   __device__ __forceinline__ void init(uint64_t seed, int epoch, uint32_t N) {
     n = N;
     int bits = 1;
     while ((1u << bits) < N) ++bits;
-    bits += bits & 1;
-    half = bits / 2;
-    mask = (1u << half) - 1u;
+    hb = bits / 2;
+    maskR = (1u << hb) - 1u;
+    maskL = (1u << (bits - hb)) - 1u;
     const uint64_t base = feistel_splitmix64(seed ^ feistel_splitmix64((uint64_t)epoch + 0x1234567ull));
 #pragma unroll
     for (int r = 0; r < 4; ++r) key[r] = (uint32_t)feistel_splitmix64(base + r);
   }
   __device__ __forceinline__ uint32_t operator()(uint32_t x) const {
     do {
-      uint32_t L = x >> half, R = x & mask;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const uint32_t F = feistel_mix32(R ^ key[r]) & mask;
-        const uint32_t nL = R;
-        R = L ^ F;
-        L = nL;
-      }
-      x = (L << half) | R;
+      uint32_t L = x >> hb, R = x & maskR;
+      L ^= feistel_mix32(R ^ key[0]) & maskL;
+      R ^= feistel_mix32(L ^ key[1]) & maskR;
+      L ^= feistel_mix32(R ^ key[2]) & maskL;
+      R ^= feistel_mix32(L ^ key[3]) & maskR;
+      x = (L << hb) | R;
     } while (x >= n);
     return x;
   }

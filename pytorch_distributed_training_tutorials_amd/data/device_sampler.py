@@ -58,9 +58,9 @@ def reference_indices(n: int, world: int, rank: int, epoch: int, seed: int = 0, 
     bits = 1
     while (1 << bits) < n:
         bits += 1
-    bits += bits & 1
-    half = bits // 2
-    mask = np.uint64((1 << half) - 1)
+    hb = bits // 2  # unbalanced split: L has bits - hb bits, R has hb
+    mask_r = np.uint64((1 << hb) - 1)
+    mask_l = np.uint64((1 << (bits - hb)) - 1)
     base = _splitmix64((seed ^ _splitmix64((epoch + 0x1234567) & _M64)) & _M64)
     keys = [np.uint64(_splitmix64((base + r) & _M64) & 0xFFFFFFFF) for r in range(4)]
     x = pos.astype(np.uint64)
@@ -68,12 +68,13 @@ def reference_indices(n: int, world: int, rank: int, epoch: int, seed: int = 0, 
     todo = np.ones(len(x), dtype=bool)
     cur = x.copy()
     while todo.any():
-        L = cur >> np.uint64(half)
-        R = cur & mask
-        for k in keys:
-            F = _mix32(R ^ k) & mask
-            L, R = R, L ^ F
-        cur = (L << np.uint64(half)) | R
+        L = cur >> np.uint64(hb)
+        R = cur & mask_r
+        L = L ^ (_mix32(R ^ keys[0]) & mask_l)
+        R = R ^ (_mix32(L ^ keys[1]) & mask_r)
+        L = L ^ (_mix32(R ^ keys[2]) & mask_l)
+        R = R ^ (_mix32(L ^ keys[3]) & mask_r)
+        cur = (L << np.uint64(hb)) | R
         done = todo & (cur < np.uint64(n))
         out[done] = cur[done]
         todo &= ~done

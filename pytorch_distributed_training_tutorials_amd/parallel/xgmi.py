@@ -56,6 +56,16 @@ class XgmiAllReduce:
         return min(self.comm.all_gather_object(int(v))) == 1
 
     def _self_test(self) -> bool:
+        # full poll budget (ranks may reach the test far apart, e.g. sharing one GPU),
+        # whatever shorter bound PTDT_XGMI_MAX_POLLS sets for the training launches
+        budget = self.x.max_polls
+        self.x.max_polls = 1 << 22  # kXgmiMaxPolls
+        try:
+            return self._self_test_body()
+        finally:
+            self.x.max_polls = budget
+
+    def _self_test_body(self) -> bool:
         for n in (1, 21, 1000, min(self.max_elems, 5000)):
             t = torch.full((n,), float(self.rank + 1), device=self.device)
             t += torch.arange(n, device=self.device, dtype=torch.float32) * 1e-3
