@@ -260,3 +260,20 @@ def test_force_collective_issues_bucket_allreduce_at_world_1(pg, dev, monkeypatc
         assert issued == (nb if force == "1" else 0), (force, issued, nb)
         grads.append(torch.cat([p.grad.reshape(-1) for p in ddp.module.parameters()]))
     torch.testing.assert_close(grads[0], grads[1], rtol=0, atol=0)
+
+
+def test_rccl_clique_single_device_collectives(dev):
+    """The single-process DataParallel transport (ncclCommInitAll clique, grouped
+    broadcast/reduce/all-reduce) on a one-GPU clique: the same calls DataParallel makes
+    over distinct GPUs (tests/test_multi_gpu.py covers 2-8 devices)."""
+    from pytorch_distributed_training_tutorials_amd._ext import native
+
+    cl = native().RcclClique([dev.index or 0])
+    assert cl.size == 1
+    t = torch.arange(1000, dtype=torch.float32, device=dev)
+    want = t.clone()
+    cl.broadcast([t], 0)
+    cl.reduce([t], 0)
+    cl.all_reduce([t])
+    torch.cuda.synchronize()
+    torch.testing.assert_close(t, want)
