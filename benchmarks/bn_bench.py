@@ -43,6 +43,7 @@ def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--native_only", action="store_true", help="skip the PyTorch composite arm")
     a = ap.parse_args()
     from pytorch_distributed_training_tutorials_amd.ops.norm import BatchNorm2d
 
@@ -64,12 +65,15 @@ def main():
             y = torch.relu(ref(xr) + rr)
             torch.autograd.grad(y, (xr, rr, ref.weight, ref.bias), g)
 
-        t_nat, t_ref = timed(native, a.iters), timed(composite, a.iters)
+        t_nat = timed(native, a.iters)
+        t_ref = float("nan") if a.native_only else timed(composite, a.iters)
         elem = x.numel() * x.element_size()
         min_bytes = elem * (4 + 7)  # fwd x,x,res,y; bwd dy,x,y,dy,x,y,dx (+dres below)
         min_bytes += elem  # d(residual)
         print(json.dumps({"metric": "BatchNorm+residual+ReLU fwd+bwd (bf16 NHWC)", "shape": list(shape),
-                          "native_us": round(t_nat * 1e6, 1), "torch_us": round(t_ref * 1e6, 1),
+                          "native_us": round(t_nat * 1e6, 1),
+                          "red_blocks": os.environ.get("PTDT_BN_RED_BLOCKS", "default"),
+                          "pipe": os.environ.get("PTDT_BN_PIPE", "1"), "torch_us": round(t_ref * 1e6, 1),
                           "speedup": round(t_ref / t_nat, 2),
                           "native_GBps_min_traffic": round(min_bytes / t_nat / 1e9, 1)}), flush=True)
 
