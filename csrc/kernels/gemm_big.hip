@@ -128,6 +128,129 @@ __device__ __forceinline__ void mfma_tile(f32x4_t (&acc)[T::FI][T::FJ], const Fr
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[kb][i], f.b[kb][j], acc[i][j], 0, 0, 0);
 }
 
+// Epilogue of a wave's FI x FJ accumulator tiles:
+// acc[i][j][r] = C[m0 + wr*FI*16 + i*16 + 4*fq + r][n0 + wc*FJ*16 + j*16 + fr]
+template <int FI, int FJ, int OUT>
+__device__ __forceinline__ void store_tile(const BigGemmArgs& g, const f32x4_t (&acc)[FI][FJ], int m0, int n0, int wr,
+                                           int wc, int fr, int fq) {
+  const bool add_bias = g.bias != nullptr && blockIdx.y == 0;
+#pragma unroll
+  for (int j = 0; j < FJ; ++j) {
+    const int n = n0 + wc * (FJ * 16) + j * 16 + fr;
+    if (n >= g.N) continue;
+    float bias = 0.f;
+    if (add_bias)
+      bias = g.bias_dtype == kF32 ? static_cast<const float*>(g.bias)[n]
+                                  : bf16_to_f32(static_cast<const uint16_t*>(g.bias)[n]);
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * (FI * 16) + i * 16 + 4 * fq + r;
+        if (m >= g.M) continue;
+        const int64_t off = (int64_t)m * g.ldc + n;
+        float v = g.alpha * acc[i][j][r];
+        if constexpr (OUT == 2) {
+          atomicAdd(static_cast<float*>(g.C) + off, v + bias);
+        } else if constexpr (OUT == 1) {
+          float* c = static_cast<float*>(g.C);
+          if (g.beta != 0.f) v += g.beta * c[off];
+          v += bias;
+          c[off] = g.relu ? fmaxf(v, 0.f) : v;
+        } else {
+          uint16_t* c = static_cast<uint16_t*>(g.C);
+          if (g.beta != 0.f) v += g.beta * bf16_to_f32(c[off]);
+          v += bias;
+          c[off] = f32_to_bf16(g.relu ? fmaxf(v, 0.f) : v);
+        }
+      }
+  }
+}
+
+// Coalesced epilogue (OUT 0 / 1): the accumulators of 64-row bands go through LDS (fp32, row
+// stride FJ*16 + 4 floats: the four lane groups of a write land on distinct banks), then each lane
+// finishes 8 consecutive columns of a row -- alpha, beta*C, bias, ReLU -- and writes them with one
+// 16-B (bf16) or two 16-B (f32) stores instead of 8 scattered 2/4-B stores per 8 outputs.
+// `scratch` is this wave's LDS region of epi_floats<FJ>() floats; the caller has made every wave
+// finish its operand reads (barrier) before the first band is written.
+template <int FJ>
+constexpr int epi_ld() { return FJ * 16 + 4; }
+template <int FJ>
+constexpr int epi_floats() { return 64 * epi_ld<FJ>(); }
+
+template <int FI, int FJ, int OUT>
+__device__ __forceinline__ void store_tile_lds(const BigGemmArgs& g, const f32x4_t (&acc)[FI][FJ], int m0, int n0,
+                                               int wr, int wc, int fr, int fq, float* scratch) {
+  static_assert(OUT == 0 || OUT == 1, "split-K slices use the atomic epilogue");
+  static_assert(FI % 4 == 0, "64-row bands");
+  constexpr int LD = epi_ld<FJ>(), W = FJ * 16, CPR = W / 8;  // columns per wave row, 8-column chunks per row
+  const int lane = fr + 16 * fq;
+  const bool add_bias = g.bias != nullptr;
+  const int ncol0 = n0 + wc * W;
+  const bool vec = (g.ldc % 8 == 0) && ((reinterpret_cast<uintptr_t>(g.C) & 15) == 0);
+#pragma unroll
+  for (int band = 0; band < FI / 4; ++band) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < FJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) scratch[(i * 16 + 4 * fq + r) * LD + j * 16 + fr] = acc[band * 4 + i][j][r];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const int mrow0 = m0 + wr * (FI * 16) + band * 64;
+#pragma unroll
+    for (int it = 0; it < 64 * CPR / 64; ++it) {
+      const int e = it * 64 + lane;  // (row, chunk) of this lane
+      const int row = e / CPR, ch = e % CPR;
+      const int m = mrow0 + row, n = ncol0 + ch * 8;
+      const float4 lo = *reinterpret_cast<const float4*>(scratch + row * LD + ch * 8);
+      const float4 hi = *reinterpret_cast<const float4*>(scratch + row * LD + ch * 8 + 4);
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      if (m >= g.M || n >= g.N) continue;
+      const bool full = vec && n + 8 <= g.N;
+      const int64_t off = (int64_t)m * g.ldc + n;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int nn = n + q;
+        float x = g.alpha * v[q];
+        if (nn < g.N) {
+          if (g.beta != 0.f)
+            x += g.beta * (OUT == 1 ? static_cast<const float*>(g.C)[off + q]
+                                    : bf16_to_f32(static_cast<const uint16_t*>(g.C)[off + q]));
+          if (add_bias)
+            x += g.bias_dtype == kF32 ? static_cast<const float*>(g.bias)[nn]
+                                      : bf16_to_f32(static_cast<const uint16_t*>(g.bias)[nn]);
+        }
+        v[q] = g.relu ? fmaxf(x, 0.f) : x;
+      }
+      if constexpr (OUT == 1) {
+        float* c = static_cast<float*>(g.C) + off;
+        if (full) {
+          *reinterpret_cast<float4*>(c) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(c + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        } else {
+          for (int q = 0; q < 8 && n + q < g.N; ++q) c[q] = v[q];
+        }
+      } else {
+        uint16_t* c = static_cast<uint16_t*>(g.C) + off;
+        if (full) {
+          uint4 u;
+          u.x = (uint32_t)f32_to_bf16(v[0]) | ((uint32_t)f32_to_bf16(v[1]) << 16);
+          u.y = (uint32_t)f32_to_bf16(v[2]) | ((uint32_t)f32_to_bf16(v[3]) << 16);
+          u.z = (uint32_t)f32_to_bf16(v[4]) | ((uint32_t)f32_to_bf16(v[5]) << 16);
+          u.w = (uint32_t)f32_to_bf16(v[6]) | ((uint32_t)f32_to_bf16(v[7]) << 16);
+          *reinterpret_cast<uint4*>(c) = u;
+        } else {
+          for (int q = 0; q < 8 && n + q < g.N; ++q) c[q] = f32_to_bf16(v[q]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();  // band reads done before the next band's writes
+  }
+}
+
 // OUT: 0 bf16 store, 1 f32 store, 2 f32 atomic add (split-K slices).
 // SCHED 0: every wave reads then multiplies each K-tile (two barriers per tile,
 //          tile k+1's DMA in flight meanwhile).
@@ -236,55 +359,213 @@ __global__ void __launch_bounds__(T::NT) gemm_bf16_lds_kernel(BigGemmArgs g, int
     }
   }
 
-  // epilogue: acc[i][j][r] = C[m0 + wr*FI*16 + i*16 + 4*fq + r][n0 + wc*FJ*16 + j*16 + fr]
-  const bool add_bias = g.bias != nullptr && blockIdx.y == 0;
-#pragma unroll
-  for (int j = 0; j < T::FJ; ++j) {
-    const int n = n0 + wc * (T::FJ * 16) + j * 16 + fr;
-    if (n >= g.N) continue;
-    float bias = 0.f;
-    if (add_bias)
-      bias = g.bias_dtype == kF32 ? static_cast<const float*>(g.bias)[n]
-                                  : bf16_to_f32(static_cast<const uint16_t*>(g.bias)[n]);
-#pragma unroll
-    for (int i = 0; i < T::FI; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wr * (T::FI * 16) + i * 16 + 4 * fq + r;
-        if (m >= g.M) continue;
-        const int64_t off = (int64_t)m * g.ldc + n;
-        float v = g.alpha * acc[i][j][r];
-        if constexpr (OUT == 2) {
-          atomicAdd(static_cast<float*>(g.C) + off, v + bias);
-        } else if constexpr (OUT == 1) {
-          float* c = static_cast<float*>(g.C);
-          if (g.beta != 0.f) v += g.beta * c[off];
-          v += bias;
-          c[off] = g.relu ? fmaxf(v, 0.f) : v;
-        } else {
-          uint16_t* c = static_cast<uint16_t*>(g.C);
-          if (g.beta != 0.f) v += g.beta * bf16_to_f32(c[off]);
-          v += bias;
-          c[off] = f32_to_bf16(g.relu ? fmaxf(v, 0.f) : v);
-        }
-      }
+  if constexpr (OUT == 2) {
+    store_tile<T::FI, T::FJ, OUT>(g, acc, m0, n0, wr, wc, fr, fq);
+  } else {
+    __builtin_amdgcn_s_barrier();  // every wave's fragment reads done: the LDS is scratch now
+    store_tile_lds<T::FI, T::FJ, OUT>(g, acc, m0, n0, wr, wc, fr, fq,
+                                      reinterpret_cast<float*>(smem) + wid * epi_floats<T::FJ>());
   }
+}
+
+
+// SCHED 2 (256x256 geometry, BK = 64): the ping-pong pairs of SCHED 1 fed from a ring of ten
+// 16-KiB operand pieces that fills the 160 KiB of LDS, so every DMA is issued 3-4 slots before
+// its first reader (SCHED 1: 2) and no wait ever drains the queue in the loop.
+//   pieces of K-tile t: A0 / A1 = A rows 0-127 / 128-255 (read by the leader wr = 0 in slot 2t /
+//   the follower wr = 1 in slot 2t+1), B0 / B1 = B rows 0-127 / 128-255 (both groups).
+//   issue schedule: slot 2k: A1(k+1), B0(k+2), B1(k+2); slot 2k+1: A0(k+2).
+//   storage: A0(t) in one of two dedicated slots (t & 1: A0(t+2) is issued right after A0(t)'s
+//   reader, the leader, is done); A1 / B0 / B1 in an 8-slot FIFO in issue order (position
+//   3(t-1) for A1(t), 3(t-2) + 1 / + 2 for B0(t) / B1(t)), whose three oldest entries --
+//   tile t-1's B0, B1, A1 -- are released together when the follower finishes tile t-1.
+//   waits (per wave, its own LDS-DMAs, 2 per piece): before slot 2s the pieces B0, B1, A0 of
+//   tile s are retired (at most 8 later DMAs in flight), before slot 2s+1 A1(s) is (at most 12).
+constexpr int PIECE = 128 * BK * 2;  // 16 KiB
+constexpr int PLDS = 10 * PIECE;     // 160 KiB
+static_assert(8 * epi_floats<4>() * 4 <= PLDS, "epilogue scratch exceeds the LDS");
+
+__device__ __forceinline__ int fifo_slot(int pos) { return (pos + 16) & 7; }
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N == 0 || N == 2 || N == 8 || N == 12, "add the literal");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  if constexpr (N == 8) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  if constexpr (N == 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+}
+
+template <int OUT>
+__global__ void __launch_bounds__(512) gemm_bf16_piece_kernel(BigGemmArgs g, int tm, int tn, int kt_per) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int FI = 8, FJ = 4;  // 128 x 64 per wave
+  const int tile = xcd_remap(blockIdx.x, tm * tn);
+  const int m0 = (tile / tn) * 256, n0 = (tile % tn) * 256;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const uint16_t* A = static_cast<const uint16_t*>(g.A);
+  const uint16_t* Bt = static_cast<const uint16_t*>(g.Bt);
+  const int nk_all = g.K / BK;
+  const int kt_begin = blockIdx.y * kt_per;
+  const int nk = min(nk_all, kt_begin + kt_per) - kt_begin;
+  const int kbase = kt_begin * BK;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4_t acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto a0_base = [&](int t) { return smem + (8 + (t & 1)) * PIECE; };
+  auto a1_base = [&](int t) { return smem + fifo_slot(3 * (t - 1)) * PIECE; };
+  auto b_base = [&](int t, int h) { return smem + fifo_slot(3 * (t - 2) + 1 + h) * PIECE; };
+  auto stage_a = [&](int t, int h, uint8_t* dst) {
+    stage_tile<128, 512>(A, g.lda, m0 + 128 * h, g.M, kbase + t * BK, dst, wid, lane);
+  };
+  auto stage_b = [&](int t, int h) {
+    stage_tile<128, 512>(Bt, g.ldb, n0 + 128 * h, g.N, kbase + t * BK, b_base(t, h), wid, lane);
+  };
+  auto issue_slot = [&](int slot) {
+    const int k = slot >> 1;
+    if ((slot & 1) == 0) {
+      if (k + 1 < nk) stage_a(k + 1, 1, a1_base(k + 1));
+      if (k + 2 < nk) {
+        stage_b(k + 2, 0);
+        stage_b(k + 2, 1);
+      }
+    } else if (k + 2 < nk) {
+      stage_a(k + 2, 0, a0_base(k + 2));
+    }
+  };
+  // end of slot 2s: A1(s) retired; end of slot 2s+1: B0, B1, A0 of tile s+1 retired
+  auto wait_even = [&](int s) {
+    if (s + 2 < nk) vm_wait<12>();
+    else if (s + 1 < nk) vm_wait<8>();
+    else vm_wait<0>();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto wait_odd = [&](int s) {
+    if (s + 2 < nk) vm_wait<8>();
+    else if (s + 1 < nk) vm_wait<2>();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto slot_barrier = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  bf16x8_t a[2][FI], b[2][FJ];
+  auto read = [&](const uint8_t* ap, const uint8_t* bp) {
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) b[kb][j] = read_frag(bp, (wc & 1) * 64 + j * 16 + fr, kb * 4 + fq);
+#pragma unroll
+      for (int i = 0; i < FI; ++i) a[kb][i] = read_frag(ap, i * 16 + fr, kb * 4 + fq);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mma = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kb][i], b[kb][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // prologue: B0(0), B1(0), A0(0), A1(0), B0(1), B1(1), A0(1) -- the issue order the waits count
+  stage_b(0, 0);
+  stage_b(0, 1);
+  stage_a(0, 0, a0_base(0));
+  stage_a(0, 1, a1_base(0));
+  if (nk > 1) {
+    stage_b(1, 0);
+    stage_b(1, 1);
+    stage_a(1, 0, a0_base(1));
+    vm_wait<8>();
+  } else {
+    vm_wait<2>();
+  }
+  slot_barrier();
+  if (wr == 0) {
+    for (int s = 0; s < nk; ++s) {
+      issue_slot(2 * s);
+      read(a0_base(s), b_base(s, wc >> 1));
+      wait_even(s);
+      slot_barrier();
+      issue_slot(2 * s + 1);
+      mma();
+      wait_odd(s);
+      slot_barrier();
+    }
+  } else {
+    for (int s = 0; s < nk; ++s) {
+      issue_slot(2 * s);
+      if (s > 0) mma();
+      wait_even(s);
+      slot_barrier();
+      issue_slot(2 * s + 1);
+      read(a1_base(s), b_base(s, wc >> 1));
+      wait_odd(s);
+      slot_barrier();
+    }
+    mma();
+  }
+  if constexpr (OUT == 2) {
+    store_tile<FI, FJ, OUT>(g, acc, m0, n0, wr, wc, fr, fq);
+  } else {
+    __builtin_amdgcn_s_barrier();  // every wave's fragment reads done: the LDS is scratch now
+    store_tile_lds<FI, FJ, OUT>(g, acc, m0, n0, wr, wc, fr, fq,
+                                reinterpret_cast<float*>(smem) + wid * epi_floats<FJ>());
+  }
+}
+
+template <int OUT>
+hipError_t launch_piece(const BigGemmArgs& g, int split, hipStream_t s) {
+  const void* fn = reinterpret_cast<const void*>(&gemm_bf16_piece_kernel<OUT>);
+  static bool attr_set = false;
+  if (!attr_set) {
+    PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, PLDS));
+    attr_set = true;
+  }
+  const int tm = (g.M + 255) / 256, tn = (g.N + 255) / 256;
+  const int nk = g.K / BK;
+  const int kt_per = (nk + split - 1) / split;
+  split = (nk + kt_per - 1) / kt_per;
+  hipLaunchKernelGGL((gemm_bf16_piece_kernel<OUT>), dim3(tm * tn, split), dim3(512), PLDS, s, g, tm, tn, kt_per);
+  return hipGetLastError();
+}
+
+// operand double buffer, or the coalesced epilogue's scratch if that is larger
+template <class T>
+constexpr int lds_bytes() {
+  return T::LDS > (T::NT / 64) * epi_floats<T::FJ>() * 4 ? T::LDS : (T::NT / 64) * epi_floats<T::FJ>() * 4;
 }
 
 template <class T, int OUT, int SCHED>
 hipError_t launch(const BigGemmArgs& g, int split, hipStream_t s) {
   const void* fn = reinterpret_cast<const void*>(&gemm_bf16_lds_kernel<T, OUT, SCHED>);
+  constexpr int lds = lds_bytes<T>();
   static bool attr_set = false;  // one flag per instantiation
   if (!attr_set) {
-    PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, T::LDS));
+    PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
     attr_set = true;
   }
   const int tm = (g.M + T::BM - 1) / T::BM, tn = (g.N + T::BN - 1) / T::BN;
   const int nk = g.K / BK;
   const int kt_per = (nk + split - 1) / split;
   split = (nk + kt_per - 1) / kt_per;  // no empty slices
-  hipLaunchKernelGGL((gemm_bf16_lds_kernel<T, OUT, SCHED>), dim3(tm * tn, split), dim3(T::NT), T::LDS, s, g, tm,
-                     tn, kt_per);
+  hipLaunchKernelGGL((gemm_bf16_lds_kernel<T, OUT, SCHED>), dim3(tm * tn, split), dim3(T::NT), lds, s, g, tm, tn,
+                     kt_per);
   return hipGetLastError();
 }
 
@@ -311,8 +592,13 @@ hipError_t gemm_bf16_big(const BigGemmArgs& g, hipStream_t s) {
     return launch_out<T128, 0>(g, split, s);  // 4 waves, one per SIMD: no ping-pong partner
   }
   if (g.tile != 256) return hipErrorInvalidValue;
+  static_assert(lds_bytes<T256>() <= 160 * 1024 && 2 * lds_bytes<T128>() <= 160 * 1024, "LDS budget");
   if (g.sched == 0) return launch_out<T256, 0>(g, split, s);
   if (g.sched == 1) return launch_out<T256, 1>(g, split, s);
+  if (g.sched == 2) {
+    if (split > 1) return launch_piece<2>(g, split, s);
+    return g.out_dtype == kF32 ? launch_piece<1>(g, 1, s) : launch_piece<0>(g, 1, s);
+  }
   return hipErrorInvalidValue;
 }
 

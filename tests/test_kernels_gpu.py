@@ -121,7 +121,7 @@ def test_gemm_layouts(native, dev, dtype, M, N, K, layout):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 1024), (300, 200, 128), (120, 1000, 2048),
                                    (1, 257, 64), (1000, 17, 192)])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("sched", [0, 1])
+@pytest.mark.parametrize("sched", [0, 1, 2])
 def test_gemm_big_matches_fp32(native, dev, M, N, K, out_dtype, sched):
     """256x256 LDS-DMA kernel: C = A.Bt^T (+bias, ReLU, alpha/beta) vs fp32 on the same bf16 operands;
     asymmetric operands catch a transposed C write, edge shapes the clamped rows."""
@@ -191,6 +191,27 @@ def test_gemm_nt_big_planner(dev, M, N, K):
     out = gemm_nt_big(A, Bt, torch.bfloat16, bias=bias, relu=True)
     tol = 1e-2 * math.sqrt(K) / 8
     torch.testing.assert_close(out.float(), ref, rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("tile,sched", [(128, -1), (256, 1), (256, 2)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_gemm_big_strided_output(native, dev, sched, tile, out_dtype):
+    """The coalesced epilogue (LDS-staged rows, 16-B stores) on output views: a row stride that is
+    not a multiple of 8 elements takes the per-element path, an aligned column slice the vector
+    one; the columns around the view stay untouched."""
+    M, N, K = 300, 200, 192
+    torch.manual_seed(tile + sched)
+    A = (torch.rand(M, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    Bt = (torch.rand(N, K, device=dev) * 2 - 1).to(torch.bfloat16)
+    bias = torch.randn(N, device=dev)
+    ref = F.relu(A.float() @ Bt.float().t() + bias)
+    tol = 1e-4 * math.sqrt(K) if out_dtype == torch.float32 else 1e-2 * math.sqrt(K) / 8
+    for pad, off in ((3, 1), (16, 8)):
+        big = torch.full((M, N + pad), 7.0, device=dev, dtype=out_dtype)
+        view = big[:, off:off + N]
+        native.gemm_big_(A, Bt, view, bias, True, 1.0, 0.0, sched, tile=tile)
+        torch.testing.assert_close(view.float(), ref, rtol=tol, atol=tol)
+        assert bool((big[:, :off] == 7).all()) and bool((big[:, off + N:] == 7).all())
 
 
 def test_gemm_big_identity_and_strides(native, dev):
