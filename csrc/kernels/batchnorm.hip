@@ -37,6 +37,8 @@
 // The ReLU mask comes from the forward output y, or -- for BNs without a residual
 // -- is recomputed from x with the forward's own fmaf(x, scale, shift), sparing
 // one of the three reads in both backward passes.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -80,6 +82,15 @@ struct VecIO {
     *reinterpret_cast<uint4*>(p) = u;
   }
 };
+
+// Row order of the reduction passes (PTDT_BN_INTERLEAVE=0: one contiguous slab per row block).
+int interleave_rows() {
+  static const int v = [] {
+    const char* e = getenv("PTDT_BN_INTERLEAVE");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v;
+}
 
 struct Geom {
   int TC, RPI;       // channel vectors per row, rows per block iteration
@@ -207,7 +218,8 @@ __device__ __forceinline__ void rearm(int* ticket) {
 
 template <typename T>
 __global__ void __launch_bounds__(kRed) bn_stats_kernel(const T* __restrict__ x, int64_t M, int C, int TC, int RPI,
-                                                        int64_t rows_per_block, float* ws, int* tickets, BnParams p) {
+                                                        int64_t rows_per_block, int il, float* ws, int* tickets,
+                                                        BnParams p) {
   constexpr int V = VecIO<T>::V;
   constexpr int U = 8;  // rows in flight per thread
   extern __shared__ float sh[];  // 2 x RPI x TC*V reduction slots, then the last-block flag
@@ -215,19 +227,23 @@ __global__ void __launch_bounds__(kRed) bn_stats_kernel(const T* __restrict__ x,
   const int tid = threadIdx.x, rr = tid / TC, tc = tid % TC;
   const int c0 = (blockIdx.y * TC + tc) * V;  // this thread's channels c0..c0+V
   const bool active = rr < RPI && c0 < C;
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t r1 = min(M, r0 + rows_per_block);
+  // il: rows interleaved across the row blocks in RPI-row chunks (block b: chunks b, b + gx, ...),
+  // so the grid sweeps the tensor front to back together, as the elementwise passes do; else each
+  // block owns one contiguous slab of rows_per_block rows (gx separate streams)
+  const int64_t rs = il ? (int64_t)gridDim.x * RPI : RPI;
+  const int64_t rb = il ? (int64_t)blockIdx.x * RPI : (int64_t)blockIdx.x * rows_per_block;
+  const int64_t re = il ? M : min(M, rb + rows_per_block);
   float acc[2][V];
 #pragma unroll
   for (int v = 0; v < V; ++v) acc[0][v] = acc[1][v] = 0.f;
   if (active) {
     float K[V];
     VecIO<T>::load(x + c0, K);  // pivot: row 0 (same for every block)
-    int64_t r = r0 + rr;
-    for (; r + (U - 1) * RPI < r1; r += U * RPI) {  // U independent 16-B loads in flight
+    int64_t r = rb + rr;
+    for (; r + (U - 1) * rs < re; r += U * rs) {  // U independent 16-B loads in flight
       float a[U][V];
 #pragma unroll
-      for (int u = 0; u < U; ++u) VecIO<T>::load(x + (r + u * RPI) * C + c0, a[u]);
+      for (int u = 0; u < U; ++u) VecIO<T>::load(x + (r + u * rs) * C + c0, a[u]);
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -237,7 +253,7 @@ __global__ void __launch_bounds__(kRed) bn_stats_kernel(const T* __restrict__ x,
           acc[1][v] = fmaf(d, d, acc[1][v]);
         }
     }
-    for (; r < r1; r += RPI) {
+    for (; r < re; r += rs) {
       float a[V];
       VecIO<T>::load(x + r * C + c0, a);
 #pragma unroll
@@ -327,7 +343,7 @@ template <typename T, int MASK, bool ADD2>
 __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
                                                              const T* __restrict__ x,
                                                              const T* __restrict__ y, int64_t M, int C, int TC,
-                                                             int RPI, int64_t rows_per_block, float* ws,
+                                                             int RPI, int64_t rows_per_block, int il, float* ws,
                                                              int* tickets, BnBwdParams p) {
   constexpr int V = VecIO<T>::V;
   constexpr int U = 4;  // rows in flight per thread (x 2-3 loads each)
@@ -336,8 +352,9 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
   const int tid = threadIdx.x, rr = tid / TC, tc = tid % TC;
   const int c0 = (blockIdx.y * TC + tc) * V;
   const bool active = rr < RPI && c0 < C;
-  const int64_t r0 = (int64_t)blockIdx.x * rows_per_block;
-  const int64_t r1 = min(M, r0 + rows_per_block);
+  const int64_t rs = il ? (int64_t)gridDim.x * RPI : RPI;  // row order: as in bn_stats_kernel
+  const int64_t rb = il ? (int64_t)blockIdx.x * RPI : (int64_t)blockIdx.x * rows_per_block;
+  const int64_t re = il ? M : min(M, rb + rows_per_block);
   float acc[2][V];
 #pragma unroll
   for (int v = 0; v < V; ++v) acc[0][v] = acc[1][v] = 0.f;
@@ -349,12 +366,12 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
       sc[v] = MASK == 2 ? p.scale[c0 + v] : 0.f;
       sf[v] = MASK == 2 ? p.shift[c0 + v] : 0.f;
     }
-    int64_t r = r0 + rr;
-    for (; r + (U - 1) * RPI < r1; r += U * RPI) {
+    int64_t r = rb + rr;
+    for (; r + (U - 1) * rs < re; r += U * rs) {
       float g[U][V], a[U][V], o[U][V], g2[ADD2 ? U : 1][V];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t off = (r + u * RPI) * C + c0;
+        const int64_t off = (r + u * rs) * C + c0;
         VecIO<T>::load(dy + off, g[u]);
         if constexpr (ADD2) VecIO<T>::load(dy2 + off, g2[u]);
         VecIO<T>::load(x + off, a[u]);
@@ -375,7 +392,7 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
           acc[1][v] = fmaf(gg, a[u][v] - mu[v], acc[1][v]);
         }
     }
-    for (; r < r1; r += RPI) {
+    for (; r < re; r += rs) {
       float g[V], a[V], o[V];
       const int64_t off = r * C + c0;
       VecIO<T>::load(dy + off, g);
@@ -475,7 +492,7 @@ hipError_t fwd_impl(const BnFwdArgs& a, hipStream_t s) {
   const Geom g = geom<T>(a.M, a.C);
   const size_t sh_red = (size_t)2 * kRed * V * sizeof(float) + 16;
   hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(g.gx, g.gy), dim3(kRed), sh_red, s, static_cast<const T*>(a.x),
-                     a.M, a.C, g.TC, g.RPI, g.rows_per_block, a.workspace, a.tickets, a.p);
+                     a.M, a.C, g.TC, g.RPI, g.rows_per_block, interleave_rows(), a.workspace, a.tickets, a.p);
   PTDT_HIP_CHECK(hipGetLastError());
   const int64_t nvec = a.M * a.C / V;
   const size_t sh_ap = (size_t)2 * a.C * sizeof(float);
@@ -523,7 +540,7 @@ hipError_t bwd_launch(const BnBwdArgs& a, const Geom& g, hipStream_t s) {
   const T* x = static_cast<const T*>(a.x);
   const T* y = static_cast<const T*>(a.y);
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK, ADD2>), dim3(g.gx, g.gy), dim3(kRed), sh_red, s, dy, dy2, x, y,
-                     a.M, a.C, g.TC, g.RPI, g.rows_per_block, a.workspace, a.tickets, a.p);
+                     a.M, a.C, g.TC, g.RPI, g.rows_per_block, interleave_rows(), a.workspace, a.tickets, a.p);
   PTDT_HIP_CHECK(hipGetLastError());
   const int64_t nvec = a.M * a.C / V;
   const size_t sh_ap = (size_t)(MASK == 2 ? 5 : 3) * a.C * sizeof(float);
