@@ -246,14 +246,20 @@ def run_persistent(args, rank, world, dev, comm):
         timed_steps = order_plan(n_warm, args.steps)
     else:
         # launch planned once (native PersistentPlan): the timed region is hipLaunchKernel(s) + the kernel
+        # the bench counts its own steps from cursor 0, so every launch names its start
+        # position (launch_at: no dependent cursor load at kernel entry)
         plan = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses, variant=variant)
         for d in range(0, n_warm, chunk):
             plan.launch(min(chunk, n_warm - d))
-        launch = plan.launch
+        if os.environ.get("PTDT_BENCH_DEVICE_CURSOR") == "1":  # A/B: start from the device cursor
+            launch_at = lambda n, p: plan.launch(n)  # noqa: E731
+        else:
+            launch_at = plan.launch_at
+        starts = [n_warm + d for d in range(0, args.steps, chunk)]
 
         def timed_steps():
-            for n in launches:
-                launch(n)
+            for n, p in zip(launches, starts):
+                launch_at(n, p)
     torch.cuda.synchronize(dev)
     if _xgmi_failed(comm, dev, xg, "warmup"):
         return _rccl_fallback(args, rank, world, dev, comm)
@@ -265,8 +271,19 @@ def run_persistent(args, rank, world, dev, comm):
     phase = None
     if args.stamps:  # diagnostic pass AFTER the timed region (timers cost a little)
         st = torch.zeros(32, dtype=torch.int64, device=dev)
-        eng.run_persistent(X, Y, args.steps, args.batch_size, sampler, cursor, losses, chunk, stamps=st,
-                           variant=variant)
+        if args.sampler == "torch":
+            eng.run_persistent(X, Y, args.steps, args.batch_size, sampler, cursor, losses, chunk, stamps=st,
+                               variant=variant)
+        else:  # the timed path: a plan (list cache warmed by a first pass) launched at known positions
+            p2 = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses, variant=variant, stamps=st)
+            pos = n_warm + args.steps
+            for rep in range(2):
+                torch.cuda.synchronize(dev)
+                st.zero_()
+                for n in launches:
+                    p2.launch_at(n, pos)
+                    pos += n
+            torch.cuda.synchronize(dev)
         v = st.tolist()
         names = (["fetch", "forward", "loss", "backward", "allreduce", "sgd_loss_report"] if which.startswith("wave") else
                  ["stage_issue", "forward", "barrier_logit_sum", "loss", "backward", "allreduce_sgd", "produce_lists"]
@@ -275,6 +292,11 @@ def run_persistent(args, rank, world, dev, comm):
         clk = v[7] / (v[8] * 10e-9) if v[8] else 0.0
         phase = {"cycles_per_step": {n: round(v[k] / args.steps, 1) for k, n in enumerate(names)},
                  "total_cycles_per_step": round(v[7] / args.steps, 1), "clock_GHz": round(clk / 1e9, 3)}
+        if which.startswith("wave"):  # kernel entry -> first step (10 ns ticks), per launch
+            nl = math.ceil(args.steps / chunk)
+            phase["prologue_us_per_launch"] = round(v[10] * 0.01 / nl, 2)
+            # entry -> position known, -> epoch list in LDS, -> past the barrier (waits forced in this pass)
+            phase["prologue_split_us"] = [round(v[k] * 0.01 / nl, 2) for k in (11, 12, 13)]
         if which.startswith("tp"):  # each wave's barrier + logit-sum phase (load balance)
             nw = int(which.split(":")[1].split("w")[0])
             phase["logit_sum_per_wave"] = [round(x / args.steps, 1) for x in v[9:9 + nw]]
@@ -321,9 +343,9 @@ def _mlp_side(args, rank, world, dev, comm, xg):
     n_w, n_t = max(args.warmup, 1), args.steps
     losses = torch.zeros(max(n_w, n_t), device=dev)
     plan = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses)
-    plan.launch(n_w)
+    plan.launch_at(n_w, 0)
     torch.cuda.synchronize(dev)
-    t = _timed(comm, dev, lambda: plan.launch(n_t))
+    t = _timed(comm, dev, lambda: plan.launch_at(n_t, n_w))
     failed = xg is not None and _xgmi_failed(comm, dev, xg, "MLP side measurement")
     return {"mlp_us_per_step": None if failed else round(1e6 * t / n_t, 3),
             "mlp_samples_per_s": None if failed else round(n_t * args.batch_size * world / t, 1),

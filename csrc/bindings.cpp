@@ -287,15 +287,26 @@ class PersistentPlan {
   // n steps from the device cursor; with explicit index lists, cursor_pos is
   // the host's view of the cursor (epoch * steps_per_epoch + step; one-epoch
   // list: the step in it) and the launch must stay inside the provided epochs
-  void launch(int64_t n, int64_t cursor_pos) {
+  void launch(int64_t n, int64_t cursor_pos) { launch_impl(n, cursor_pos, -1, 0); }
+  void launch_impl(int64_t n, int64_t cursor_pos, int start_e, int start_j) {
     TORCH_CHECK(n >= 0 && n <= capacity_, "persistent plan: n_steps exceeds the losses buffer");
     const int64_t S = steps_per_epoch_;
     TORCH_CHECK(L_.p.idx == nullptr || (cursor_pos >= (int64_t)L_.p.idx_e0 * S &&
                                         cursor_pos + n <= (int64_t)(L_.p.idx_e0 + L_.p.idx_epochs) * S),
                 "persistent plan: with explicit index lists a launch must stay inside the provided epochs");
     c10::hip::HIPGuard guard(dev_);
-    hip_check(persistent_launch(L_, (int)n, L_.p.idx ? cursor_pos : -1, c10::hip::getCurrentHIPStream(dev_).stream()),
+    hip_check(persistent_launch(L_, (int)n, L_.p.idx ? cursor_pos : -1, c10::hip::getCurrentHIPStream(dev_).stream(),
+                                start_e, start_j),
               "persistent launch");
+  }
+  // n steps from absolute position pos = epoch * steps_per_epoch + step, which the
+  // caller asserts the device cursor holds (its own step count, e.g. the bench's
+  // warm-up): the engines skip the dependent cursor load at kernel entry
+  void launch_at(int64_t n, int64_t pos) {
+    TORCH_CHECK(pos >= 0, "persistent plan: launch_at needs a position >= 0");
+    const int64_t S = steps_per_epoch_;
+    TORCH_CHECK(pos / S < (int64_t)1 << 30, "persistent plan: position out of range");
+    launch_impl(n, pos, (int)(pos / S), (int)(pos % S));
   }
   int64_t capacity() const { return capacity_; }
 
@@ -1096,6 +1107,7 @@ PYBIND11_MODULE(_C, m) {
            py::arg("stamps") = py::none(), py::arg("variant") = 0, py::arg("x_zero_padded") = false,
            py::arg("idx") = py::none(), py::arg("lcache") = py::none(), py::arg("idx_e0") = 0)
       .def("launch", &PersistentPlan::launch, py::arg("n_steps"), py::arg("cursor_pos") = -1)
+      .def("launch_at", &PersistentPlan::launch_at, py::arg("n_steps"), py::arg("pos"))
       .def_property_readonly("capacity", &PersistentPlan::capacity);
   m.def("persistent_engine", &persistent_engine, py::arg("B"), py::arg("Din"), py::arg("H"), py::arg("Dout"),
         py::arg("loss_kind"), py::arg("num_samples"), py::arg("world"), py::arg("variant") = 0,

@@ -1038,7 +1038,8 @@ hipError_t fused_mlp_persistent_prepare(const FusedMlpArgs& a, const PersistArgs
   return hipSuccess;
 }
 
-hipError_t persistent_launch(PersistLaunch& L, int n_steps, int64_t cursor_host_pos, hipStream_t s) {
+hipError_t persistent_launch(PersistLaunch& L, int n_steps, int64_t cursor_host_pos, hipStream_t s, int start_e,
+                             int start_j) {
   if (n_steps <= 0) return hipSuccess;
   if (L.fn == nullptr) return hipErrorInvalidValue;
   if (L.p.idx != nullptr) {  // explicit lists cover epochs [idx_e0, idx_e0 + idx_epochs) only
@@ -1048,6 +1049,9 @@ hipError_t persistent_launch(PersistLaunch& L, int n_steps, int64_t cursor_host_
   }
   L.p.n_steps = n_steps;
   L.p.cursor_host_pos = cursor_host_pos;
+  L.p.has_start = start_e >= 0 ? 1 : 0;
+  L.p.start_e = start_e;
+  L.p.start_j = start_j;
   void* args[] = {&L.a, &L.p};
   return hipLaunchKernel(L.fn, dim3(1), dim3(L.threads), args, L.lds, s);
 }

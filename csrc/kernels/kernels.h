@@ -82,6 +82,10 @@ struct PersistArgs {
   int64_t cursor_host_pos;  // the caller's view of the cursor (epoch * steps_per_epoch + step), or -1
   int32_t* lcache;       // optional [2][al4(num_samples)] launch-to-launch epoch-list cache (sampler.h ListCache)
   int32_t* ltag;         // its [2] epoch tags (-1: empty); both null: every launch recomputes its lists
+  // host-asserted start position (PersistentPlan.launch_at): when has_start is set the
+  // caller guarantees the device cursor holds (start_e, start_j), and the wave/TP engines
+  // take it from the kernel arguments instead of a dependent load at kernel entry
+  int has_start, start_e, start_j;
 };
 // Engine choice: the register-resident single-wave engine (linear_wave.hip) runs
 // Linear(Din, Dout) models with B <= 64 and small Dout; everything else runs the
@@ -120,7 +124,8 @@ struct PersistLaunch {
   PersistArgs p{};
 };
 hipError_t fused_mlp_persistent_prepare(const FusedMlpArgs& a, const PersistArgs& p, PersistLaunch* out);
-hipError_t persistent_launch(PersistLaunch& L, int n_steps, int64_t cursor_host_pos, hipStream_t s);
+hipError_t persistent_launch(PersistLaunch& L, int n_steps, int64_t cursor_host_pos, hipStream_t s,
+                             int start_e = -1, int start_j = 0);
 bool linear_wave_supported(const FusedMlpArgs& a, const PersistArgs& p);
 bool mlp_mfma_persistent_supported(const FusedMlpArgs& a, const PersistArgs& p);
 bool mlp_tp_supported(const FusedMlpArgs& a, const PersistArgs& p);

@@ -675,15 +675,26 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   constexpr bool SCATTER = DOUT == 1 && R > 1;
   constexpr int RY = SCATTER ? 1 : R;  // target rows a lane loads / computes the loss of
   extern __shared__ int elist[];
+  // diagnostic (stamps): kernel entry, for the prologue share of a launch (stamps[10], 10 ns ticks)
+  const int64_t r_entry = pa.stamps != nullptr ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int B = a.B, Din = a.Din;
   const int estride = al4(pa.num_samples);
   const int S = (pa.num_samples + B - 1) / B;
-  const int e0 = pa.cursor[0], j0 = pa.cursor[1];
+  const int e0 = pa.has_start ? pa.start_e : pa.cursor[0], j0 = pa.has_start ? pa.start_j : pa.cursor[1];
   const int64_t pos0 = (int64_t)e0 * S + j0;
   const int n = pa.n_steps;
-  const int T = (int)((pos0 + n - 1) / S - pos0 / S);
+  const int T = (j0 + n - 1) / S;  // epoch barriers crossed (j0 < S)
   auto list = [&](int e) { return elist + (e & 1) * estride; };
+  // diagnostic prologue split (stamps[11..13], 10 ns ticks): position known, list in LDS, after the barrier
+  int64_t r_pro[3] = {0, 0, 0};
+  auto pstamp = [&](int k) {
+    if (pa.stamps != nullptr) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      r_pro[k] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    }
+  };
+  pstamp(0);
 
   // Only the first epoch's list is on the path to step 0. The next one is
   // zero-filled (row 0: the trainer reads stale-but-valid indices for the kNB
@@ -692,16 +703,41 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   // barrier, while the trainer runs epoch e0.
   // With a list cache (pa.lcache) a launch that starts inside an already
   // computed epoch copies its list instead of recomputing the permutation.
+  // The trainer wave's parameters and momenta are read first: their latency
+  // overlaps the epoch list's (both on the path to step 0).
+  const int lane = (int)threadIdx.x;
+  const int q = (lane & 63) >> 4, i = lane & 15;  // feature group, row slot
+  const int k0 = q * KP;
+  const bool hb = a.has_bias != 0;
+  const bool use_mom = a.mom != nullptr && a.momentum != 0.f;
+  const int nW = DOUT * Din;
+  float W[DOUT][KP], M[DOUT][KP], Wb[DOUT], Mb[DOUT];
+  if (wave == 0) {
+    const auto P = gptr(a.P);
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        const bool in = k0 + k < Din;
+        W[c][k] = in ? P[c * Din + k0 + k] : 0.f;
+        M[c][k] = (in && use_mom) ? gptr(a.mom)[c * Din + k0 + k] : 0.f;
+      }
+      Wb[c] = hb ? P[nW + c] : 0.f;
+      Mb[c] = (hb && use_mom) ? gptr(a.mom)[nW + c] : 0.f;
+    }
+  }
   const ListCache lc{pa.lcache, pa.ltag, estride};
   rank_epoch_indices_or(given_list(pa, e0), list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
                      (int)threadIdx.x, kThreads, lc);
   for (int k = (int)threadIdx.x; k < pa.num_samples; k += kThreads) list(e0 + 1)[k] = 0;
+  pstamp(1);
   // Loss ring (pa.loss_ring): the trainer stores each lane's scaled loss share
   // per step (one ds_write), the helper waves add the 64 shares and write
   // losses[] -- the per-step cross-lane loss reduction leaves the critical path.
   const int ring = pa.loss_ring ? 2 * S + kNB : 0;  // slots; 2 epochs + prefetch depth never overwrite unread
   float* const lring = reinterpret_cast<float*>(elist + 2 * estride + 16);  // after the 8 u64 timer slots
   __syncthreads();
+  pstamp(2);
   if (wave != 0) {
     const int ht = (int)threadIdx.x - 64, hn = kThreads - 64;
     int64_t lo = pos0;
@@ -734,33 +770,12 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     return;
   }
 
-  const int lane = (int)threadIdx.x;
-  const int q = lane >> 4, i = lane & 15;  // feature group, row slot
-  const int k0 = q * KP;
   const int rho_own = SCATTER ? (q & (R - 1)) : 0;  // the row whose loss this lane computes
-  const bool hb = a.has_bias != 0;
-  const bool use_mom = a.mom != nullptr && a.momentum != 0.f;
   const float lr = a.lr, mu = a.momentum, damp = a.dampening, wd = a.weight_decay;
   const int nesterov = a.nesterov;
   const auto X = gptr(a.X);
-  const int nW = DOUT * Din;
   const int ldx = a.ldx > 0 ? a.ldx : Din;  // feature slots past Din read X's zero padding
 
-  float W[DOUT][KP], M[DOUT][KP], Wb[DOUT], Mb[DOUT];
-  {
-    const auto P = gptr(a.P);
-#pragma unroll
-    for (int c = 0; c < DOUT; ++c) {
-#pragma unroll
-      for (int k = 0; k < KP; ++k) {
-        const bool in = k0 + k < Din;
-        W[c][k] = in ? P[c * Din + k0 + k] : 0.f;
-        M[c][k] = (in && use_mom) ? gptr(a.mom)[c * Din + k0 + k] : 0.f;
-      }
-      Wb[c] = hb ? P[nW + c] : 0.f;
-      Mb[c] = (hb && use_mom) ? gptr(a.mom)[nW + c] : 0.f;
-    }
-  }
   int opt_step = a.opt_step ? *a.opt_step : 0;
   const XgmiArgs& ar = a.ar;
   const int world = AR ? ar.world : 1;
@@ -1120,6 +1135,12 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
       for (int k = 0; k < 6; ++k) pa.stamps[k] += (int64_t)tk.acc[k];
       pa.stamps[7] += (int64_t)__builtin_amdgcn_s_memtime() - t_begin;
       pa.stamps[8] += (int64_t)__builtin_amdgcn_s_memrealtime() - r_begin;
+      pa.stamps[10] += r_begin - r_entry;
+      if (pa.stamps_n >= 14) {
+        pa.stamps[11] += r_pro[0] - r_entry;
+        pa.stamps[12] += r_pro[1] - r_pro[0];
+        pa.stamps[13] += r_pro[2] - r_pro[1];
+      }
     }
   }
 }

@@ -222,7 +222,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   // positions are produced S+1 steps ahead inside the loop)
   const int ns = pa.num_samples;
   const int S = (ns + B - 1) / B;
-  const int e0 = pa.cursor[0], j0 = pa.cursor[1];
+  const int e0 = pa.has_start ? pa.start_e : pa.cursor[0], j0 = pa.has_start ? pa.start_j : pa.cursor[1];
   const int n = pa.n_steps;
   const uint32_t Nn = (uint32_t)pa.N;
   const ListCache lc{pa.lcache, pa.ltag, d.estride};

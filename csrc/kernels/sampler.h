@@ -85,17 +85,55 @@ struct ListCache {
 // The epoch's list from a caller-provided index array (e.g. the host's torch-
 // identical DistributedSampler order) when `given` is set, else from the cache
 // when it holds `epoch`, else the Feistel one (also written to the cache).
+// Copy of a global list into LDS with every load in flight at once (up to
+// kListSpec entries per thread): the plain loop waited for each unrolled group of
+// 4 loads, two global round trips for 8 entries per thread, on the path to step 0.
+constexpr int kListSpec = 16;
+__device__ __forceinline__ void list_load(const int32_t* src, int num_samples, int tid, int nt, int32_t (&v)[kListSpec]) {
+#pragma unroll
+  for (int u = 0; u < kListSpec; ++u) {
+    const int i = tid + u * nt;
+    v[u] = i < num_samples ? src[i] : 0;
+  }
+}
+__device__ __forceinline__ void list_store(int32_t* out, int num_samples, int tid, int nt, const int32_t (&v)[kListSpec]) {
+#pragma unroll
+  for (int u = 0; u < kListSpec; ++u) {
+    const int i = tid + u * nt;
+    if (i < num_samples) out[i] = v[u];
+  }
+}
+
 __device__ __forceinline__ void rank_epoch_indices_or(const int32_t* given, int32_t* out, uint32_t N, int W, int rank,
                                                       int num_samples, uint64_t seed, int epoch, int shuffle, int tid,
                                                       int nt, const ListCache& lc = ListCache{nullptr, nullptr, 0}) {
+  const bool spec = num_samples <= kListSpec * nt;
   if (given != nullptr) {
-    for (int i = tid; i < num_samples; i += nt) out[i] = given[i];
+    if (spec) {
+      int32_t v[kListSpec];
+      list_load(given, num_samples, tid, nt, v);
+      list_store(out, num_samples, tid, nt, v);
+    } else {
+      for (int i = tid; i < num_samples; i += nt) out[i] = given[i];
+    }
     return;
   }
-  if (lc.lists != nullptr && __builtin_amdgcn_readfirstlane(lc.tag[epoch & 1]) == epoch) {
+  if (lc.lists != nullptr) {
+    // the slot's entries are read together with its tag (speculatively: the slot is
+    // allocated whatever epoch it holds), one round trip on a hit
     const int32_t* src = lc.lists + (epoch & 1) * lc.stride;
-    for (int i = tid; i < num_samples; i += nt) out[i] = src[i];
-    return;
+    const int tag = lc.tag[epoch & 1];
+    if (spec) {
+      int32_t v[kListSpec];
+      list_load(src, num_samples, tid, nt, v);
+      if (__builtin_amdgcn_readfirstlane(tag) == epoch) {
+        list_store(out, num_samples, tid, nt, v);
+        return;
+      }
+    } else if (__builtin_amdgcn_readfirstlane(tag) == epoch) {
+      for (int i = tid; i < num_samples; i += nt) out[i] = src[i];
+      return;
+    }
   }
   if (lc.lists != nullptr && tid == 0) lc.tag[epoch & 1] = -1;  // slot being overwritten until published
   rank_epoch_indices(out, N, W, rank, num_samples, seed, epoch, shuffle, tid, nt);

@@ -149,6 +149,43 @@ def test_persistent_plan_with_list_cache_equals_per_step(dev, kind):
     torch.testing.assert_close(res[0], res[1], rtol=tol, atol=tol)
 
 
+@pytest.mark.parametrize("kind", ["linear_mse", "mlp_tp"])
+def test_persistent_plan_launch_at_equals_device_cursor(dev, kind):
+    """PersistentPlan.launch_at(n, pos) (start position from the host's step count, no
+    cursor load at kernel entry) runs bitwise the same trajectory as launch(n) from the
+    device cursor, and leaves the cursor where launch(n) does."""
+    from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP, ddp_toy_model
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+
+    if kind == "linear_mse":
+        X, Y = torch.rand(640, 20, device=dev), torch.rand(640, 1, device=dev)
+        mk, loss = (lambda: ddp_toy_model()), "mse"
+    else:
+        X, Y = torch.randn(500, 20, device=dev), torch.randint(0, 10, (500,), device=dev)
+        mk, loss = (lambda: ToyMLP(20, 64, 10)), "ce_index"
+    splits = [1, 5, 37, 3, 20, 43, 41]
+    res, curs, engines = [], [], []
+    for mode in ("cursor", "at"):
+        torch.manual_seed(7)
+        eng = FusedMLPStep(mk().to(dev), loss=loss, lr=0.05, momentum=0.9)
+        sampler = DeviceDistributedSampler(X.shape[0], 1, 0, seed=1, device=dev)
+        cursor = torch.zeros(2, dtype=torch.int32, device=dev)
+        losses = torch.zeros(max(splits), device=dev)
+        plan = eng.persistent_plan(X, Y, 32, sampler, cursor, losses)
+        pos = 0
+        for n in splits:
+            plan.launch(n) if mode == "cursor" else plan.launch_at(n, pos)
+            pos += n
+        torch.cuda.synchronize()
+        res.append(eng.P.clone())
+        curs.append(cursor.tolist())
+        engines.append(eng.persistent_engine(32, sampler))
+    assert engines[0].startswith("tp" if kind == "mlp_tp" else "wave"), engines[0]
+    assert curs[0] == curs[1]
+    assert torch.equal(res[0], res[1])
+
+
 @pytest.mark.parametrize("kind", ["mlp", "linear", "linear_rows"])
 def test_persistent_engine_two_ranks_one_gpu(tmp_path, kind):
     world = 2
