@@ -175,6 +175,8 @@ struct TpStage {
 };
 constexpr int kTpLD2 = 20;  // W2 slice (classes x 16 units), b128 rows
 constexpr int kTpLDT = 36;  // per-wave transposes: 16 (class / unit) x 32 rows
+constexpr int kTpLossRing = 32;  // loss-ring slots (power of two)
+constexpr int kTpLossFlush = 16; // steps per flush: the slots being added are never the one written meanwhile
 __host__ __device__ __forceinline__ int tp_wave_floats() { return 16 * kTpLD2 + 2 * 16 * kTpLDT + 16; }
 __host__ __device__ __forceinline__ int tp_stage_floats(int MT) { return 32 * (16 * MT + 4) + 16 * MT * 36 + 32 * 16; }
 
@@ -215,6 +217,27 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   float* const Th = W2m + 16 * LD2;                           // [16 units][LDT] H^T of this slice
   float* const Tdz = Th + 16 * LDT;                           // [16 classes][LDT] dZ^T
   float* const B2m = Tdz + 16 * LDT;                          // [16] b2 (the forward's class-4q+i reads)
+  // [kTpLossRing][64] loss ring (16-B aligned, after the keys): wave 0 stores each lane's
+  // scaled loss share per step; every kTpLossFlush steps all waves add the shares of the
+  // past kTpLossFlush slots in lane order
+  float* const lring = lds + al4((int)(reinterpret_cast<float*>(fkeys) - lds) + 48);
+  auto flush_losses = [&](int lo, int hi) {  // steps [lo, hi), hi - lo <= kTpLossFlush
+    const int j = w + NW * l;
+    if (j < hi - lo) {
+      const int step = lo + j;
+      const f4* sh = reinterpret_cast<const f4*>(lring + (step & (kTpLossRing - 1)) * 64);
+      float acc = 0.f;
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const f4 v = sh[u];
+        acc += v[0];
+        acc += v[1];
+        acc += v[2];
+        acc += v[3];
+      }
+      pa.losses[step] = acc;
+    }
+  };
   auto list = [&](int e) { return elist + (e % 3) * d.estride; };
   auto stage = [&](int slot) { return stage0 + slot * St::FLOATS; };
 
@@ -453,7 +476,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     stage_sel(w1 ? e0 + 1 : e0, w1 ? 0 : j0 + 1);
   }
 
-  float* const losses = pa.losses;
+  const float inv_full = 1.f / (float)(LOSS == kLossMSE ? B * Dout : B);
   // last step's (averaged) gradients, written to the DDP bucket at the end
   float lg1[MT][4], lg2[4], ldb2 = 0.f;
 #pragma unroll
@@ -531,24 +554,28 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 #pragma unroll
       for (int i = 0; i < 4; ++i) Th[(4 * q + i) * LDT + 16 * t + c] = ht[t][i];
     stage_write(sn);
+    // wave-private or previous-step data the loss needs, read before the barrier so
+    // that only the partial logits are waited for after it: b2 (this wave's mirror)
+    // and the current batch's targets (staged in slot sc before the last barrier)
+    const f4 b2v = *reinterpret_cast<const f4*>(B2m + 4 * q);
+    const float* const ys = st + St::Y_OFF;
+    int yl[2];
+    f4 yf[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if constexpr (LOSS == kLossCEIndex) yl[t] = reinterpret_cast<const int*>(ys)[16 * t + c];
+      else yf[t] = *reinterpret_cast<const f4*>(ys + (16 * t + c) * 16 + 4 * q);
+    }
     tick(1);
     __syncthreads();
-    {  // the rows of position k + 2 (its list entries were produced before this barrier)
-      const bool w2 = nj + 1 == S;
-      stage_sel(w2 ? ne + 1 : ne, w2 ? 0 : nj + 1);
-    }
     if constexpr (ST) {  // the barrier alone (per wave, stamps[13 + w])
       const int64_t t = (int64_t)__builtin_amdgcn_s_memtime();
       acc_bar += t - tmark;
       tmark = t;
     }
     float zf[2][4];
-    const f4 b2v = *reinterpret_cast<const f4*>(B2m + 4 * q);
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) zf[t][i] = b2v[i];
-    // all partial reads in flight before the first add (a runtime-count loop waited on each)
+    // all partial reads in flight before the first add (a runtime-count loop waited on
+    // each), and ahead of the next rows' list reads in the LDS queue
     f4 pz[4][2];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
@@ -558,15 +585,23 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         pz[v][1] = src[64];
       }
     }
+    {  // the rows of position k + 2 (its list entries were produced before this barrier)
+      const bool w2 = nj + 1 == S;
+      stage_sel(w2 ? ne + 1 : ne, w2 ? 0 : nj + 1);
+    }
+    if ((k & (kTpLossFlush - 1)) == 0 && k > 0) flush_losses(k - kTpLossFlush, k);  // shares written before this barrier
+    f4 zs[2] = {b2v, b2v};
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {  // wave order: identical sums in every wave
+    for (int v = 0; v < 4; ++v) {  // wave order: identical sums in every wave (vector adds: v_pk_add_f32)
       if (v < NW) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          zf[0][i] += pz[v][0][i];
-          zf[1][i] += pz[v][1][i];
-        }
+        zs[0] += pz[v][0];
+        zs[1] += pz[v][1];
       }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      zf[0][i] = zs[0][i];
+      zf[1][i] = zs[1][i];
     }
     tick(2);
 
@@ -574,13 +609,12 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     float g[2][4];
     float lsum = 0.f;
     int cnt = 0;
-    const float* const ys = st + St::Y_OFF;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int row = 16 * t + c;
       const bool rv = row < nb;
       if constexpr (LOSS == kLossMSE) {
-        const f4 y = *reinterpret_cast<const f4*>(ys + row * 16 + 4 * q);
+        const f4 y = yf[t];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const bool ok = rv && 4 * q + i < Dout;
@@ -602,7 +636,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         se = rows4_sum(se);
         const float rse = __builtin_amdgcn_rcpf(se);  // softmax = e / se (v_rcp_f32); the log only feeds the loss
         if constexpr (LOSS == kLossCEIndex) {
-          const int y = reinterpret_cast<const int*>(ys)[row];
+          const int y = yl[t];
           const bool use = rv && y != a.ignore_index;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -616,7 +650,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
           }
           cnt += __popcll(__ballot(use && q == 0));
         } else {  // soft targets: -(t . log_softmax(z)), grad = softmax * sum(t) - t
-          const f4 y = *reinterpret_cast<const f4*>(ys + row * 16 + 4 * q);
+          const f4 y = yf[t];
           float ts = 0.f;
 #pragma unroll
           for (int i = 0; i < 4; ++i) ts += y[i];  // classes >= Dout stage as 0
@@ -635,19 +669,19 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         }
       }
     }
+    // 1 / count: the full batch's value precomputed (uniform branch; the IEEE division
+    // only for a short batch or ignored targets)
     float inv;
     if constexpr (LOSS == kLossCEIndex) {
       cnt = __builtin_amdgcn_readfirstlane(cnt);
-      inv = 1.f / (float)(cnt > 0 ? cnt : 1);
-    } else if constexpr (LOSS == kLossMSE) {
-      inv = 1.f / (float)(nb * Dout);
+      if (cnt == B) inv = inv_full;
+      else inv = 1.f / (float)(cnt > 0 ? cnt : 1);
     } else {
-      inv = 1.f / (float)nb;
+      if (nb == B) inv = inv_full;
+      else inv = 1.f / (float)(LOSS == kLossMSE ? nb * Dout : nb);
     }
-    if (w == 0) {  // the step's loss: one wave reduces and reports it
-      lsum = wave_sum(lsum);
-      if (l == 0) losses[k] = (LOSS == kLossCEIndex && cnt == 0) ? NAN : lsum * inv;
-    }
+    if (w == 0)  // this lane's share of the step's loss (added up by flush_losses, off the critical path)
+      lring[(k & (kTpLossRing - 1)) * 64 + l] = (LOSS == kLossCEIndex && cnt == 0) ? NAN : lsum * inv;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       g[0][i] *= inv;
@@ -777,6 +811,12 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     tick(5);
   }
 
+  if (n > 0) {  // the remaining loss shares
+    __syncthreads();
+    const int kf = ((n - 1) / kTpLossFlush) * kTpLossFlush;
+    flush_losses(kf, n);
+  }
+
   // ---- write back: parameters, momentum, the last step's averaged gradients (DDP bucket)
   float* const Pw = a.P;
   float* const Gw = a.G;
@@ -850,7 +890,7 @@ bool tp_vec_x(const FusedMlpArgs& a) {
 size_t tp_lds_bytes(const FusedMlpArgs& a, const PersistArgs& p) {
   const int NW = a.H / 16;
   const size_t fl = (size_t)3 * al4(p.num_samples) + (size_t)3 * tp_stage_floats(tp_mt(a)) +
-                    (size_t)2 * NW * 64 * 8 + (size_t)NW * tp_wave_floats() + 48;
+                    (size_t)2 * NW * 64 * 8 + (size_t)NW * tp_wave_floats() + 48 + 3 + (size_t)kTpLossRing * 64;
   return fl * sizeof(float);
 }
 

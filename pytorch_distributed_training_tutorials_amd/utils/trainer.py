@@ -258,7 +258,7 @@ class Trainer:
         shard = _Shard(self.world_size, self.rank, n)
         plan = self.engine.persistent_plan(X, Y, dl.batch_size, shard, self._cursor, self._loss_buf[:E * S],
                                            idx=lists, idx_e0=e0)
-        plan.launch(E * S, e0 * S)
+        plan.launch_at(E * S, e0 * S)  # start position from the arguments (the cursor copy is for the end state)
         self.global_step += E * S
         if self.xgmi is not None and self._xgmi_failed():
             self._fallback_to_rccl(e0, e1, restore)
