@@ -322,7 +322,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_kernel(FusedMlpArgs a, P
     for (int ry = 0; ry < RY; ++ry) {
       const int sel = SPLIT ? sel_y_next : sel_next[ry];
       if constexpr (LOSS == kLossCEIndex) {
-        f.yi[ry] = (int)gptr(a.Yi)[sel];
+        f.yi[ry] = reinterpret_cast<const int*>(a.Yi)[2 * (int64_t)sel];  // low dword (see mlp_tp.hip)
       } else {
 #pragma unroll
         for (int c = 0; c < DOUT; ++c) f.y[ry][c] = gptr(a.Yf)[(int64_t)sel * DOUT + c];
@@ -819,7 +819,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     for (int ry = 0; ry < RY; ++ry) {
       const int sel = SCATTER ? sel_y_next : sel_next[ry];
       if constexpr (LOSS == kLossCEIndex) {
-        f.yi[ry] = (int)gptr(a.Yi)[sel];
+        f.yi[ry] = reinterpret_cast<const int*>(a.Yi)[2 * (int64_t)sel];  // low dword (see mlp_tp.hip)
       } else {
 #pragma unroll
         for (int c = 0; c < DOUT; ++c) f.y[ry][c] = gptr(a.Yf)[(int64_t)sel * DOUT + c];

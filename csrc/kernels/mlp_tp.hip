@@ -406,7 +406,10 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 #pragma unroll
     for (int k = 0; k < KY; ++k) {
       if (k < nky) {
-        if constexpr (YI) yv[k] = __int_as_float((int)gptr(a.Yi)[ysel[k]]);
+        // the low dword of the int64 label only: a dwordx2 load left its dead high half to
+        // the register allocator, which reused it in the forward behind a vmcnt(0) -- a
+        // stall on this step's batch loads every step
+        if constexpr (YI) yv[k] = __int_as_float(reinterpret_cast<const int*>(a.Yi)[2 * (int64_t)ysel[k]]);
         else yv[k] = gptr(a.Yf)[(int64_t)ysel[k] * Dout + ycol[k]];
       }
     }
@@ -507,14 +510,17 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     const int ne = wrap ? ce + 1 : ce, nj = wrap ? 0 : cj + 1;
     const int sn = sc == 2 ? 0 : sc + 1;
     const int nb = min(B, ns - cj * B);
-    stage_issue();  // position k + 1 (rows read last step); stale-but-valid past the launch
-    tick(0);
+    // list production BEFORE the batch loads: no global load is outstanding here, so the
+    // vmcnt(0) waits hipcc places in the producer (VGPR reuse, the given-list path) cost
+    // nothing; after stage_issue they stalled every C-th step for a full load round trip
     if (pc == 0) {
       produce(wrap ? ce + 2 : ce + 1, wrap ? 0 : cj + 1);
       pc = C;
     }
     --pc;
     tick(6);
+    stage_issue();  // position k + 1 (rows read last step); stale-but-valid past the launch
+    tick(0);
     const float* const st = stage(sc);
 
     // ---------------- fwd1: HT = W1aug . Xaug^T (this wave's 16 units x 32 rows), ReLU
