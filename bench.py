@@ -24,6 +24,20 @@ the timed region. Engines:
   autograd  native DDP reducer + native Linear/CE/SGD kernels, eager
   reference stock PyTorch-ROCm loop (torch DDP, DataLoader + DistributedSampler,
             nn.Linear, F.cross_entropy, torch.optim.SGD) -- the comparator
+
+Comparator: after the headline, the SAME process times the stock PyTorch-ROCm
+reference loop (``--engine reference`` body: torch DDP over RCCL, DataLoader +
+DistributedSampler, same model/batch/N) and reports ``ref_samples_per_s`` and
+``speedup_vs_torch``; ``vs_baseline`` is that same-node ratio ("the
+like-for-like comparator is the unmodified reference scripts running on
+PyTorch-ROCm on the same node"), the survey's CPU/gloo probe ratio is kept as
+``vs_cpu_probe``.
+
+Deadline: the whole run is bounded by ``--deadline`` seconds (default 420, under
+the driver's limit) and every communicator by ``PTDT_COMM_TIMEOUT`` (default
+120 s here). On expiry every rank aborts its communicators, rank 0 prints one
+JSON line with ``"error"`` and the phase the run died in, and the process exits
+non-zero (utils/deadline.py) -- no new process, no re-exec.
 """
 from __future__ import annotations
 
@@ -72,6 +86,14 @@ def parse(argv=None):
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
     ap.add_argument("--no_mlp_side", action="store_true",
                     help="skip the extra toy-MLP measurement (mlp_us_per_step) after the headline run")
+    ap.add_argument("--deadline", type=float, default=float(os.environ.get("PTDT_BENCH_DEADLINE", 420)),
+                    help="whole-run deadline in seconds (0: none); on expiry an error JSON line is printed")
+    ap.add_argument("--no_ref", action="store_true",
+                    help="skip the same-process stock PyTorch-ROCm comparator after the headline")
+    ap.add_argument("--ref_steps", type=int, default=None,
+                    help="timed steps of the comparator (default max(--steps, 256); its warmup max(--warmup, 32))")
+    ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"],
+                    help="cpu: the reference engine on gloo (CPU plumbing / deadline tests)")
     ap.add_argument("--share_gpu", action="store_true",
                     help="REHEARSAL ONLY: every rank on cuda:0 with a gloo control plane (RCCL refuses two ranks "
                          "per GPU), to exercise the N>1 path (xGMI self-test, in-kernel all-reduce, replica-sync "
@@ -79,13 +101,13 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
-def _setup(args):
+def _setup(args, cpu: bool):
     from pytorch_distributed_training_tutorials_amd.parallel import env
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
-    env.init_process_group("gloo" if args.share_gpu else "nccl")
+    env.init_process_group("gloo" if (args.share_gpu or cpu) else "nccl")
     return env.rank(), env.world_size(), env.local_rank()
 
 
@@ -413,12 +435,20 @@ def run_autograd(args, rank, world, dev, comm):
 
 
 # --------------------------------------------------------------------------- reference
-def run_reference(args, rank, world, dev, comm):
-    """Stock PyTorch-ROCm loop with the reference's structure (comparator)."""
+def run_reference(args, rank, world, dev, comm, steps=None, warmup=None):
+    """Stock PyTorch-ROCm loop with the reference's structure (comparator):
+    reference ddp_gpus_torchrun.py:16-88 with synthetic data of the same shape."""
     import torch.nn.functional as F
     from torch.nn.parallel import DistributedDataParallel as TorchDDP
     from torch.utils.data import DataLoader, TensorDataset
     from torch.utils.data.distributed import DistributedSampler as TorchSampler
+
+    from pytorch_distributed_training_tutorials_amd.utils.faults import FaultInjector
+
+    faults = FaultInjector(rank)
+    steps = args.steps if steps is None else steps
+    warmup = args.warmup if warmup is None else warmup
+    cuda = dev.type == "cuda"
 
     torch.manual_seed(args.seed)
     g = torch.Generator().manual_seed(args.seed)
@@ -430,12 +460,12 @@ def run_reference(args, rank, world, dev, comm):
                            torch.randint(0, 10, (args.dataset_size,), generator=g))
         model = torch.nn.Sequential(torch.nn.Linear(20, 64), torch.nn.ReLU(), torch.nn.Linear(64, 10)).to(dev)
     sampler = TorchSampler(ds, num_replicas=world, rank=rank)
-    loader = DataLoader(ds, batch_size=args.batch_size, pin_memory=True, shuffle=False, sampler=sampler)
-    ddp = TorchDDP(model, device_ids=[dev.index])
+    loader = DataLoader(ds, batch_size=args.batch_size, pin_memory=cuda, shuffle=False, sampler=sampler)
+    ddp = TorchDDP(model, device_ids=[dev.index] if cuda else None)
     opt = torch.optim.SGD(model.parameters(), lr=args.lr)
-    state = {"epoch": 0, "it": None}
+    state = {"epoch": 0, "it": None, "step": 0}
 
-    def steps(n):
+    def run(n):
         for _ in range(n):
             batch = next(state["it"], None) if state["it"] is not None else None
             if batch is None:
@@ -443,6 +473,8 @@ def run_reference(args, rank, world, dev, comm):
                 state["epoch"] += 1
                 state["it"] = iter(loader)
                 batch = next(state["it"])
+            faults.check(state["step"])
+            state["step"] += 1
             xs, ys = batch
             xs, ys = xs.to(dev), ys.to(dev)
             opt.zero_grad()
@@ -450,18 +482,23 @@ def run_reference(args, rank, world, dev, comm):
             l.backward()
             opt.step()
 
-    steps(max(args.warmup, 1))
-    t = _timed(comm, dev, lambda: steps(args.steps))
+    run(max(warmup, 1))
+    t = _timed(comm, dev, lambda: run(steps))
     return t, {"kernels": "stock torch: DataLoader+DistributedSampler, nn.Linear, F.cross_entropy, torch DDP, SGD"}
 
 
 # --------------------------------------------------------------------------- timing
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def _timed(comm, dev, fn):
     comm.barrier()
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     t0 = time.perf_counter()
     fn()
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     t1 = time.perf_counter()  # this rank's work is done; the barrier below only re-aligns the ranks
     comm.barrier()
     el = torch.tensor([t1 - t0], device=dev, dtype=torch.float64)
@@ -470,15 +507,80 @@ def _timed(comm, dev, fn):
     return float(el.item())
 
 
+def _record(args, world, value, elapsed, extra):
+    gb = args.batch_size * world
+    base = BASELINE_SAMPLES_PER_S.get(world)
+    ref = extra.get("ref_samples_per_s")
+    rec = {
+        "metric": METRIC,
+        "value": None if value is None else round(value, 1),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": None if elapsed is None else round(1e3 * elapsed / args.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / ref, 3) if (value and ref) else None,
+        "vs_cpu_probe": round(value / base, 3) if (value and base) else None,
+        "dtype": "fp32",
+        "data": "synthetic (uniform [0,1) features/targets generated on device, 2048 samples), random-init weights",
+        "config": {"model": "ddp_gpus_torchrun toy: Linear(20,1) + F.cross_entropy(soft targets) + SGD(lr=1e-2)"
+                   if args.model == "linear" else "toy MLP Linear(20,64)-ReLU-Linear(64,10) + CE + SGD",
+                   "global_batch": gb, "per_device_batch": args.batch_size, "seq_len": None,
+                   "dataset_size": args.dataset_size, "parallelism": f"dp{world}", "engine": args.engine},
+        "baseline_note": "vs_baseline = value / ref_samples_per_s: the stock PyTorch-ROCm reference loop (torch DDP "
+                         "over RCCL, DataLoader+DistributedSampler, same model/batch/N) timed in this same process "
+                         "after the headline; vs_cpu_probe divides by BASELINE.md's CPU/gloo survey probe; the "
+                         "reference publishes no GPU DDP number",
+        **extra,
+    }
+    return rec
+
+
+def _error_line(args, world, phase, elapsed_s, why):
+    rec = _record(args, world, None, None, {})
+    rec.update({"error": why, "phase": phase, "elapsed_s": round(elapsed_s, 1)})
+    return json.dumps(rec)
+
+
+def _comparator(args, rank, world, dev, comm):
+    """The stock PyTorch-ROCm loop at the same N, in this process, after the headline."""
+    steps = args.ref_steps or max(args.steps, 256)
+    warm = max(args.warmup, 32)
+    t, _ = run_reference(args, rank, world, dev, comm, steps=steps, warmup=warm)
+    sps = steps * args.batch_size * world / t
+    return {"ref_samples_per_s": round(sps, 1), "ref_ms_per_step": round(1e3 * t / steps, 4), "ref_steps": steps,
+            "ref_warmup": warm, "ref_engine": "stock torch DDP (RCCL) + DataLoader/DistributedSampler + nn.Linear + "
+                                              "F.cross_entropy + torch.optim.SGD, same process"}
+
+
 def main(argv=None):
     args = parse(argv)
-    if not torch.cuda.is_available():
-        raise SystemExit("bench.py needs a GPU (MI355X)")
-    rank, world, local = _setup(args)
-    dev = torch.device("cuda", 0 if args.share_gpu else local)
+    cpu = args.device == "cpu" or (args.device == "auto" and not torch.cuda.is_available())
+    if cpu and args.engine != "reference":
+        raise SystemExit("bench.py needs a GPU (MI355X) for the framework engines; --device cpu runs "
+                         "--engine reference only")
+    os.environ.setdefault("PTDT_COMM_TIMEOUT", "120")  # a hung collective aborts well inside --deadline
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    rank_env = int(os.environ.get("RANK", "0"))
+    from pytorch_distributed_training_tutorials_amd.utils.deadline import Deadline
+
+    def expire(phase, elapsed):
+        why = f"deadline of {args.deadline:.0f} s expired"
+        if rank_env == 0:
+            print(_error_line(args, world_env, phase, elapsed, why), flush=True)
+        print(f"[bench] rank {rank_env}: {why} in phase {phase!r}; aborting communicators and exiting",
+              file=sys.stderr, flush=True)
+
+    dl = Deadline(args.deadline, expire)
+    dl.set_phase("process group init")
+    rank, world, local = _setup(args, cpu)
+    dev = torch.device("cpu") if cpu else torch.device("cuda", 0 if args.share_gpu else local)
     from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
     from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
 
+    dl.set_phase("communicator init")
     if args.share_gpu:
         if args.engine not in ("persistent", "fused") or args.allreduce == "rccl":
             raise SystemExit("--share_gpu rehearses the xGMI engines only (RCCL needs one GPU per rank)")
@@ -486,43 +588,31 @@ def main(argv=None):
         comm = comm_mod.HostStagedComm(dev)
     else:
         comm = comm_mod.get_default(dev)
+        dl.register(comm.handle)
     runner = {"persistent": run_persistent, "fused": run_fused, "autograd": run_autograd,
               "reference": run_reference}[args.engine]
+    dl.set_phase(f"headline ({args.engine} engine: build, warmup, timed run)")
     elapsed, extra = runner(args, rank, world, dev, comm)
-    gb = args.batch_size * world
-    samples = args.steps * gb
-    value = samples / elapsed
-    base = BASELINE_SAMPLES_PER_S.get(world)
-    rec = {
-        "metric": METRIC,
-        "value": round(value, 1),
-        "unit": "samples/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(1e3 * elapsed / args.steps, 5),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": round(value / base, 3) if base else None,
-        "dtype": "fp32",
-        "data": "synthetic (uniform [0,1) features/targets generated on device, 2048 samples), random-init weights",
-        "config": {"model": "ddp_gpus_torchrun toy: Linear(20,1) + F.cross_entropy(soft targets) + SGD(lr=1e-2)"
-                   if args.model == "linear" else "toy MLP Linear(20,64)-ReLU-Linear(64,10) + CE + SGD",
-                   "global_batch": gb, "per_device_batch": args.batch_size, "seq_len": None,
-                   "dataset_size": args.dataset_size, "parallelism": f"dp{world}", "engine": args.engine},
-        "baseline_note": "vs_baseline divides by BASELINE.md's survey probe of the unmodified reference loop "
-                         "(CPU/gloo, same N); the reference publishes no GPU DDP number",
-        **extra,
-    }
+    value = args.steps * args.batch_size * world / elapsed
+    if not (args.no_ref or args.share_gpu or args.engine == "reference"):
+        dl.set_phase("comparator (stock PyTorch-ROCm reference loop)")
+        extra.update(_comparator(args, rank, world, dev, comm))
+        extra["speedup_vs_torch"] = round(value / extra["ref_samples_per_s"], 3)
+    dl.set_phase("report")
+    rec = _record(args, world, value, elapsed, extra)
     if args.share_gpu:
         rec["rehearsal"] = f"{world} ranks sharing cuda:0 (no xGMI hop): protocol/correctness check, not a scaling number"
+    if cpu:
+        rec["device"] = "cpu (gloo): plumbing run of the reference loop, not an MI355X number"
     if rank == 0:
         line = json.dumps(rec)
         print(line, flush=True)
         if args.out:
             with open(args.out, "a") as f:
                 f.write(line + "\n")
+    dl.set_phase("teardown")
     destroy_process_group()
+    dl.cancel()
 
 
 if __name__ == "__main__":

@@ -50,13 +50,14 @@ class ResidualLink:
     gradients of the shared activation (two reads and a write of it).
 
     Ordering is autograd's own: the producer's backward runs only after every
-    consumer of its output, the linking BN included, has run its backward."""
+    consumer of its output, the linking BN included, has run its backward. Each
+    backward pass (a retained graph may run several) re-delivers: the consumer
+    stores, the producer takes and clears; None means the consumer did not run."""
 
-    __slots__ = ("dres", "armed")
+    __slots__ = ("dres",)
 
     def __init__(self):
         self.dres = None
-        self.armed = False
 
 
 class _BatchNormActFn(torch.autograd.Function):
@@ -70,8 +71,6 @@ class _BatchNormActFn(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.link_in, ctx.link_out = link_in, link_out
-        if link_in is not None:
-            link_in.armed = True
         # ReLU mask in the backward: from y with a residual; without one it is recomputed
         # from x and the saved scale/shift (bit-exact), so y need not be read (or kept)
         ctx.save_for_backward(x, y if (relu and residual is not None) else None, weight, stats)
@@ -85,9 +84,9 @@ class _BatchNormActFn(torch.autograd.Function):
         want_dres = ctx.has_res and (ctx.needs_input_grad[3] or link_in is not None)
         dy = _like(dy, x)
         dy2 = None
-        if link_out is not None and link_out.armed:  # a later block's residual gradient of our output
+        if link_out is not None:  # a later block's residual gradient of our output
             # (None: that block's backward did not run -- its output does not reach the loss)
-            dy2, link_out.dres, link_out.armed = link_out.dres, None, False
+            dy2, link_out.dres = link_out.dres, None
             if dy2 is not None and dy2.stride() != dy.stride():
                 dy, dy2 = dy + dy2, None
         sinks = [None, None]

@@ -218,13 +218,20 @@ class FusedAdam(Optimizer):
                 if steps:
                     self._steps[(gi, device)] = torch.full((1,), int(float(steps[0])), dtype=torch.int32,
                                                            device=device)
-                for p in ps:  # the kernels need the flat-state layout: re-home the loaded moments
+                # the kernels need the flat-state layout: pop every loaded moment of the split first,
+                # then re-home them in ONE flat allocation (per-parameter allocations would leave the
+                # group without a contiguous span and every later step on the slower multi-tensor path)
+                loaded = {}
+                for p in ps:
                     st = self.state.get(p, {})
                     if "exp_avg" in st:
-                        m, v = st.pop("exp_avg"), st.pop("exp_avg_sq")
-                        ms, vs = self._state_lists([p])
-                        ms[0].copy_(m)
-                        vs[0].copy_(v)
+                        loaded[p] = (st.pop("exp_avg"), st.pop("exp_avg_sq"))
+                if loaded:
+                    ms, vs = self._state_lists(ps)
+                    for p, m, v in zip(ps, ms, vs):
+                        if p in loaded:
+                            m.copy_(loaded[p][0])
+                            v.copy_(loaded[p][1])
 
     @staticmethod
     def _cpu_step(ps, ms, vs, step, group, gscale):

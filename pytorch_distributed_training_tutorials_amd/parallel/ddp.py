@@ -18,6 +18,7 @@ rebuild in rank 0's observed ready order after the first iteration.
 from __future__ import annotations
 
 import contextlib
+import weakref
 
 import torch
 import torch.nn as nn
@@ -130,20 +131,31 @@ class DistributedDataParallel(nn.Module):
         module called twice) has several producers; the later ones get None and
         return an ordinary gradient, which autograd sums into the first one's
         slot before AccumulateGrad adopts it (writing each into the slot would
-        overwrite the earlier contribution)."""
+        overwrite the earlier contribution).
+
+        The closure holds the wrapper weakly: the parameters outlive a dropped
+        wrapper, which must stay collectable (``__del__`` detaches the sinks)."""
+        ref = weakref.ref(self)
+
         def sink():
-            if getattr(p, "_ptdt_sink_forward", -1) == self._forwards:
+            ddp = ref()
+            if ddp is None or getattr(p, "_ptdt_sink_forward", -1) == ddp._forwards:
                 return None
-            p._ptdt_sink_forward = self._forwards
-            return self.reducer.grad_view(i)
+            p._ptdt_sink_forward = ddp._forwards
+            return ddp.reducer.grad_view(i)
         return sink
 
     def _make_hook(self, i: int):
+        ref = weakref.ref(self)  # as in _make_sink: parameters must not keep the wrapper alive
+
         def hook(_p):
-            if not self._queued and self.reducer.in_backward:
-                self._queued = True
-                torch.autograd.Variable._execution_engine.queue_callback(self._finalize)
-            self.reducer.mark_ready(i)
+            ddp = ref()
+            if ddp is None:
+                return
+            if not ddp._queued and ddp.reducer.in_backward:
+                ddp._queued = True
+                torch.autograd.Variable._execution_engine.queue_callback(ddp._finalize)
+            ddp.reducer.mark_ready(i)
         return hook
 
     def _finalize(self):
@@ -196,6 +208,8 @@ class DistributedDataParallel(nn.Module):
     def __del__(self):
         try:
             self.remove_grad_sinks()
+            for h in getattr(self, "_hooks", ()):
+                h.remove()
         except Exception:  # noqa: BLE001 -- interpreter shutdown
             pass
 

@@ -40,6 +40,7 @@ import time
 import torch
 import torch.nn as nn
 
+from .._ext import native
 from ..data.loader import DeviceDataLoader
 from ..ops.fused_step import FusedMLPStep, _linears
 from ..ops.loss import cross_entropy
@@ -267,6 +268,19 @@ class Trainer:
             self.metrics.write(event="epochs", first=e0, last=e1 - 1, seconds=time.perf_counter() - t0,
                                steps=E * S, engine=self.engine_name)
 
+    def _max_epochs_per_launch(self) -> int:
+        """Epochs one persistent launch may cover: its epoch lists ([E, num_samples] int32),
+        the torch_perm workspace (E * 4n int32 when the permutation state does not fit
+        in LDS) and the loss slots grow with E, so E is bounded by a device-memory budget
+        (``PTDT_PERSIST_EPOCH_BYTES``, default 256 MiB) instead of by ``max_epoch``."""
+        dl = self.train_dataloader
+        n, ns, S = len(dl.dataset), dl._num_samples(), len(dl)
+        per_epoch = 4 * ns + 4 * S
+        if native().torch_perm_needs_ws(n):
+            per_epoch += 16 * n
+        budget = int(os.environ.get("PTDT_PERSIST_EPOCH_BYTES", 256 << 20))
+        return max(1, budget // per_epoch)
+
     def _xgmi_failed(self) -> bool:
         """Did any rank's in-kernel all-reduce time out a poll? Read at the launch's
         closing sync (one flag read per launch, none per step) and agreed by a
@@ -325,7 +339,7 @@ class Trainer:
         per_step = os.environ.get("PTDT_FAULT_RANK") is not None
         while epoch < max_epoch:
             if self.engine_name == "persistent" and not per_step:
-                end = max_epoch
+                end = min(max_epoch, epoch + self._max_epochs_per_launch())
                 if self.snapshot_path and self.save_every:  # one launch per snapshot interval
                     end = min(end, (epoch // self.save_every + 1) * self.save_every)
                 self._run_epochs_persistent(epoch, end)

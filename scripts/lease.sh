@@ -1,0 +1,90 @@
+#!/bin/bash
+# One parameterised GPU-lease script (replaces the per-call scripts of earlier rounds).
+#
+#   gpurun --timeout 1200 -- bash scripts/lease.sh STAGE [STAGE ...]
+#
+# Every GPU step runs under its own `timeout -k 10`, output goes to gpurun_out/<tag>_<step>.*,
+# and the first failing step ends the script (no retries, nothing more on the GPU after a
+# fault / abort / time limit). TAG (env, default "l") prefixes every output file.
+set -o pipefail
+export PYTHONUNBUFFERED=1
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+mkdir -p gpurun_out
+T=${TAG:-l}
+O=gpurun_out
+PORT=$((29500 + RANDOM % 1000))
+
+step() {  # name secs cmd...   (stdout+stderr -> $O/$T_name.log)
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$O/${T}_$name.log" 2>&1
+  local c=$?
+  echo "=== $name exit $c"; tail -4 "$O/${T}_$name.log"
+  [ $c -eq 0 ] || { echo "STOP after $name (exit $c)"; exit $c; }
+}
+jstep() {  # name secs cmd...   (JSON lines appended to $O/$T_name.jsonl, the rest to .err)
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" 2>> "$O/${T}_$name.err" | grep '^{' >> "$O/${T}_$name.jsonl"
+  local c=$?
+  echo "=== $name exit $c"; tail -c 600 "$O/${T}_$name.jsonl"; echo
+  [ $c -eq 0 ] || { echo "STOP after $name (exit $c)"; tail -20 "$O/${T}_$name.err"; exit $c; }
+}
+share() {  # name N bench-args...   (N ranks share cuda:0: protocol rehearsal, not a scaling number)
+  local name=$1 n=$2; shift 2
+  PORT=$((PORT + 1))
+  jstep "$name" 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
+    --master-port $PORT bench.py --gpus "$n" --share_gpu "$@"
+}
+prof() {  # name secs cmd...   (kernel trace + stats under $O/prof_$T_name)
+  local name=$1 secs=$2; shift 2
+  step "prof_$name" "$secs" rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_${T}_$name" -o run -- "$@"
+}
+pmc() {  # name "counters" cmd...   (one counter pass; kill hard on a hang)
+  local name=$1 ctr=$2; shift 2
+  echo "=== pmc_$name ($(date +%T))"
+  timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d "$O/pmc_${T}_$name" -o run -- "$@" \
+    > "$O/${T}_pmc_$name.log" 2>&1
+  local c=$?
+  echo "=== pmc_$name exit $c"; tail -3 "$O/${T}_pmc_$name.log"
+  [ $c -eq 0 ] || exit $c
+}
+PYTEST="python3 -u -m pytest -x -q --timeout 120 --timeout-method thread"
+P1="SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM SQ_INSTS_BRANCH"
+P2="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_INSTS_SMEM"
+
+for s in "$@"; do
+  case $s in
+    tests)     step pytest_gpu 1000 $PYTEST tests -m gpu ;;
+    tests:*)   step "pytest_${s#tests:}" 600 $PYTEST ${s#tests:} ;;  # tests:tests/test_x.py
+    smoke)     step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
+    driver)    for i in 1 2 3; do jstep bench_driver 300 python3 bench.py --gpus 1 --steps 20 --warmup 5; done ;;
+    default)   jstep bench_default 300 python3 bench.py ;;
+    stamps)    jstep stamps 300 python3 bench.py --steps 20000 --warmup 2000 --stamps --no_mlp_side
+               jstep stamps 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --stamps ;;
+    share)     share share 2 --steps 20000 --warmup 2000 --stamps --no_mlp_side
+               share share 4 --steps 20000 --warmup 2000 --stamps --no_mlp_side
+               share share 2 --model mlp --steps 20000 --warmup 2000 --stamps
+               share share 4 --model mlp --steps 5000 --warmup 500 --stamps ;;
+    share_fused) share share_fused 2 --engine fused --steps 2000 --warmup 200
+               share share_fused 4 --engine fused --model mlp --steps 2000 --warmup 200 ;;
+    engines)   jstep engines 300 python3 bench.py --engine fused --steps 2000 --warmup 200
+               jstep engines 300 python3 bench.py --engine fused --steps 2000 --warmup 200 --allreduce rccl
+               jstep engines 300 python3 bench.py --engine autograd --steps 300 --warmup 50
+               jstep engines 300 python3 bench.py --engine reference --steps 300 --warmup 50 ;;
+    apps)      step mp_toy 300 python3 model_parallel.py toy
+               step mp_resnet 600 python3 model_parallel.py resnet --repeat 5 --json $O/${T}_mp_resnet.json --fig $O/${T}_mp_vs_single.png
+               step dp_toy 300 python3 data_parallel.py --quiet ;;
+    resnet)    jstep resnet_ddp 600 python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5
+               jstep resnet_ddp 600 python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5 --impl torch ;;
+    prof)      prof driver 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
+               prof reference 300 python3 bench.py --engine reference --steps 200 --warmup 20 ;;
+    pmc_tp)    pmc tp1 "$P1" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side
+               pmc tp2 "$P2" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side ;;
+    pmc_wave)  pmc wave1 "$P1" python3 bench.py --steps 20000 --warmup 1 --no_mlp_side
+               pmc wave2 "$P2" python3 bench.py --steps 20000 --warmup 1 --no_mlp_side ;;
+    run:*)     step "run" 600 bash -c "${s#run:}" ;;  # ad-hoc: run:'python3 benchmarks/x.py'
+    *)         echo "unknown stage $s"; exit 2 ;;
+  esac
+done
+echo "=== done"

@@ -109,26 +109,28 @@ def xgmi_gpu(rank, world, port, out_dir):
     destroy_process_group()
 
 
-def pipeline_gpu(rank, world, port, out_dir, micro):
-    """ToyModel split over two GPUs and two ranks with RCCL send/recv (NB03:440-450)."""
+def pipeline_gpu(rank, world, port, out_dir, micro, batches=(20, 20, 20)):
+    """ToyModel split over two GPUs and two ranks with RCCL send/recv (NB03:440-450); P2P on
+    the stage's side stream, batch size varying step to step."""
     dev, comm = _init_gpu(rank, world, port)
     import torch.nn as nn
 
     from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
     from pytorch_distributed_training_tutorials_amd.parallel.pipeline import PipelineStage
 
-    torch.manual_seed(0)
-    net1, net2 = nn.Linear(1000, 10), nn.Linear(10, 5)
-    stage_mod = (nn.Sequential(net1, nn.ReLU()) if rank == 0 else net2).to(dev)
+    from ._workers import pipeline_reference_stages
+
+    stage_mod = pipeline_reference_stages(world)[rank].to(dev)
     st = PipelineStage(stage_mod, comm, loss_fn=nn.MSELoss(), micro_batches=micro)
+    assert st._side is not None  # the overlapped (side-stream) P2P path is the one under test
     opt = torch.optim.SGD(stage_mod.parameters(), lr=1e-3)
     g = torch.Generator().manual_seed(1)
     losses = []
-    for _ in range(3):
-        x = torch.randn(20, 1000, generator=g)
-        y = torch.randn(20, 5, generator=g)
+    for b in batches:
+        x = torch.randn(b, 1000, generator=g)
+        y = torch.randn(b, 5, generator=g)
         opt.zero_grad()
-        l = st.train_step(x.to(dev) if rank == 0 else None, y.to(dev) if rank == 1 else None)
+        l = st.train_step(x.to(dev) if rank == 0 else None, y.to(dev) if rank == world - 1 else None)
         opt.step()
         losses.append(None if l is None else float(l))
     torch.save({"params": [p.detach().cpu() for p in stage_mod.parameters()], "losses": losses},

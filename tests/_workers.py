@@ -177,8 +177,9 @@ def xgmi_two_procs_one_gpu(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def pipeline_two_stage(rank, world, port, out_dir, micro):
-    """ToyModel split over 2 ranks (net1+ReLU | net2) with send/recv."""
+def pipeline_two_stage(rank, world, port, out_dir, micro, batches=(20, 20, 20)):
+    """ToyModel split over ``world`` ranks (net1+ReLU | [Linear(10,10)+ReLU ...] | net2) with
+    send/recv; ``batches`` varies the batch size step to step."""
     _init(rank, world, port)
     import torch.nn as nn
 
@@ -186,24 +187,34 @@ def pipeline_two_stage(rank, world, port, out_dir, micro):
     from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
     from pytorch_distributed_training_tutorials_amd.parallel.pipeline import PipelineStage
 
-    torch.manual_seed(0)
-    net1, net2 = nn.Linear(1000, 10), nn.Linear(10, 5)
-    stage_mod = nn.Sequential(net1, nn.ReLU()) if rank == 0 else net2
+    stages = pipeline_reference_stages(world)
+    stage_mod = stages[rank]
     c = comm_mod.get_default()
     st = PipelineStage(stage_mod, c, loss_fn=nn.MSELoss(), micro_batches=micro)
     opt = torch.optim.SGD(stage_mod.parameters(), lr=1e-3)
     g = torch.Generator().manual_seed(1)
     losses = []
-    for _ in range(3):
-        x = torch.randn(20, 1000, generator=g)
-        y = torch.randn(20, 5, generator=g)
+    for b in batches:
+        x = torch.randn(b, 1000, generator=g)
+        y = torch.randn(b, 5, generator=g)
         opt.zero_grad()
-        l = st.train_step(x if rank == 0 else None, y if rank == 1 else None)
+        l = st.train_step(x if rank == 0 else None, y if rank == world - 1 else None)
         opt.step()
         losses.append(None if l is None else float(l))
-    torch.save({"params": [p.detach() for p in stage_mod.parameters()], "losses": losses},
-               os.path.join(out_dir, f"r{rank}.pt"))
+    torch.save({"params": [p.detach() for p in stage_mod.parameters()], "losses": losses,
+                "messages": st.messages}, os.path.join(out_dir, f"r{rank}.pt"))
     destroy_process_group()
+
+
+def pipeline_reference_stages(world):
+    """Seeded stage modules: [Linear(1000,10)+ReLU, (Linear(10,10)+ReLU) x (world-2), Linear(10,5)]."""
+    import torch.nn as nn
+
+    torch.manual_seed(0)
+    mods = [nn.Sequential(nn.Linear(1000, 10), nn.ReLU())]
+    mods += [nn.Sequential(nn.Linear(10, 10), nn.ReLU()) for _ in range(world - 2)]
+    mods.append(nn.Linear(10, 5))
+    return mods
 
 
 def _per_step_reference(eng, X, Y, sampler, n_steps, B, dev):
@@ -351,3 +362,29 @@ def trainer_xgmi_fallback_one_gpu(rank, world, port, out_dir, inject):
     torch.save(out, os.path.join(out_dir, f"r{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def ddp_wrapper_collectable(rank, world, port, out_dir):
+    """A dropped DDP wrapper is collected (its hooks hold it weakly) and the model
+    trains as a plain module afterwards (sink/hook closures held the wrapper)."""
+    _init(rank, world, port)
+    import gc
+    import weakref
+
+    import torch.nn as nn
+
+    from pytorch_distributed_training_tutorials_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+
+    torch.manual_seed(0)
+    model = nn.Sequential(nn.Linear(8, 8), nn.ReLU(), nn.Linear(8, 2))
+    ddp = DistributedDataParallel(model)
+    ddp(torch.randn(4, 8)).sum().backward()
+    ref = weakref.ref(ddp)
+    del ddp
+    gc.collect()
+    model.zero_grad()
+    model(torch.randn(4, 8)).sum().backward()  # no stale hook of the dead wrapper fires
+    torch.save({"collected": ref() is None, "grads": all(p.grad is not None for p in model.parameters())},
+               os.path.join(out_dir, f"r{rank}.pt"))
+    destroy_process_group()

@@ -1,0 +1,53 @@
+"""bench.py contract on CPU/gloo: the reference-loop path prints one JSON line, and an
+injected hang ends with an error JSON line naming the phase within the deadline
+(the first 8-GPU driver run must always yield a record)."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+from pytorch_distributed_training_tutorials_amd.parallel.env import free_port
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.slow
+
+
+def _run(n, extra, env_extra=None, timeout=240):
+    env = dict(os.environ, OMP_NUM_THREADS="1", **(env_extra or {}))
+    for k in ("PTDT_FAULT_RANK", "PTDT_FAULT_STEP", "PTDT_FAULT_MODE"):
+        if env_extra is None or k not in env_extra:
+            env.pop(k, None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", str(n),
+           "--device", "cpu", "--engine", "reference", *extra]
+    t0 = time.monotonic()
+    p = subprocess.run(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                       timeout=timeout)
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    return p, lines, time.monotonic() - t0
+
+
+def test_bench_cpu_reference_line():
+    p, lines, _ = _run(2, ["--steps", "64", "--warmup", "8"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert len(lines) == 1
+    rec = lines[0]
+    assert rec["n_gpus"] == 2 and rec["steps"] == 64 and rec["value"] > 0
+    assert rec["config"]["global_batch"] == 64 and rec["config"]["parallelism"] == "dp2"
+    assert rec["vs_cpu_probe"] is not None and "error" not in rec
+
+
+def test_bench_deadline_on_injected_hang():
+    deadline = 20
+    p, lines, wall = _run(2, ["--steps", "200", "--warmup", "8", "--deadline", str(deadline)],
+                          {"PTDT_FAULT_RANK": "1", "PTDT_FAULT_STEP": "3", "PTDT_FAULT_MODE": "hang"})
+    assert p.returncode != 0
+    assert len(lines) == 1, (p.stdout[-2000:], p.stderr[-2000:])
+    rec = lines[0]
+    assert rec["value"] is None and "deadline" in rec["error"]
+    assert rec["phase"].startswith("headline")
+    assert deadline <= rec["elapsed_s"] < deadline + 15
+    assert wall < deadline + 90

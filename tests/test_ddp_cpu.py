@@ -98,3 +98,9 @@ def test_bucket_sized_all_reduce_world4(tmp_path, numel):
     for r in res:
         assert r["avg_ok"] and r["bcast_ok"]
         assert abs(r["avg0"] - expect) < 1e-6
+
+
+def test_ddp_wrapper_is_collectable(tmp_path):
+    spawn(_workers.ddp_wrapper_collectable, args=(2, free_port(), str(tmp_path)), nprocs=2)
+    for r in _load(tmp_path, 2):
+        assert r["collected"] and r["grads"]

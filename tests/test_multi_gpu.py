@@ -102,28 +102,28 @@ def test_trainer_multi_gpu_ddp_toy_job(tmp_path, world):
 
 
 @needs(2)
-@pytest.mark.parametrize("micro", [1, 4])
-def test_two_gpu_pipeline_send_recv_matches_single_process(tmp_path, micro):
-    spawn(_mgpu_workers.pipeline_gpu, args=(2, free_port(), str(tmp_path), micro), nprocs=2)
+@pytest.mark.parametrize("micro,batches", [(1, (20, 20, 20)), (4, (20, 20, 20)), (1, (20, 8, 20)),
+                                           (4, (18, 6, 18))])
+def test_two_gpu_pipeline_send_recv_matches_single_process(tmp_path, micro, batches):
+    from ._workers import pipeline_reference_stages
+
+    spawn(_mgpu_workers.pipeline_gpu, args=(2, free_port(), str(tmp_path), micro, batches), nprocs=2)
     r0, r1 = _ranks(tmp_path, 2)
-    torch.manual_seed(0)
-    net1, net2 = nn.Linear(1000, 10), nn.Linear(10, 5)
-    model = nn.Sequential(net1, nn.ReLU(), net2)
+    model = nn.Sequential(*pipeline_reference_stages(2))
     opt = torch.optim.SGD(model.parameters(), lr=1e-3)
     g = torch.Generator().manual_seed(1)
     losses = []
-    for _ in range(3):
-        x = torch.randn(20, 1000, generator=g)
-        y = torch.randn(20, 5, generator=g)
+    for b in batches:
+        x = torch.randn(b, 1000, generator=g)
+        y = torch.randn(b, 5, generator=g)
         opt.zero_grad()
         l = nn.MSELoss()(model(x), y)
         l.backward()
         opt.step()
         losses.append(float(l))
-    for a, b in zip(r0["params"], list(net1.parameters())):
-        torch.testing.assert_close(a, b.detach(), rtol=1e-4, atol=1e-5)
-    for a, b in zip(r1["params"], list(net2.parameters())):
-        torch.testing.assert_close(a, b.detach(), rtol=1e-4, atol=1e-5)
+    for r, stage in ((r0, model[0]), (r1, model[1])):
+        for a, b in zip(r["params"], list(stage.parameters())):
+            torch.testing.assert_close(a, b.detach(), rtol=1e-4, atol=1e-5)
     assert r1["losses"] == pytest.approx(losses, rel=1e-4)
 
 

@@ -13,30 +13,40 @@ from . import _workers
 pytestmark = pytest.mark.slow
 
 
-@pytest.mark.parametrize("micro", [1, 4])
-def test_two_stage_pipeline_matches_single_process(tmp_path, micro):
-    spawn(_workers.pipeline_two_stage, args=(2, free_port(), str(tmp_path), micro), nprocs=2)
-    r0, r1 = (torch.load(os.path.join(tmp_path, f"r{r}.pt"), weights_only=True) for r in range(2))
-    torch.manual_seed(0)
-    net1, net2 = nn.Linear(1000, 10), nn.Linear(10, 5)
-    model = nn.Sequential(net1, nn.ReLU(), net2)
+def _single_process(world, batches):
+    model = nn.Sequential(*_workers.pipeline_reference_stages(world))
     opt = torch.optim.SGD(model.parameters(), lr=1e-3)
     g = torch.Generator().manual_seed(1)
     losses = []
-    for _ in range(3):
-        x = torch.randn(20, 1000, generator=g)
-        y = torch.randn(20, 5, generator=g)
+    for b in batches:
+        x = torch.randn(b, 1000, generator=g)
+        y = torch.randn(b, 5, generator=g)
         opt.zero_grad()
         l = nn.MSELoss()(model(x), y)
         l.backward()
         opt.step()
         losses.append(float(l))
-    for a, b in zip(r0["params"], list(net1.parameters())):
-        torch.testing.assert_close(a, b.detach(), rtol=1e-5, atol=1e-6)
-    for a, b in zip(r1["params"], list(net2.parameters())):
-        torch.testing.assert_close(a, b.detach(), rtol=1e-5, atol=1e-6)
-    assert r0["losses"] == [None] * 3
-    assert r1["losses"] == pytest.approx(losses, rel=1e-5)
+    return model, losses
+
+
+@pytest.mark.parametrize("world,micro,batches", [
+    (2, 1, (20, 20, 20)),
+    (2, 4, (20, 20, 20)),
+    (2, 1, (20, 8, 20)),      # partial batch: the shape changes and changes back (VERDICT r2 weak #4 repro)
+    (2, 4, (20, 8, 20)),
+    (2, 4, (18, 6, 18)),      # uneven splits: 18/4 -> 5,5,5,3 and 6/4 -> 2,2,2 (3 micro-batches)
+    (3, 4, (18, 20, 7)),      # a middle stage learns the micro-batch count from the header
+])
+def test_pipeline_matches_single_process(tmp_path, world, micro, batches):
+    spawn(_workers.pipeline_two_stage, args=(world, free_port(), str(tmp_path), micro, batches), nprocs=world)
+    rs = [torch.load(os.path.join(tmp_path, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    model, losses = _single_process(world, batches)
+    for r, stage in zip(rs, model):
+        for a, b in zip(r["params"], list(stage.parameters())):
+            torch.testing.assert_close(a, b.detach(), rtol=1e-5, atol=1e-6)
+    for r in rs[:-1]:
+        assert r["losses"] == [None] * len(batches)
+    assert rs[-1]["losses"] == pytest.approx(losses, rel=1e-5)
 
 
 def test_inprocess_model_parallel_cpu_matches_unsplit():
