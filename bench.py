@@ -568,12 +568,12 @@ def main(argv=None):
 
     def expire(phase, elapsed):
         why = f"deadline of {args.deadline:.0f} s expired"
-        if rank_env == 0:
-            print(_error_line(args, world_env, phase, elapsed, why), flush=True)
+        if rank_env == 0:  # own line even if another process left a partial one on the shared stdout
+            print("\n" + _error_line(args, world_env, phase, elapsed, why), flush=True)
         print(f"[bench] rank {rank_env}: {why} in phase {phase!r}; aborting communicators and exiting",
               file=sys.stderr, flush=True)
 
-    dl = Deadline(args.deadline, expire)
+    dl = Deadline(args.deadline, expire, exit_delay_s=0.0 if rank_env == 0 else 5.0)
     dl.set_phase("process group init")
     rank, world, local = _setup(args, cpu)
     dev = torch.device("cpu") if cpu else torch.device("cuda", 0 if args.share_gpu else local)
@@ -606,7 +606,7 @@ def main(argv=None):
         rec["device"] = "cpu (gloo): plumbing run of the reference loop, not an MI355X number"
     if rank == 0:
         line = json.dumps(rec)
-        print(line, flush=True)
+        print("\n" + line, flush=True)  # starts a line even after another rank's partial output
         if args.out:
             with open(args.out, "a") as f:
                 f.write(line + "\n")

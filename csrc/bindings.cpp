@@ -37,6 +37,20 @@ int dt_of(const Tensor& t) {
   return -1;
 }
 
+// the LLM.int8 pieces also take IEEE half (the reference's load_in_8bit Llama runs in fp16)
+int dt_of16(const Tensor& t) {
+  if (t.scalar_type() == at::kHalf) return kF16;
+  return dt_of(t);
+}
+
+at::ScalarType scalar_of(const std::string& name) {
+  if (name == "float32") return at::kFloat;
+  if (name == "bfloat16") return at::kBFloat16;
+  if (name == "float16") return at::kHalf;
+  TORCH_CHECK(false, "int8_mm: out dtype must be float32, bfloat16 or float16, got ", name);
+  return at::kFloat;
+}
+
 void check_gpu(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
@@ -747,7 +761,7 @@ Tensor int8_col_outliers_(Tensor x, double threshold) {
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "int8_col_outliers: contiguous [M, K]");
   c10::hip::HIPGuard guard(x.device().index());
   Tensor mask = at::empty({x.size(1)}, x.options().dtype(at::kByte));
-  hip_check(int8_col_outliers(x.data_ptr(), dt_of(x), (int)x.size(0), (int)x.size(1), (float)threshold,
+  hip_check(int8_col_outliers(x.data_ptr(), dt_of16(x), (int)x.size(0), (int)x.size(1), (float)threshold,
                               mask.data_ptr<uint8_t>(), cur_stream(x)),
             "int8_col_outliers");
   return mask;
@@ -764,14 +778,14 @@ std::vector<Tensor> int8_quant_rows_(Tensor x, c10::optional<Tensor> mask) {
   c10::hip::HIPGuard guard(x.device().index());
   Tensor q = at::empty(x.sizes(), x.options().dtype(at::kChar));
   Tensor s = at::empty({x.size(0)}, x.options().dtype(at::kFloat));
-  hip_check(int8_quant_rows(x.data_ptr(), dt_of(x), (int)x.size(0), (int)x.size(1), mp, q.data_ptr<int8_t>(),
+  hip_check(int8_quant_rows(x.data_ptr(), dt_of16(x), (int)x.size(0), (int)x.size(1), mp, q.data_ptr<int8_t>(),
                             s.data_ptr<float>(), cur_stream(x)),
             "int8_quant_rows");
   return {q, s};
 }
 
 Tensor int8_mm_(Tensor A, Tensor sa, Tensor B, Tensor sb, c10::optional<Tensor> addend, c10::optional<Tensor> bias,
-                bool out_bf16) {
+                const std::string& out_dtype) {
   check_gpu(A, "A");
   check_gpu(B, "B");
   TORCH_CHECK(A.scalar_type() == at::kChar && B.scalar_type() == at::kChar && A.dim() == 2 && B.dim() == 2 &&
@@ -788,16 +802,16 @@ Tensor int8_mm_(Tensor A, Tensor sa, Tensor B, Tensor sb, c10::optional<Tensor> 
     ad = addend->data_ptr<float>();
   }
   const void* bp = nullptr;
-  int bias_bf16 = 0;
+  int bias_dt = kF32;
   if (bias.has_value() && bias->defined()) {
-    TORCH_CHECK(bias->numel() == N && (bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kBFloat16));
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "int8_mm: bias [N]");
     bp = bias->data_ptr();
-    bias_bf16 = bias->scalar_type() == at::kBFloat16;
+    bias_dt = dt_of16(*bias);
   }
   c10::hip::HIPGuard guard(A.device().index());
-  Tensor y = at::empty({M, N}, A.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  Tensor y = at::empty({M, N}, A.options().dtype(scalar_of(out_dtype)));
   hip_check(int8_mm(A.data_ptr<int8_t>(), sa.data_ptr<float>(), B.data_ptr<int8_t>(), sb.data_ptr<float>(), ad, bp,
-                    bias_bf16, (int)M, (int)N, (int)K, y.data_ptr(), dt_of(y), cur_stream(A)),
+                    bias_dt, (int)M, (int)N, (int)K, y.data_ptr(), dt_of16(y), cur_stream(A)),
             "int8_mm");
   return y;
 }
@@ -1144,7 +1158,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("int8_col_outliers", &int8_col_outliers_, py::arg("x"), py::arg("threshold"));
   m.def("int8_quant_rows", &int8_quant_rows_, py::arg("x"), py::arg("mask") = py::none());
   m.def("int8_mm", &int8_mm_, py::arg("A"), py::arg("sa"), py::arg("B"), py::arg("sb"), py::arg("addend") = py::none(),
-        py::arg("bias") = py::none(), py::arg("out_bf16") = false);
+        py::arg("bias") = py::none(), py::arg("out_dtype") = "float32");
   m.def("bn_relu", &bn_relu);
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("num_batches_tracked"), py::arg("residual"), py::arg("relu"),

@@ -55,6 +55,11 @@ template <> struct Cvt<uint16_t> {
   __device__ __forceinline__ static float load(const uint16_t* p, int64_t i) { return bf16_to_f32(p[i]); }
   __device__ __forceinline__ static void store(uint16_t* p, int64_t i, float v) { p[i] = f32_to_bf16(v); }
 };
+// IEEE half (kF16): the LLM.int8 path's activations (the reference's load_in_8bit Llama runs in fp16)
+template <> struct Cvt<_Float16> {
+  __device__ __forceinline__ static float load(const _Float16* p, int64_t i) { return (float)p[i]; }
+  __device__ __forceinline__ static void store(_Float16* p, int64_t i, float v) { p[i] = (_Float16)v; }
+};
 
 // ----------------------------------------------------------- wave64 reductions
 // DPP / permlane based: every step is one VALU instruction (v_add_f32_dpp,

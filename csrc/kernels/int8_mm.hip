@@ -9,11 +9,18 @@
 // and multiplied in 16/32-bit instead (the caller gathers them: usually a handful).
 //   int8_col_outliers : column absmax > threshold -> mask[K]
 //   int8_quant_rows   : per-row absmax over the non-outlier columns, q = rint(x / s)
-//   int8_mm           : int32 products on v_mfma_i32_16x16x64_i8 (2x the bf16 rate, exact),
-//                       dequantised in the fp32 epilogue with the addend (outlier part) and bias
-// The MFMA's A and B fragments are read straight from global memory (16 contiguous
-// bytes of a row per lane, the same k set for A and B in every lane group), so the
-// kernel needs K % 16 == 0 and 16-byte aligned rows.
+//   int8_mm           : int32 products on v_mfma_i32_16x16x64_i8 (exact), dequantised in
+//                       the fp32 epilogue with the addend (outlier part) and bias
+// Activations / outputs / bias: fp32, bf16 or fp16 (the reference's Llama runs in fp16).
+//
+// int8_mm, tiled path (K % 128 == 0): 128x128 output tile per workgroup of 4 waves (2x2,
+// 64x64 each = 4x4 MFMA tiles), K in 128-byte tiles staged global -> LDS with
+// global_load_lds_dwordx4 (16 B per lane, no VGPR round trip), double-buffered: tile k+1's
+// DMA is in flight (counted vmcnt) while tile k is multiplied. A tile is rows x 8 chunks
+// of 16 B; chunk c of row r lives in slot c ^ ((r >> 1) & 7), so the 16 rows read by one
+// ds_read_b128 hit 16 distinct slots (conflict-free) -- the layout of gemm_big.hip's bf16
+// tiles, whose 64-element K-tile is the same 128 bytes. Workgroup ids are XCD-remapped.
+// Direct path (other K % 16 == 0): fragments straight from global memory, 64x64 tiles.
 #include "common.h"
 #include "kernels.h"
 
@@ -54,12 +61,57 @@ __global__ void __launch_bounds__(kThreads) row_quant_kernel(const T* __restrict
   if (threadIdx.x == 0) scale[r] = sc;
 }
 
+__device__ __forceinline__ float load_any(const void* p, int dtype, int64_t i) {
+  if (dtype == kF32) return static_cast<const float*>(p)[i];
+  if (dtype == kF16) return (float)static_cast<const _Float16*>(p)[i];
+  return bf16_to_f32(static_cast<const uint16_t*>(p)[i]);
+}
+__device__ __forceinline__ void store_any(void* p, int dtype, int64_t i, float v) {
+  if (dtype == kF32) static_cast<float*>(p)[i] = v;
+  else if (dtype == kF16) static_cast<_Float16*>(p)[i] = (_Float16)v;
+  else static_cast<uint16_t*>(p)[i] = f32_to_bf16(v);
+}
+
+struct I8Epi {
+  const float* sa;
+  const float* sb;
+  const float* addend;
+  const void* bias;
+  int bias_dtype;
+  void* y;
+  int y_dtype;
+  int M, N;
+};
+
+// acc[i][j][r] = C[m0 + 16 i + 4 g + r][n0 + 16 j + c] of this wave's FI x FJ 16x16 tiles
+template <int FI, int FJ>
+__device__ __forceinline__ void i8_epilogue(const I8Epi& e, const i32x4 (&acc)[FI][FJ], int m0, int n0, int c,
+                                            int g) {
+#pragma unroll
+  for (int j = 0; j < FJ; ++j) {
+    const int n = n0 + 16 * j + c;
+    if (n >= e.N) continue;
+    const float sbn = e.sb[n];
+    const float bn = e.bias ? load_any(e.bias, e.bias_dtype, n) : 0.f;
+#pragma unroll
+    for (int i = 0; i < FI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + 16 * i + 4 * g + r;
+        if (m >= e.M) continue;
+        const int64_t off = (int64_t)m * e.N + n;
+        float v = (float)acc[i][j][r] * e.sa[m] * sbn;
+        if (e.addend) v += e.addend[off];
+        v += bn;
+        store_any(e.y, e.y_dtype, off, v);
+      }
+  }
+}
+
+// ------------------------------------------------------------------ direct path
 // 64x64 output tile per workgroup, 4 waves of 32x32 (2x2 MFMA tiles of 16x16), K in steps of 64
-__global__ void __launch_bounds__(kThreads) i8_mm_kernel(const int8_t* __restrict__ A, const float* __restrict__ sa,
-                                                         const int8_t* __restrict__ B, const float* __restrict__ sb,
-                                                         const float* __restrict__ addend, const void* bias,
-                                                         int bias_bf16, int M, int N, int K, void* y, int y_bf16,
-                                                         int tm, int tn) {
+__global__ void __launch_bounds__(kThreads) i8_mm_kernel(const int8_t* __restrict__ A, const int8_t* __restrict__ B,
+                                                         int K, I8Epi e, int tm, int tn) {
   const int tile = xcd_remap(blockIdx.x, tm * tn);
   const int m0 = (tile / tn) * 64, n0 = (tile % tn) * 64;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -75,9 +127,9 @@ __global__ void __launch_bounds__(kThreads) i8_mm_kernel(const int8_t* __restric
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     ra[i] = m0 + wr * 32 + 16 * i + c;
-    va[i] = ra[i] < M;
+    va[i] = ra[i] < e.M;
     rb[i] = n0 + wc * 32 + 16 * i + c;
-    vb[i] = rb[i] < N;
+    vb[i] = rb[i] < e.N;
   }
   for (int k0 = 0; k0 < K; k0 += 64) {
     const int k = k0 + 16 * g;  // this lane group's 16 consecutive k (same set for A and B)
@@ -93,58 +145,140 @@ __global__ void __launch_bounds__(kThreads) i8_mm_kernel(const int8_t* __restric
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[i], b[j], acc[i][j], 0, 0, 0);
   }
-  // D layout: [m = 4 g + r][n = c] of each 16x16 tile
+  i8_epilogue<2, 2>(e, acc, m0 + wr * 32, n0 + wc * 32, c, g);
+}
+
+// ------------------------------------------------------------------ tiled path
+constexpr int TM = 128, TN = 128, BKB = 128;         // output tile, K bytes per K-tile
+constexpr int TILE_BYTES = TM * BKB;                  // one operand tile (16 KiB)
+constexpr int BUF = 2 * TILE_BYTES;                   // A + B
+constexpr int LDS_BYTES = 2 * BUF;                    // double buffered: 64 KiB (2 workgroups per CU)
+constexpr int DMA_PER_OPERAND = TILE_BYTES / (kThreads * 16);  // 4
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gbl_void;
+
+// LDS-DMA of one 128-row x 128-byte operand tile (rows row0.., bytes k0..k0+127)
+__device__ __forceinline__ void stage_i8(const int8_t* __restrict__ src, int K, int row0, int nrows, int k0,
+                                         uint8_t* lds_tile, int wid, int lane) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < DMA_PER_OPERAND; ++i) {
+    const int p = i * kThreads + wid * 64 + lane;  // linear 16-B chunk of the tile image
+    const int r = p >> 3, slot = p & 7;
+    const int ch = slot ^ ((r >> 1) & 7);       // logical 16-B k-chunk stored in this slot
+    const int gr = min(row0 + r, nrows - 1);    // clamp: edge rows are computed, never stored
+    const int8_t* gsrc = src + (int64_t)gr * K + k0 + ch * 16;
+    uint8_t* dst = lds_tile + (i * kThreads + wid * 64) * 16;  // wave-uniform base; hardware adds lane * 16
+    __builtin_amdgcn_global_load_lds((gbl_void*)gsrc, (lds_void*)dst, 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ i32x4 frag(const uint8_t* lds_tile, int row, int ch) {
+  const int slot = ch ^ ((row >> 1) & 7);
+  return *reinterpret_cast<const i32x4*>(lds_tile + row * BKB + slot * 16);
+}
+
+__global__ void __launch_bounds__(kThreads) i8_mm_tiled_kernel(const int8_t* __restrict__ A,
+                                                               const int8_t* __restrict__ B, int K, I8Epi e, int tm,
+                                                               int tn) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int FI = 4, FJ = 4;  // 64x64 per wave
+  const int tile = xcd_remap(blockIdx.x, tm * tn);
+  const int m0 = (tile / tn) * TM, n0 = (tile % tn) * TN;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int c = lane & 15, g = lane >> 4;
+  const int nk = K / BKB;
+  i32x4 acc[FI][FJ];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wr * 32 + 16 * i + 4 * g + r;
-        const int n = n0 + wc * 32 + 16 * j + c;
-        if (m < M && n < N) {
-          float v = (float)acc[i][j][r] * sa[m] * sb[n];
-          if (addend) v += addend[(int64_t)m * N + n];
-          if (bias) v += bias_bf16 ? bf16_to_f32(static_cast<const uint16_t*>(bias)[n]) : static_cast<const float*>(bias)[n];
-          if (y_bf16)
-            static_cast<uint16_t*>(y)[(int64_t)m * N + n] = f32_to_bf16(v);
-          else
-            static_cast<float*>(y)[(int64_t)m * N + n] = v;
-        }
-      }
+    for (int j = 0; j < FJ; ++j) acc[i][j] = i32x4{0, 0, 0, 0};
+
+  auto stage = [&](int kt, uint8_t* buf) {
+    stage_i8(A, K, m0, e.M, kt * BKB, buf, wid, lane);
+    stage_i8(B, K, n0, e.N, kt * BKB, buf + TILE_BYTES, wid, lane);
+  };
+  stage(0, smem);
+  for (int kt = 0; kt < nk; ++kt) {
+    const uint8_t* cur = smem + (kt & 1) * BUF;
+    if (kt + 1 < nk) {
+      stage(kt + 1, smem + ((kt + 1) & 1) * BUF);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile kt landed (2 x 4 DMAs), kt+1 in flight
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt is visible
+    __builtin_amdgcn_sched_barrier(0);
+    i32x4 a[2][FI], b[2][FJ];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {  // two 64-byte halves of the K-tile
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) b[kb][j] = frag(cur + TILE_BYTES, wc * 64 + 16 * j + c, kb * 4 + g);
+#pragma unroll
+      for (int i = 0; i < FI; ++i) a[kb][i] = frag(cur, wr * 64 + 16 * i + c, kb * 4 + g);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < FI; ++i)
+#pragma unroll
+        for (int j = 0; j < FJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[kb][i], b[kb][j], acc[i][j], 0, 0, 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();  // buffer kt & 1 free for tile kt + 2
+  }
+  i8_epilogue<FI, FJ>(e, acc, m0 + wr * 64, n0 + wc * 64, c, g);
+}
+
+template <typename T>
+hipError_t outliers_t(const void* x, int M, int K, float threshold, uint8_t* mask, hipStream_t s) {
+  const dim3 grid((K + kThreads - 1) / kThreads);
+  hipLaunchKernelGGL(col_outlier_kernel<T>, grid, dim3(kThreads), 0, s, static_cast<const T*>(x), M, K, threshold,
+                     mask);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t quant_t(const void* x, int M, int K, const uint8_t* mask, int8_t* q, float* scale, hipStream_t s) {
+  hipLaunchKernelGGL(row_quant_kernel<T>, dim3(M), dim3(kThreads), 0, s, static_cast<const T*>(x), K, mask, q, scale);
+  return hipGetLastError();
 }
 
 }  // namespace
 
 hipError_t int8_col_outliers(const void* x, int dtype, int M, int K, float threshold, uint8_t* mask, hipStream_t s) {
   if (K <= 0) return hipSuccess;
-  const dim3 grid((K + kThreads - 1) / kThreads);
-  if (dtype == kF32)
-    hipLaunchKernelGGL(col_outlier_kernel<float>, grid, dim3(kThreads), 0, s, (const float*)x, M, K, threshold, mask);
-  else
-    hipLaunchKernelGGL(col_outlier_kernel<uint16_t>, grid, dim3(kThreads), 0, s, (const uint16_t*)x, M, K, threshold,
-                       mask);
-  return hipGetLastError();
+  if (dtype == kF32) return outliers_t<float>(x, M, K, threshold, mask, s);
+  if (dtype == kF16) return outliers_t<_Float16>(x, M, K, threshold, mask, s);
+  return outliers_t<uint16_t>(x, M, K, threshold, mask, s);
 }
 
 hipError_t int8_quant_rows(const void* x, int dtype, int M, int K, const uint8_t* mask, int8_t* q, float* scale,
                            hipStream_t s) {
   if (M <= 0 || K <= 0) return hipSuccess;
-  if (dtype == kF32)
-    hipLaunchKernelGGL(row_quant_kernel<float>, dim3(M), dim3(kThreads), 0, s, (const float*)x, K, mask, q, scale);
-  else
-    hipLaunchKernelGGL(row_quant_kernel<uint16_t>, dim3(M), dim3(kThreads), 0, s, (const uint16_t*)x, K, mask, q,
-                       scale);
-  return hipGetLastError();
+  if (dtype == kF32) return quant_t<float>(x, M, K, mask, q, scale, s);
+  if (dtype == kF16) return quant_t<_Float16>(x, M, K, mask, q, scale, s);
+  return quant_t<uint16_t>(x, M, K, mask, q, scale, s);
 }
 
+bool int8_mm_tiled_supported(int M, int N, int K) { return M > 0 && N > 0 && K >= BKB && K % BKB == 0; }
+
 hipError_t int8_mm(const int8_t* A, const float* sa, const int8_t* B, const float* sb, const float* addend,
-                   const void* bias, int bias_bf16, int M, int N, int K, void* y, int y_dtype, hipStream_t s) {
+                   const void* bias, int bias_dtype, int M, int N, int K, void* y, int y_dtype, hipStream_t s) {
   if (M <= 0 || N <= 0) return hipSuccess;
   if (K % 16 != 0) return hipErrorInvalidValue;
+  const I8Epi e{sa, sb, addend, bias, bias_dtype, y, y_dtype, M, N};
+  const bool aligned = (reinterpret_cast<uintptr_t>(A) & 15) == 0 && (reinterpret_cast<uintptr_t>(B) & 15) == 0;
+  if (aligned && int8_mm_tiled_supported(M, N, K)) {
+    const int tm = (M + TM - 1) / TM, tn = (N + TN - 1) / TN;
+    hipLaunchKernelGGL(i8_mm_tiled_kernel, dim3(tm * tn), dim3(kThreads), LDS_BYTES, s, A, B, K, e, tm, tn);
+    return hipGetLastError();
+  }
   const int tm = (M + 63) / 64, tn = (N + 63) / 64;
-  hipLaunchKernelGGL(i8_mm_kernel, dim3(tm * tn), dim3(kThreads), 0, s, A, sa, B, sb, addend, bias, bias_bf16, M, N, K,
-                     y, y_dtype == kBF16 ? 1 : 0, tm, tn);
+  hipLaunchKernelGGL(i8_mm_kernel, dim3(tm * tn), dim3(kThreads), 0, s, A, B, K, e, tm, tn);
   return hipGetLastError();
 }
 

@@ -13,7 +13,9 @@
 
 namespace ptdt {
 
-enum DType : int { kF32 = 0, kBF16 = 1 };
+// kF16 is accepted only where a launcher says so (the LLM.int8 pieces); elsewhere
+// "not kF32" means bf16.
+enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
 
 // --------------------------------------------------------------------------
 // Fused small-MLP train step (csrc/kernels/fused_mlp.hip).
@@ -292,8 +294,11 @@ hipError_t int8_weight_gemm(const void* x, int x_dtype, const int8_t* q, const f
 hipError_t int8_col_outliers(const void* x, int dtype, int M, int K, float threshold, uint8_t* mask, hipStream_t s);
 hipError_t int8_quant_rows(const void* x, int dtype, int M, int K, const uint8_t* mask, int8_t* q, float* scale,
                            hipStream_t s);
+// x / y / bias dtypes: kF32, kBF16 or kF16. K % 128 == 0 and 16-B aligned operands take the
+// LDS-staged 128x128-tile kernel (int8_mm_tiled_supported), other K % 16 == 0 the direct one.
 hipError_t int8_mm(const int8_t* A, const float* sa, const int8_t* B, const float* sb, const float* addend,
-                   const void* bias, int bias_bf16, int M, int N, int K, void* y, int y_dtype, hipStream_t s);
+                   const void* bias, int bias_dtype, int M, int N, int K, void* y, int y_dtype, hipStream_t s);
+bool int8_mm_tiled_supported(int M, int N, int K);
 
 // BatchNorm(train stats applied) + ReLU fused epilogue over NCHW (csrc/kernels/elementwise.hip)
 hipError_t bn_relu_apply(const void* x, int dtype, const float* scale, const float* shift, int64_t N,

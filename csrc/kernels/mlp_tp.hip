@@ -30,8 +30,10 @@
 // position are produced S+1 steps ahead of their use, C = min(8, S) positions at a
 // time by all threads, so epoch transitions cost nothing. With an all-reduce (world > 1) every lane
 // exchanges its gradient registers over xGMI with the LL protocol of
-// comm/xgmi.h (push to every peer, poll, sum in rank order: bit-identical
-// replicas), then applies SGD.
+// comm/xgmi.h in a lane-major slot layout (tp_allreduce_lm: push to every peer,
+// poll, sum in rank order: bit-identical replicas), then applies SGD.
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 #include "sampler.h"
@@ -39,7 +41,7 @@
 namespace ptdt {
 namespace {
 
-constexpr int kTpThreadsMax = 256;
+constexpr int kTpThreadsMax = 320;  // up to 4 compute waves + the helper wave
 using f4 = __attribute__((ext_vector_type(4))) float;
 
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
@@ -102,61 +104,73 @@ __device__ __forceinline__ float sgd1(float& w, float& m, float g, bool first, f
   return w;
 }
 
-// Gradient all-reduce of NV register values over xGMI (LL words, comm/xgmi.h):
-// push[k] lanes send value k (flat index idx[k]) to every peer, then every lane
-// with need[k] polls the W contributions and sums them in rank order (its own
-// from the register). Returns false after a poll timeout (and sets *err).
+// Lane-major gradient all-reduce (replaces tp_allreduce on the step's critical path).
+// Every rank runs the same lane -> parameter mapping, so the exchange need not use the
+// flat parameter index: value k of wave w, lane l travels in LL slot (w NV + k) 64 + l.
+// One push instruction then writes 64 consecutive words (512 contiguous bytes, 4 cache
+// lines) instead of 64 words strided by Din (64 separate uncached transactions), and one
+// poll instruction reads them back the same way -- round 2's flat-index pushes were
+// 3.3K scattered uncached writes per step (share-GPU W=2: 6.4 us/step vs 2.8 at W=1).
+// Polls of 2 peers are in flight together; the loop is uniform (ballot exit,
+// every lane re-polls its whole set), contributions are summed in rank order (own value
+// from the register): bit-identical replicas. Padded values (zero gradients) travel too.
 template <int NV>
-__device__ __forceinline__ bool tp_allreduce(const XgmiArgs& x, uint32_t seq, float (&v)[NV], const int (&idx)[NV],
-                                             const bool (&push)[NV], const bool (&need)[NV]) {
+__device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq, float (&v)[NV], int wave, int lane) {
   const int parity = (int)(seq & 1u);
   const uint64_t hi = (uint64_t)seq << 32;
   const bool drop = x.drop_push != 0u && seq >= x.drop_push;
+  const int base = wave * NV * 64 + lane;
+  for (int p = 0; p < x.world; ++p) {
+    if (p == x.rank || drop) continue;
+    uint64_t PTDT_GLOBAL* const dst =
+        (uint64_t PTDT_GLOBAL*)x.peers[p] + (int64_t)(parity * x.world + x.rank) * x.max_elems + base;
 #pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    if (!push[k] || drop) continue;
-    const uint64_t w = hi | (uint64_t)__float_as_uint(v[k]);
-    for (int p = 0; p < x.world; ++p)
-      if (p != x.rank)
-        __hip_atomic_store(xgmi_slot(x.peers[p], parity, x.rank, x.world, x.max_elems, idx[k]), w, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int k = 0; k < NV; ++k)
+      __hip_atomic_store(dst + k * 64, hi | (uint64_t)__float_as_uint(v[k]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  bool ok = true;
   float acc[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) acc[k] = 0.f;
-  for (int p = 0; p < x.world; ++p) {
-    if (p == x.rank) {
+  bool ok = true;
+  constexpr int G = 2;  // peers polled together (VGPR budget: 2 waves share SIMD 0 with the helper)
+  for (int p0 = 0; p0 < x.world; p0 += G) {
+    uint64_t w[G][NV];
+    auto issue = [&]() {
 #pragma unroll
-      for (int k = 0; k < NV; ++k) acc[k] += v[k];
-      continue;
-    }
-    uint64_t w[NV];
+      for (int g = 0; g < G; ++g) {
+        const int p = p0 + g;
+        const bool real = p < x.world && p != x.rank;  // uniform
+        const uint64_t PTDT_GLOBAL* src =
+            (const uint64_t PTDT_GLOBAL*)x.local + (int64_t)(parity * x.world + (real ? p : 0)) * x.max_elems + base;
 #pragma unroll
-    for (int k = 0; k < NV; ++k)  // all polls of this peer in flight together
-      w[k] = need[k] ? __hip_atomic_load(xgmi_slot(x.local, parity, p, x.world, x.max_elems, idx[k]), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_SYSTEM)
-                     : hi;
+        for (int k = 0; k < NV; ++k)
+          w[g][k] = real ? __hip_atomic_load(src + k * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : hi;
+      }
+    };
+    issue();
     for (uint32_t polls = 0;; ++polls) {
-      bool all = true;
+      bool m = false;
 #pragma unroll
-      for (int k = 0; k < NV; ++k) all &= (uint32_t)(w[k] >> 32) == seq;
-      if (all) break;
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int k = 0; k < NV; ++k) m |= (uint32_t)(w[g][k] >> 32) != seq;
+      if (__builtin_amdgcn_ballot_w64(m) == 0) break;
       if (polls >= x.max_polls) {
         __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         ok = false;
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-      for (int k = 0; k < NV; ++k)
-        if ((uint32_t)(w[k] >> 32) != seq)
-          w[k] = __hip_atomic_load(xgmi_slot(x.local, parity, p, x.world, x.max_elems, idx[k]), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
+      issue();
     }
     if (!ok) break;
 #pragma unroll
-    for (int k = 0; k < NV; ++k) acc[k] += need[k] ? __uint_as_float((uint32_t)w[k]) : 0.f;
+    for (int g = 0; g < G; ++g) {
+      const int p = p0 + g;
+      if (p >= x.world) break;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) acc[k] += p == x.rank ? v[k] : __uint_as_float((uint32_t)w[g][k]);
+    }
   }
   const float inv = 1.f / (float)x.world;
 #pragma unroll
@@ -221,8 +235,8 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   // scaled loss share per step; every kTpLossFlush steps all waves add the shares of the
   // past kTpLossFlush slots in lane order
   float* const lring = lds + al4((int)(reinterpret_cast<float*>(fkeys) - lds) + 48);
-  auto flush_losses = [&](int lo, int hi) {  // steps [lo, hi), hi - lo <= kTpLossFlush
-    const int j = w + NW * l;
+  auto flush_losses = [&](int lo, int hi) {  // steps [lo, hi), hi - lo <= kTpLossFlush (helper wave)
+    const int j = l;
     if (j < hi - lo) {
       const int step = lo + j;
       const f4* sh = reinterpret_cast<const f4*>(lring + (step & (kTpLossRing - 1)) * 64);
@@ -308,27 +322,27 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   __syncthreads();
   if (tid == 0 && pa.idx == nullptr) list_cache_publish(lc, e0);
 
-  // Chunked producer: every C = min(8, S) steps ALL threads produce the entries of the
-  // C positions S+1 .. S+C ahead (one entry per thread for B <= 32), so the cycle-
-  // walking Feistel of the device sampler costs one evaluation per thread per C steps
-  // on every wave alike. Produced lists are not cached (the cache only holds lists
-  // computed whole by a prologue); three LDS slots keep any produced epoch clear of
-  // the epochs still read (positions P and P+1).
+  // Helper wave (w == NW): owns the sampler lists and the batch staging, so the NW compute
+  // waves run only the step's math. Per step k, between the barriers of steps k-1 and k, it
+  //   * produces list entries C = min(8, S) positions at a time, S+1 positions ahead of use
+  //     (cycle-walking Feistel of the device sampler; three LDS epoch slots keep any produced
+  //     epoch clear of the ones still read),
+  //   * reads position k+1's rows from the list, loads them (X rows, targets) and writes
+  //     them into stage slot (k+1) % 3 (rows and X^T) -- that slot was last read in step
+  //     k-2's backward (before barrier k-1) and is next read in step k+1 (after barrier k),
+  //   * adds the loss shares wave 0 left in the LDS ring for 16 past steps.
+  // It meets the compute waves at their one barrier per step: no extra synchronisation.
+  // Round 2 ran all of this on the compute waves (~900 of ~7500 cycles per step).
   const int C = min(8, S);
-  const int o0 = tid / B, r0 = tid - o0 * B;  // this thread's first chunk entry (position offset, row)
   auto produce = [&](int te, int tj) {  // positions (te, tj) .. + C - 1: they span epochs te, te + 1
     FeistelPerm fa, fb;
     if (feistel) {
       fa = keys_load(te);
       fb = keys_load(te + 1);
-      if (tid == 0 && fkeys[((te + 2) & 3) * 12 + 8] != te + 2) keys_store(te + 2);
+      if (l == 0 && fkeys[((te + 2) & 3) * 12 + 8] != te + 2) keys_store(te + 2);
     }
-    for (int idx = tid; idx < C * B; idx += T) {
-      int o = o0, r = r0;
-      if (idx != tid) {  // only when the chunk outnumbers the threads (small workgroups)
-        o = idx / B;
-        r = idx - o * B;
-      }
+    for (int idx = l; idx < C * B; idx += 64) {
+      const int o = idx / B, r = idx - o * B;
       int J = tj + o, E = te;
       if (J >= S) {
         J -= S;
@@ -348,39 +362,34 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     }
   };
 
-  // ---- batch staging: the next position's batch tile (32 rows of X, the targets) is
-  // loaded by ALL threads at the top of a step and written to the next LDS slot (rows,
-  // and X^T) before the step's barrier, so every wave's operands are LDS reads and the
-  // global latency hides under the step's MFMAs. Item e = tid + k T of the tile (float4
-  // chunks when VX, else single floats) for k below a count that is uniform across the
-  // workgroup; the last item is repeated past the end (identical writes) and rows past
-  // the batch read clamped rows: no divergent branches, no per-step divisions.
+  // ---- batch staging (helper lanes l = 0..63): item e = l + 64 k of the 32-row tile (float4
+  // chunks when VX, else single floats) for k below a count uniform over the wave; the last
+  // item is repeated past the end (identical writes), rows past the batch read clamped rows.
   constexpr int KX = VX ? 4 : 16, KY = 8;
   const auto X = gptr(a.X);
   const int ldx = a.ldx > 0 ? a.ldx : Din;
   const int xper = VX ? Din / 4 : Din;  // items per row
-  const int nkx = (32 * xper + T - 1) / T;
+  const int nkx = (32 * xper + 63) / 64;
   int xrow[KX], xcol[KX];
 #pragma unroll
   for (int k = 0; k < KX; ++k) {
-    const int e = min(tid + k * T, 32 * xper - 1);
+    const int e = min(l + k * 64, 32 * xper - 1);
     xrow[k] = e / xper;
     xcol[k] = e - xrow[k] * xper;
   }
   constexpr bool YI = LOSS == kLossCEIndex;
   const int yper = YI ? 1 : Dout;
-  const int nky = (32 * yper + T - 1) / T;
+  const int nky = (32 * yper + 63) / 64;
   int yrow[KY], ycol[KY];
 #pragma unroll
   for (int k = 0; k < KY; ++k) {
-    const int e = min(tid + k * T, 32 * yper - 1);
+    const int e = min(l + k * 64, 32 * yper - 1);
     yrow[k] = e / yper;
     ycol[k] = e - yrow[k] * yper;
   }
-  f4 xv[KX];
+  using XV = typename std::conditional<VX, f4, float>::type;  // a float4 chunk or one float
+  XV xv[KX];
   float yv[KY];
-  // the dataset rows of a position's items, read from the LDS list one step before
-  // their loads are issued (after a barrier: the producer's writes are visible)
   int xsel[KX], ysel[KY];
   auto stage_sel = [&](int E, int J) {
     const int nb = min(B, ns - J * B);
@@ -399,16 +408,15 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         if constexpr (VX) {
           xv[k] = *reinterpret_cast<const f4*>(a.X + (int64_t)xsel[k] * ldx + 4 * xcol[k]);
         } else {
-          xv[k][0] = X[(int64_t)xsel[k] * ldx + xcol[k]];
+          xv[k] = X[(int64_t)xsel[k] * ldx + xcol[k]];
         }
       }
     }
 #pragma unroll
     for (int k = 0; k < KY; ++k) {
       if (k < nky) {
-        // the low dword of the int64 label only: a dwordx2 load left its dead high half to
-        // the register allocator, which reused it in the forward behind a vmcnt(0) -- a
-        // stall on this step's batch loads every step
+        // the low dword of the int64 label only (a dwordx2 load's dead high half was reused
+        // as a temporary behind a vmcnt(0))
         if constexpr (YI) yv[k] = __int_as_float(reinterpret_cast<const int*>(a.Yi)[2 * (int64_t)ysel[k]]);
         else yv[k] = gptr(a.Yf)[(int64_t)ysel[k] * Dout + ycol[k]];
       }
@@ -425,8 +433,8 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 #pragma unroll
           for (int i = 0; i < 4; ++i) st[St::XT_OFF + (4 * xcol[k] + i) * LDXT + row] = xv[k][i];
         } else {
-          st[row * LDX + xcol[k]] = xv[k][0];
-          st[St::XT_OFF + xcol[k] * LDXT + row] = xv[k][0];
+          st[row * LDX + xcol[k]] = xv[k];
+          st[St::XT_OFF + xcol[k] * LDXT + row] = xv[k];
         }
       }
     }
@@ -434,7 +442,47 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     for (int k = 0; k < KY; ++k)
       if (k < nky) st[St::Y_OFF + (YI ? yrow[k] : yrow[k] * 16 + ycol[k])] = yv[k];
   };
+  // position of step 0 staged synchronously (helper), visible to all after the barrier
+  if (w == NW) {
+    stage_sel(e0, j0);
+    stage_issue();
+    stage_write(0);
+  }
+  __syncthreads();
 
+  const float inv_full = 1.f / (float)(LOSS == kLossMSE ? B * Dout : B);
+  const int ce0 = e0, cj0 = j0;
+  if (w == NW) {
+    // ================================================================ helper wave
+    int ce = ce0, cj = cj0, sc = 0, pc = 0;
+    for (int k = 0; k < n; ++k) {
+      const bool wrap = cj + 1 == S;
+      const int ne = wrap ? ce + 1 : ce, nj = wrap ? 0 : cj + 1;
+      const int sn = sc == 2 ? 0 : sc + 1;
+      if (pc == 0) {
+        produce(wrap ? ce + 2 : ce + 1, wrap ? 0 : cj + 1);
+        pc = C;
+      }
+      --pc;
+      stage_sel(ne, nj);  // position k + 1 (stale-but-valid past the launch)
+      stage_issue();
+      // shares of steps [k-17, k-1): written by wave 0 before barrier k-1
+      if (k > 1 && ((k - 1) & (kTpLossFlush - 1)) == 0) flush_losses(k - 1 - kTpLossFlush, k - 1);
+      stage_write(sn);
+      __syncthreads();  // barrier of step k
+      ce = ne;
+      cj = nj;
+      sc = sn;
+    }
+    if (n > 0) {  // the remaining loss shares (every step's share written before the final barrier)
+      __syncthreads();
+      const int kf = n > 1 ? (((n - 2) / kTpLossFlush) * kTpLossFlush) : 0;
+      for (int lo = kf; lo < n; lo += kTpLossFlush) flush_losses(lo, min(n, lo + kTpLossFlush));
+    }
+    return;
+  }
+
+  // ================================================================ compute waves
   // ---- resident state: this wave's W1 rows (b1 as column Din) and W2 columns in
   // MFMA result layouts, so the gradients land on them lane for lane and SGD runs
   // in registers:
@@ -469,17 +517,6 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   uint32_t seq = AR ? *a.ar.seq : 0u;
   bool failed = AR && *a.ar.err != 0;
 
-  // position of step 0 staged synchronously
-  stage_sel(e0, j0);
-  stage_issue();
-  stage_write(0);
-  __syncthreads();
-  {  // the rows of position 1 (epoch e0 + 1's list is filled up to batch j0)
-    const bool w1 = j0 + 1 == S;
-    stage_sel(w1 ? e0 + 1 : e0, w1 ? 0 : j0 + 1);
-  }
-
-  const float inv_full = 1.f / (float)(LOSS == kLossMSE ? B * Dout : B);
   // last step's (averaged) gradients, written to the DDP bucket at the end
   float lg1[MT][4], lg2[4], ldb2 = 0.f;
 #pragma unroll
@@ -488,10 +525,8 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) lg1[mt][i] = 0.f;
   }
-
-  int ce = e0, cj = j0;  // current position (epoch, step in epoch): no divisions in the loop
-  int sc = 0;            // LDS slot of the current batch
-  int pc = 0;            // steps until the next production chunk
+  int ce = ce0, cj = cj0;  // current position (epoch, step in epoch): no divisions in the loop
+  int sc = 0;              // LDS slot of the current batch
   constexpr bool stamps = ST;  // s_memtime is scalar: every wave times, thread 0 reports
   int64_t tmark = stamps ? (int64_t)__builtin_amdgcn_s_memtime() : 0;
   int64_t acc_t[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -510,17 +545,6 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     const int ne = wrap ? ce + 1 : ce, nj = wrap ? 0 : cj + 1;
     const int sn = sc == 2 ? 0 : sc + 1;
     const int nb = min(B, ns - cj * B);
-    // list production BEFORE the batch loads: no global load is outstanding here, so the
-    // vmcnt(0) waits hipcc places in the producer (VGPR reuse, the given-list path) cost
-    // nothing; after stage_issue they stalled every C-th step for a full load round trip
-    if (pc == 0) {
-      produce(wrap ? ce + 2 : ce + 1, wrap ? 0 : cj + 1);
-      pc = C;
-    }
-    --pc;
-    tick(6);
-    stage_issue();  // position k + 1 (rows read last step); stale-but-valid past the launch
-    tick(0);
     const float* const st = stage(sc);
 
     // ---------------- fwd1: HT = W1aug . Xaug^T (this wave's 16 units x 32 rows), ReLU
@@ -559,7 +583,6 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) Th[(4 * q + i) * LDT + 16 * t + c] = ht[t][i];
-    stage_write(sn);
     // wave-private or previous-step data the loss needs, read before the barrier so
     // that only the partial logits are waited for after it: b2 (this wave's mirror)
     // and the current batch's targets (staged in slot sc before the last barrier)
@@ -580,8 +603,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       tmark = t;
     }
     float zf[2][4];
-    // all partial reads in flight before the first add (a runtime-count loop waited on
-    // each), and ahead of the next rows' list reads in the LDS queue
+    // all partial reads in flight before the first add (a runtime-count loop waited on each)
     f4 pz[4][2];
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
@@ -591,11 +613,6 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         pz[v][1] = src[64];
       }
     }
-    {  // the rows of position k + 2 (its list entries were produced before this barrier)
-      const bool w2 = nj + 1 == S;
-      stage_sel(w2 ? ne + 1 : ne, w2 ? 0 : nj + 1);
-    }
-    if ((k & (kTpLossFlush - 1)) == 0 && k > 0) flush_losses(k - kTpLossFlush, k);  // shares written before this barrier
     f4 zs[2] = {b2v, b2v};
 #pragma unroll
     for (int v = 0; v < 4; ++v) {  // wave order: identical sums in every wave (vector adds: v_pk_add_f32)
@@ -761,28 +778,14 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         seq += 1u;
         constexpr int NV = 4 * MT + 5;
         float v[NV];
-        int idx[NV];
-        bool push[NV], need[NV];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const int in = 16 * mt + 4 * q + i;
-            const int off = in < Din ? d.oW1 + unit * Din + in : (hb && in == Din ? d.ob1 + unit : -1);
-            v[mt * 4 + i] = gv1[mt][i];
-            idx[mt * 4 + i] = off >= 0 ? off : 0;
-            push[mt * 4 + i] = need[mt * 4 + i] = off >= 0;
-          }
-          const int cls = 4 * q + i;
+          for (int mt = 0; mt < MT; ++mt) v[mt * 4 + i] = gv1[mt][i];
           v[4 * MT + i] = gv2[i];
-          idx[4 * MT + i] = cls < Dout ? d.oW2 + cls * H + unit : 0;
-          push[4 * MT + i] = need[4 * MT + i] = cls < Dout;
         }
-        v[4 * MT + 4] = db2;  // b2[class c]: one lane per class pushes
-        idx[4 * MT + 4] = (hb && c < Dout) ? d.ob2 + c : 0;
-        push[4 * MT + 4] = hb && c < Dout && q == 0 && w == 0;
-        need[4 * MT + 4] = hb && c < Dout;
-        failed = !tp_allreduce<NV>(a.ar, seq, v, idx, push, need);
+        v[4 * MT + 4] = db2;  // b2[class c]: the same value in every wave (identical loss in every wave)
+        failed = !tp_allreduce_lm<NV>(a.ar, seq, v, w, l);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -816,12 +819,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     sc = sn;
     tick(5);
   }
-
-  if (n > 0) {  // the remaining loss shares
-    __syncthreads();
-    const int kf = ((n - 1) / kTpLossFlush) * kTpLossFlush;
-    flush_losses(kf, n);
-  }
+  if (n > 0) __syncthreads();  // the helper's final flush reads every step's loss share
 
   // ---- write back: parameters, momentum, the last step's averaged gradients (DDP bucket)
   float* const Pw = a.P;
@@ -907,6 +905,8 @@ bool mlp_tp_supported(const FusedMlpArgs& a, const PersistArgs& p) {
   if (a.B < 1 || a.B > 32 || a.Din < 1 || a.Din + (a.has_bias ? 1 : 0) > 32 || a.Dout < 1 || a.Dout > 16)
     return false;
   if (a.ar.world > kXgmiMaxRanks) return false;
+  // lane-major exchange slots: NW waves x NV values x 64 lanes per rank and parity
+  if (a.ar.world > 1 && (a.H / 16) * (4 * tp_mt(a) + 5) * 64 > a.ar.max_elems) return false;
   if (p.N <= 0 || p.num_samples <= 0) return false;
   return tp_lds_bytes(a, p) <= 160 * 1024;
 }
@@ -922,7 +922,7 @@ hipError_t mlp_tp_prepare(const FusedMlpArgs& a, const PersistArgs& p, PersistLa
   const size_t lds = tp_lds_bytes(a, p);
   if (lds > 64 * 1024) PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   out->fn = fn;
-  out->threads = 64 * (a.H / 16);
+  out->threads = 64 * (a.H / 16 + 1);  // compute waves + the helper wave
   out->lds = lds;
   out->a = a;
   out->p = p;

@@ -16,7 +16,9 @@ columns; every other feature is quantised row-wise (absmax per token) to int8
 and multiplied int8 x int8 -> int32 on MFMA (``v_mfma_i32_16x16x64_i8``,
 csrc/kernels/int8_mm.hip), dequantised in the epilogue where the outlier product
 and the bias are added. (Gathering the outlier columns reads their indices on
-the host, as bitsandbytes does.)
+the host, as bitsandbytes does.) fp32, bf16 and fp16 activations run natively
+(the reference's load_in_8bit Llama is fp16); the plain-PyTorch
+``llm_int8_reference`` is the CPU path and the numerics reference only.
 """
 from __future__ import annotations
 
@@ -25,11 +27,15 @@ import torch.nn as nn
 
 from .._ext import native, use_native
 
+_NATIVE_DTYPES = (torch.float32, torch.bfloat16, torch.float16)
+_DTYPE_NAME = {torch.float32: "float32", torch.bfloat16: "bfloat16", torch.float16: "float16"}
+
 
 def quantize_rowwise(w: torch.Tensor):
     """(int8 q, fp32 scale) with ``w ~= q * scale[:, None]``."""
-    if use_native(w) and w.dtype in (torch.float32, torch.bfloat16):
-        return tuple(native().quantize_int8(w.contiguous()))
+    if use_native(w) and w.dtype in _NATIVE_DTYPES:
+        wq = w.float() if w.dtype == torch.float16 else w  # exact widening: same absmax and rounding
+        return tuple(native().quantize_int8(wq.contiguous()))
     wf = w.float()
     amax = wf.abs().amax(dim=1)
     scale = torch.where(amax > 0, amax / 127.0, torch.ones_like(amax))
@@ -85,10 +91,13 @@ class Int8Linear(nn.Module):
         return self.weight_q.float() * self.weight_scale[:, None]
 
     def _llm_int8(self, x2: torch.Tensor) -> torch.Tensor:
-        C = native()
         b = self.bias
-        if not (use_native(x2) and x2.dtype in (torch.float32, torch.bfloat16) and self.in_features % 16 == 0):
+        if not use_native(x2):  # CPU tensors: the plain-PyTorch reference
             return llm_int8_reference(x2, self.weight_q, self.weight_scale, b, self.threshold)
+        if x2.dtype not in _NATIVE_DTYPES or self.in_features % 16 != 0:
+            raise NotImplementedError(f"LLM.int8 on GPU: dtype {x2.dtype} (float32/bfloat16/float16) and "
+                                      f"in_features % 16 == 0 (got {self.in_features})")
+        C = native()
         x2 = x2.contiguous()
         mask = C.int8_col_outliers(x2, self.threshold)
         cols = mask.nonzero().flatten()  # host read: usually a handful of features
@@ -97,16 +106,19 @@ class Int8Linear(nn.Module):
         if cols.numel():
             wdq = self.weight_q.index_select(1, cols).float() * self.weight_scale[:, None]
             addend = (x2.index_select(1, cols).float() @ wdq.t()).contiguous()
-        return C.int8_mm(xq, sx, self.weight_q, self.weight_scale, addend, b, x2.dtype == torch.bfloat16)
+        return C.int8_mm(xq, sx, self.weight_q, self.weight_scale, addend, b, _DTYPE_NAME[x2.dtype])
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         shape = x.shape
         x2 = x.reshape(-1, shape[-1])
         if self.llm_int8:
             return self._llm_int8(x2).reshape(*shape[:-1], self.out_features)
-        if use_native(x2) and x2.dtype in (torch.float32, torch.bfloat16):
-            b = self.bias if self.bias is None or self.bias.dtype == x2.dtype else self.bias.to(x2.dtype)
-            y = native().int8_linear(x2.contiguous(), self.weight_q, self.weight_scale, b)
+        if use_native(x2) and x2.dtype in _NATIVE_DTYPES:
+            # weight-only kernel: fp32 / bf16 activations; fp16 runs it in fp32 (exact widening) and
+            # rounds the output back to fp16
+            xin = x2.float() if x2.dtype == torch.float16 else x2
+            b = self.bias if self.bias is None or self.bias.dtype == xin.dtype else self.bias.to(xin.dtype)
+            y = native().int8_linear(xin.contiguous(), self.weight_q, self.weight_scale, b).to(x2.dtype)
         else:
             y = (x2.float() @ self.dequantized_weight().t()).to(x.dtype)
             if self.bias is not None:

@@ -30,11 +30,15 @@ import time
 
 
 class Deadline:
-    def __init__(self, seconds: float, on_expire=None, exit_code: int = 3, grace_s: float = 10.0):
+    def __init__(self, seconds: float, on_expire=None, exit_code: int = 3, grace_s: float = 10.0,
+                 exit_delay_s: float = 0.0):
         self.seconds = float(seconds)
         self.on_expire = on_expire
         self.exit_code = exit_code
         self.grace_s = grace_s
+        # a non-reporting rank waits this long before exiting: the launcher tears the job down
+        # on the first exit, which must not cut off the reporting rank's record
+        self.exit_delay_s = exit_delay_s
         self.phase = "start"
         self.t0 = time.monotonic()
         self._abortables: list = []
@@ -85,6 +89,8 @@ class Deadline:
         t = threading.Thread(target=abort_all, daemon=True)
         t.start()
         t.join(self.grace_s)
+        if self.exit_delay_s > 0:
+            time.sleep(self.exit_delay_s)
         with contextlib.suppress(Exception):
             sys.stdout.flush()
             sys.stderr.flush()

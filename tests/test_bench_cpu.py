@@ -26,7 +26,8 @@ def _run(n, extra, env_extra=None, timeout=240):
     t0 = time.monotonic()
     p = subprocess.run(cmd, cwd=REPO, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
                        timeout=timeout)
-    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    # the record may share a line with another rank's unterminated output: take it from '{"metric"'
+    lines = [json.loads(l[l.index('{"metric"'):]) for l in p.stdout.splitlines() if '{"metric"' in l]
     return p, lines, time.monotonic() - t0
 
 

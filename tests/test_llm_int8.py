@@ -24,9 +24,11 @@ def test_llm_int8_reference_cpu_tracks_fp32_and_handles_outliers():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("M,N,K", [(70, 50, 128), (64, 64, 64), (5, 130, 48), (129, 17, 256)])
+@pytest.mark.parametrize("M,N,K", [(70, 50, 128), (64, 64, 64), (5, 130, 48), (129, 17, 256),
+                                   (256, 384, 512), (130, 260, 384), (1, 300, 1024), (300, 7, 128)])
 def test_int8_mm_exact_integer_products(dev, M, N, K):
-    """v_mfma_i32_16x16x64_i8 operand map: exact int32 products (scales 1, f32 out)."""
+    """v_mfma_i32_16x16x64_i8 operand map: exact int32 products (scales 1, f32 out); K % 128 == 0
+    runs the LDS-staged tiled kernel (edge tiles included), the rest the direct one."""
     from pytorch_distributed_training_tutorials_amd._ext import native
 
     g = torch.Generator().manual_seed(M + N + K)
@@ -38,7 +40,28 @@ def test_int8_mm_exact_integer_products(dev, M, N, K):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("out", ["float32", "bfloat16", "float16"])
+def test_int8_mm_epilogue_dtypes(dev, out):
+    """Scales, the outlier addend and a bias of the output dtype, rounded once into out."""
+    from pytorch_distributed_training_tutorials_amd._ext import native
+
+    M, N, K = 96, 200, 256
+    g = torch.Generator().manual_seed(7)
+    A = torch.randint(-127, 128, (M, K), generator=g, dtype=torch.int8)
+    B = torch.randint(-127, 128, (N, K), generator=g, dtype=torch.int8)
+    sa, sb = torch.rand(M, generator=g) * 0.01, torch.rand(N, generator=g) * 0.01
+    add = torch.randn(M, N, generator=g)
+    dt = getattr(torch, out)
+    bias = torch.randn(N, generator=g).to(dt)
+    ref = (A.double() @ B.double().t()) * sa.double()[:, None] * sb.double()[None, :] + add.double() + bias.double()
+    y = native().int8_mm(A.to(dev), sa.to(dev), B.to(dev), sb.to(dev), add.to(dev), bias.to(dev), out)
+    assert y.dtype == dt
+    tol = {"float32": 1e-5, "bfloat16": 1e-2, "float16": 2e-3}[out]
+    torch.testing.assert_close(y.cpu().double(), ref.to(dt).double(), rtol=tol, atol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("outliers", [0, 3])
 def test_llm_int8_linear_matches_reference(dev, dtype, outliers):
     from pytorch_distributed_training_tutorials_amd.ops.quant import Int8Linear, llm_int8_reference
@@ -51,9 +74,24 @@ def test_llm_int8_linear_matches_reference(dev, dtype, outliers):
     y = m(x)
     ref = llm_int8_reference(x.reshape(-1, 256), m.weight_q, m.weight_scale, m.bias, m.threshold).reshape(y.shape)
     tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    assert y.dtype == dtype
     torch.testing.assert_close(y, ref, **tol)
     full = lin(x).float()
     assert (y.float() - full).abs().max() <= 0.03 * full.abs().max()
+
+
+@pytest.mark.gpu
+def test_int8_weight_only_fp16(dev):
+    """Weight-only int8 on fp16 activations (run in fp32, output fp16) tracks the fp16 Linear."""
+    from pytorch_distributed_training_tutorials_amd.ops.quant import Int8Linear
+
+    lin = _lin(K=256, N=96, seed=2).to(dev).half()
+    m = Int8Linear.from_linear(lin)
+    x = torch.randn(17, 256, device=dev, dtype=torch.float16)
+    y = m(x)
+    assert y.dtype == torch.float16
+    full = lin(x).float()
+    assert (y.float() - full).abs().max() <= 0.02 * full.abs().max()
 
 
 @pytest.mark.gpu
