@@ -308,7 +308,7 @@ def run_persistent(args, rank, world, dev, comm):
             torch.cuda.synchronize(dev)
         v = st.tolist()
         names = (["fetch", "forward", "loss", "backward", "allreduce", "sgd_loss_report"] if which.startswith("wave") else
-                 ["stage_issue", "forward", "barrier_logit_sum", "loss", "backward", "allreduce_sgd", "produce_lists"]
+                 ["helper_wave_staging", "forward", "barrier_logit_sum", "loss", "backward", "sgd", "allreduce"]
                  if which.startswith("tp") else
                  ["prefetch_issue", "forward", "loss", "backward", "allreduce", "sgd_land", "epoch_indices"])
         clk = v[7] / (v[8] * 10e-9) if v[8] else 0.0

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Diagnose the same-device stage-stream pipeline (models/mp_resnet.py).
 
-Compares the training step of ``PipelineParallelResNet50(streams="force")`` (stage 0 and
+Compares the training step of ``PipelineParallelResNet50(streams=True)`` (stage 0 and
 stage 1 on two HIP streams of ONE device) with the single-queue schedule, per parameter,
 under several conditions, one JSON line each:
 
@@ -65,11 +65,11 @@ def main():
 
     base = step(fresh(False), x)
     compare("sq_vs_sq", step(fresh(False), x), base)
-    compare("streams", step(fresh("force"), x), base)
+    compare("streams", step(fresh(True), x), base)
     torch.backends.cudnn.deterministic = True
     base_det = step(fresh(False), x)
     compare("sq_vs_sq_det", step(fresh(False), x), base_det)
-    compare("streams_det", step(fresh("force"), x), base_det)
+    compare("streams_det", step(fresh(True), x), base_det)
     torch.backends.cudnn.deterministic = False
     xcl = x.contiguous(memory_format=torch.channels_last)
 
@@ -78,7 +78,7 @@ def main():
 
     base_cl = step(fresh_cl(False), xcl)
     compare("sq_vs_sq_cl", step(fresh_cl(False), xcl), base_cl)
-    compare("streams_cl", step(fresh_cl("force"), xcl), base_cl)
+    compare("streams_cl", step(fresh_cl(True), xcl), base_cl)
 
 
 if __name__ == "__main__":

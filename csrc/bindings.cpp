@@ -761,8 +761,10 @@ Tensor int8_col_outliers_(Tensor x, double threshold) {
   TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "int8_col_outliers: contiguous [M, K]");
   c10::hip::HIPGuard guard(x.device().index());
   Tensor mask = at::empty({x.size(1)}, x.options().dtype(at::kByte));
+  Tensor ws = at::empty({x.size(1)}, x.options().dtype(at::kInt));
   hip_check(int8_col_outliers(x.data_ptr(), dt_of16(x), (int)x.size(0), (int)x.size(1), (float)threshold,
-                              mask.data_ptr<uint8_t>(), cur_stream(x)),
+                              mask.data_ptr<uint8_t>(), reinterpret_cast<unsigned*>(ws.data_ptr<int32_t>()),
+                              cur_stream(x)),
             "int8_col_outliers");
   return mask;
 }

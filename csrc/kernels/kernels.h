@@ -291,7 +291,9 @@ hipError_t int8_weight_gemm(const void* x, int x_dtype, const int8_t* q, const f
 // LLM.int8 (csrc/kernels/int8_mm.hip): outlier columns (|x| > threshold), row-wise
 // activation quantisation with them zeroed, int8 x int8 -> int32 MFMA GEMM with the
 // dequantisation, the caller's outlier product (addend, f32 [M,N]) and bias in the epilogue.
-hipError_t int8_col_outliers(const void* x, int dtype, int M, int K, float threshold, uint8_t* mask, hipStream_t s);
+// ws: K unsigned of scratch (the column maxima)
+hipError_t int8_col_outliers(const void* x, int dtype, int M, int K, float threshold, uint8_t* mask, unsigned* ws,
+                             hipStream_t s);
 hipError_t int8_quant_rows(const void* x, int dtype, int M, int K, const uint8_t* mask, int8_t* q, float* scale,
                            hipStream_t s);
 // x / y / bias dtypes: kF32, kBF16 or kF16. K % 128 == 0 and 16-B aligned operands take the

@@ -178,8 +178,10 @@ __device__ __forceinline__ bool ll_exchange(bool active, uint64_t PTDT_GLOBAL* p
   }
 }
 
-// Uniform LL exchange for layout F (row slot i <-> rank i, csrc/comm/xgmi.h words).
-// Differences from ll_exchange (tools/exchange_bench.hip measures both):
+// Uniform LL exchange for layout F (row slot i <-> rank i, csrc/comm/xgmi.h words) -- an
+// alternative kept for tools/exchange_bench.hip, NOT used by the engines: measured on MI355X
+// (profiles/r3_exchange_bench.jsonl) it is no faster than ll_exchange; the exchange is bound by
+// the store-to-visible latency, not by the poll loop. Differences from ll_exchange:
 //   * every lane polls a real slot: slot i < world (i != rank) polls rank i's chunk;
 //     this rank's own slot and the slots >= world poll a peer's chunk too and then
 //     take the own registers / 0. The poll loop is ONE uniform loop with a ballot
@@ -191,41 +193,49 @@ __device__ __forceinline__ bool ll_exchange(bool active, uint64_t PTDT_GLOBAL* p
 // own registers in slot `rank`, 0 above world), so the caller's row16_sum gives the
 // same bits as before, on every rank. Returns false after a poll timeout (sets *err).
 template <int KP, int DOUT>
-__device__ __forceinline__ bool ll_exchange_u(bool push, uint64_t PTDT_GLOBAL* push_base,
-                                              uint64_t PTDT_GLOBAL* poll_base, int my_rank, int slot, int world,
-                                              int max_elems, uint32_t seq, int k0, int Din, bool hb, bool bias_lane,
-                                              bool padded, const float (&gW)[DOUT][KP], const float (&gb)[DOUT],
-                                              float (&v)[DOUT][KP], float (&vb)[DOUT], int* err,
-                                              uint32_t max_polls) {
-  constexpr int NS = DOUT * (KP + 1);
+__device__ __forceinline__ void ll_push_chunk(uint64_t PTDT_GLOBAL* push_base, int my_rank, int world, int max_elems,
+                                              uint32_t seq, int k0, int Din, bool hb, bool bias_lane, bool padded,
+                                              const float (&gW)[DOUT][KP], const float (&gb)[DOUT]) {
   const int parity = (int)(seq & 1u);
   const int nW = DOUT * Din;
   const uint64_t hi = (uint64_t)seq << 32;
-  if (push) {
-    uint64_t PTDT_GLOBAL* const dst = push_base + (int64_t)(parity * world + my_rank) * max_elems;
-    if (!padded) {
+  uint64_t PTDT_GLOBAL* const dst = push_base + (int64_t)(parity * world + my_rank) * max_elems;
+  if (!padded) {
 #pragma unroll
-      for (int c = 0; c < DOUT; ++c)
+    for (int c = 0; c < DOUT; ++c)
 #pragma unroll
-        for (int k = 0; k < KP; ++k)
+      for (int k = 0; k < KP; ++k)
+        __hip_atomic_store(dst + c * Din + k0 + k, hi | __float_as_uint(gW[c][k]), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+  } else {
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c)
+#pragma unroll
+      for (int k = 0; k < KP; ++k)
+        if (k0 + k < Din)
           __hip_atomic_store(dst + c * Din + k0 + k, hi | __float_as_uint(gW[c][k]), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_SYSTEM);
-    } else {
-#pragma unroll
-      for (int c = 0; c < DOUT; ++c)
-#pragma unroll
-        for (int k = 0; k < KP; ++k)
-          if (k0 + k < Din)
-            __hip_atomic_store(dst + c * Din + k0 + k, hi | __float_as_uint(gW[c][k]), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    if (hb && bias_lane)
-#pragma unroll
-      for (int c = 0; c < DOUT; ++c)
-        __hip_atomic_store(dst + nW + c, hi | __float_as_uint(gb[c]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  const bool peer = slot < world && slot != my_rank;
-  const int src_rank = peer ? slot : (my_rank + 1 == world ? 0 : my_rank + 1);  // some real peer's chunk
+  if (hb && bias_lane)
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c)
+      __hip_atomic_store(dst + nW + c, hi | __float_as_uint(gb[c]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Poll half of ll_exchange_u: slot `slot` < world polls rank `slot`'s chunk (every rank's,
+// own included when `own_from_memory`, i.e. the own chunk was self-pushed); other slots poll
+// a real peer's chunk and take 0 (or the own registers for slot == rank without self-push).
+template <int KP, int DOUT>
+__device__ __forceinline__ bool ll_poll_chunk(uint64_t PTDT_GLOBAL* poll_base, int my_rank, int slot, int world,
+                                              int max_elems, uint32_t seq, int k0, int Din, bool hb,
+                                              bool own_from_memory, const float (&gW)[DOUT][KP],
+                                              const float (&gb)[DOUT], float (&v)[DOUT][KP], float (&vb)[DOUT],
+                                              int* err, uint32_t max_polls) {
+  constexpr int NS = DOUT * (KP + 1);
+  const int parity = (int)(seq & 1u);
+  const int nW = DOUT * Din;
+  const bool mem = slot < world && (slot != my_rank || own_from_memory);
+  const int src_rank = mem ? slot : (my_rank + 1 == world ? 0 : my_rank + 1);  // some real chunk
   uint64_t PTDT_GLOBAL* const src = poll_base + (int64_t)(parity * world + src_rank) * max_elems;
   int off[NS];
 #pragma unroll
@@ -245,17 +255,17 @@ __device__ __forceinline__ bool ll_exchange_u(bool push, uint64_t PTDT_GLOBAL* p
     for (int s = 0; s < NS; ++s) m |= (uint32_t)(w[s] >> 32) != seq;
     return __builtin_amdgcn_ballot_w64(m) != 0;  // uniform
   };
-  const bool own = slot == my_rank;
+  const bool own = slot == my_rank && !own_from_memory;
   auto take = [&](const uint64_t (&w)[NS]) {
 #pragma unroll
     for (int c = 0; c < DOUT; ++c) {
 #pragma unroll
       for (int k = 0; k < KP; ++k) {
         const float x = __uint_as_float((uint32_t)w[c * (KP + 1) + k]);
-        v[c][k] = own ? gW[c][k] : ((peer && k0 + k < Din) ? x : 0.f);
+        v[c][k] = own ? gW[c][k] : ((mem && k0 + k < Din) ? x : 0.f);
       }
       const float xb = __uint_as_float((uint32_t)w[c * (KP + 1) + KP]);
-      vb[c] = own ? gb[c] : ((peer && hb) ? xb : 0.f);
+      vb[c] = own ? gb[c] : ((mem && hb) ? xb : 0.f);
     }
   };
   issue(wa);
@@ -277,6 +287,18 @@ __device__ __forceinline__ bool ll_exchange_u(bool push, uint64_t PTDT_GLOBAL* p
       return false;
     }
   }
+}
+
+template <int KP, int DOUT>
+__device__ __forceinline__ bool ll_exchange_u(bool push, uint64_t PTDT_GLOBAL* push_base,
+                                              uint64_t PTDT_GLOBAL* poll_base, int my_rank, int slot, int world,
+                                              int max_elems, uint32_t seq, int k0, int Din, bool hb, bool bias_lane,
+                                              bool padded, const float (&gW)[DOUT][KP], const float (&gb)[DOUT],
+                                              float (&v)[DOUT][KP], float (&vb)[DOUT], int* err,
+                                              uint32_t max_polls) {
+  if (push) ll_push_chunk<KP, DOUT>(push_base, my_rank, world, max_elems, seq, k0, Din, hb, bias_lane, padded, gW, gb);
+  return ll_poll_chunk<KP, DOUT>(poll_base, my_rank, slot, world, max_elems, seq, k0, Din, hb, false, gW, gb, v, vb,
+                                 err, max_polls);
 }
 
 template <int R, int KP, int DOUT, int RY>
@@ -1105,11 +1127,17 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     // ---- all-reduce over ranks: row slot r <-> rank r, summed with the same DPP tree
     if (AR && !failed) {
       seq += 1u;
-      float v[DOUT][KP], vb[DOUT];  // slot i: rank i's chunk (own from registers), 0 above world
-      const bool drop = ar.drop_push != 0u && seq >= ar.drop_push;  // fault injection: never reach the peers
-      const bool ok = ll_exchange_u<KP, DOUT>(i < world && i != my_rank && !drop, push_dst, poll_src, my_rank, i,
-                                              world, max_elems, seq, k0, Din, hb, q == 0, 4 * KP != Din, gW, gb, v,
-                                              vb, ar.err, ar.max_polls);
+      float v[DOUT][KP], vb[DOUT];
+#pragma unroll
+      for (int c = 0; c < DOUT; ++c) {  // own contribution from registers, slots >= world add 0
+        vb[c] = i == my_rank ? gb[c] : 0.f;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) v[c][k] = i == my_rank ? gW[c][k] : 0.f;
+      }
+      // (ll_exchange_u / a separate pusher or poller wave measured no faster: tools/exchange_bench.hip)
+      const bool ok = ll_exchange<KP, DOUT>(i < world && i != my_rank, push_dst, poll_src, my_rank, i, world,
+                                            max_elems, seq, k0, Din, hb, q == 0, 4 * KP != Din, gW, gb, v, vb,
+                                            ar.err, ar.max_polls, ar.drop_push != 0u && seq >= ar.drop_push);
       failed = !ok;
       failed = __any(failed);
 #pragma unroll

@@ -795,6 +795,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         db2 = v[4 * MT + 4];
       }
     }
+    tick(6);  // the all-reduce alone (0 at world 1; index 6 was the list producer before the helper wave)
     // padded inputs / classes have zero gradients and zero weights: no masks needed
     const bool first = opt_step == 0;
 #pragma unroll
@@ -857,7 +858,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   if (tid == 0) {
     pa.cursor[0] = ce;
     pa.cursor[1] = cj;
-    if (stamps) {  // [0] stage issue+produce [1] fwd [2] barrier+sum [3] loss [4] bwd MFMA [5] all-reduce+SGD
+    if (stamps) {  // [0] - (helper wave) [1] fwd [2] barrier+sum [3] loss [4] bwd MFMA [5] SGD [6] all-reduce
       for (int k = 0; k < 7; ++k) pa.stamps[k] += acc_t[k];
       pa.stamps[7] += (int64_t)__builtin_amdgcn_s_memtime() - t_begin;
       pa.stamps[8] += (int64_t)__builtin_amdgcn_s_memrealtime() - r_begin;
@@ -871,9 +872,9 @@ int tp_mt(const FusedMlpArgs& a) { return a.Din + (a.has_bias ? 1 : 0) <= 16 ? 1
 
 template <int LOSS, bool AR, bool VX>
 const void* pick_mt(int mt, bool st) {
-  if (st && !AR)  // phase timers: world-1 diagnostic builds only
-    return mt == 1 ? (const void*)mlp_tp_kernel<1, LOSS, false, VX, true>
-                   : (const void*)mlp_tp_kernel<2, LOSS, false, VX, true>;
+  if (st)  // phase timers (diagnostic instantiations; the all-reduce's share shows at world > 1)
+    return mt == 1 ? (const void*)mlp_tp_kernel<1, LOSS, AR, VX, true>
+                   : (const void*)mlp_tp_kernel<2, LOSS, AR, VX, true>;
   return mt == 1 ? (const void*)mlp_tp_kernel<1, LOSS, AR, VX, false> : (const void*)mlp_tp_kernel<2, LOSS, AR, VX, false>;
 }
 
@@ -905,8 +906,9 @@ bool mlp_tp_supported(const FusedMlpArgs& a, const PersistArgs& p) {
   if (a.B < 1 || a.B > 32 || a.Din < 1 || a.Din + (a.has_bias ? 1 : 0) > 32 || a.Dout < 1 || a.Dout > 16)
     return false;
   if (a.ar.world > kXgmiMaxRanks) return false;
-  // lane-major exchange slots: NW waves x NV values x 64 lanes per rank and parity
-  if (a.ar.world > 1 && (a.H / 16) * (4 * tp_mt(a) + 5) * 64 > a.ar.max_elems) return false;
+  // lane-major exchange slots: NW waves x NV values x 64 lanes per rank and parity (max_elems 0:
+  // a configuration query without a buffer yet -- XgmiAllReduce's default holds 16x more)
+  if (a.ar.world > 1 && a.ar.max_elems > 0 && (a.H / 16) * (4 * tp_mt(a) + 5) * 64 > a.ar.max_elems) return false;
   if (p.N <= 0 || p.num_samples <= 0) return false;
   return tp_lds_bytes(a, p) <= 160 * 1024;
 }

@@ -71,7 +71,11 @@ def _run(cmd):
     return p.stdout
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False, stamps: bool = False) -> Path:
+    """Build the extension. ``stamps=True`` builds a DIAGNOSTIC copy instead: the single-wave
+    engine with its per-phase timers compiled in (-DPTDT_WAVE_STAMPS=1, objects in
+    build/native_stamps, every other object shared), linked to tools/bin/_C_stamps.so; load it
+    with ``PTDT_EXT_PATH=tools/bin/_C_stamps.so`` for ``bench.py --stamps`` phase splits."""
     hipcc = _hipcc()
     incs, tlib, abi, _ = _torch_paths()
     py_inc = sysconfig.get_paths()["include"]
@@ -88,13 +92,19 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     jobs = jobs or min(8, (os.cpu_count() or 2))
     todo = []
     objs = []
+    stamp_dir = REPO / "build" / "native_stamps"
+    if stamps:
+        stamp_dir.mkdir(parents=True, exist_ok=True)
     for src in kernels:
-        obj = BUILD / (src.stem + ".o")
+        wave = src.stem.startswith("linear_wave")
+        obj = (stamp_dir if (stamps and wave) else BUILD) / (src.stem + ".o")
         objs.append(obj)
         if force or _newer(src, obj, hdrs):
             # single-wave engine: no SLP vectorisation -- it splits DPP adds into
             # v_mov_dpp + v_pk_add pairs (plus zero-inits), ~50 extra VALU per step
-            extra = ["-fno-slp-vectorize"] if src.stem.startswith("linear_wave") else []
+            extra = ["-fno-slp-vectorize"] if wave else []
+            if stamps and wave:
+                extra.append("-DPTDT_WAVE_STAMPS=1")
             todo.append([hipcc, *common, *extra, "-c", str(src), "-o", str(obj)])
     for src in hosts:
         obj = BUILD / (src.stem + ".host.o")
@@ -107,14 +117,16 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
             for out in ex.map(_run, todo):
                 if verbose and out.strip():
                     print(out)
-    relink = force or bool(todo) or not TARGET.exists() or any(o.stat().st_mtime > TARGET.stat().st_mtime for o in objs)
+    target = (REPO / "tools" / "bin" / "_C_stamps.so") if stamps else TARGET
+    target.parent.mkdir(parents=True, exist_ok=True)
+    relink = force or bool(todo) or not target.exists() or any(o.stat().st_mtime > target.stat().st_mtime for o in objs)
     if relink:
-        tmp = TARGET.with_suffix(".tmp.so")
+        tmp = target.with_suffix(".tmp.so")
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", str(tmp), *map(str, objs),
               f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-ltorch_python",
               "-lrccl", "-lamdhip64", f"-Wl,-rpath,{tlib}", "-Wl,--no-as-needed"])
-        os.replace(tmp, TARGET)
-    return TARGET
+        os.replace(tmp, target)
+    return target
 
 
 def main(argv=None):
@@ -122,8 +134,9 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--stamps", action="store_true", help="diagnostic build with the wave engine's phase timers")
     a = ap.parse_args(argv)
-    out = build(force=a.force, jobs=a.jobs, verbose=a.verbose)
+    out = build(force=a.force, jobs=a.jobs, verbose=a.verbose, stamps=a.stamps)
     print(f"built {out}")
 
 

@@ -22,6 +22,14 @@ step() {  # name secs cmd...   (stdout+stderr -> $O/$T_name.log)
   echo "=== $name exit $c"; tail -4 "$O/${T}_$name.log"
   [ $c -eq 0 ] || { echo "STOP after $name (exit $c)"; exit $c; }
 }
+tstep() {  # like step, but test failures (exit 1) do not end the script; crashes/timeouts do
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$O/${T}_$name.log" 2>&1
+  local c=$?
+  echo "=== $name exit $c"; tail -4 "$O/${T}_$name.log"
+  [ $c -eq 0 ] || [ $c -eq 1 ] || { echo "STOP after $name (exit $c)"; exit $c; }
+}
 jstep() {  # name secs cmd...   (JSON lines appended to $O/$T_name.jsonl, the rest to .err)
   local name=$1 secs=$2; shift 2
   echo "=== $name ($(date +%T))"
@@ -55,8 +63,8 @@ P2="SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_
 
 for s in "$@"; do
   case $s in
-    tests)     step pytest_gpu 1000 $PYTEST tests -m gpu ;;
-    tests:*)   step "pytest_${s#tests:}" 600 $PYTEST ${s#tests:} ;;  # tests:tests/test_x.py
+    tests)     tstep pytest_gpu 1000 python3 -u -m pytest -q -rf --timeout 120 --timeout-method thread tests -m gpu ;;
+    tests:*)   tstep pytest_sel 600 python3 -u -m pytest -q -rf --timeout 120 --timeout-method thread ${s#tests:} ;;
     smoke)     step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     driver)    for i in 1 2 3; do jstep bench_driver 300 python3 bench.py --gpus 1 --steps 20 --warmup 5; done ;;
     default)   jstep bench_default 300 python3 bench.py ;;
@@ -66,6 +74,12 @@ for s in "$@"; do
                share share 4 --steps 20000 --warmup 2000 --stamps --no_mlp_side
                share share 2 --model mlp --steps 20000 --warmup 2000 --stamps
                share share 4 --model mlp --steps 5000 --warmup 500 --stamps ;;
+    wstamps)   # single-wave engine phase split (diagnostic build, tools/bin/_C_stamps.so) at W = 1, 2, 4
+               export PTDT_EXT_PATH=$PWD/tools/bin/_C_stamps.so
+               jstep wstamps 300 python3 bench.py --steps 20000 --warmup 2000 --stamps --no_mlp_side --no_ref
+               share wstamps 2 --steps 20000 --warmup 2000 --stamps --no_mlp_side
+               share wstamps 4 --steps 20000 --warmup 2000 --stamps --no_mlp_side
+               unset PTDT_EXT_PATH ;;
     share_fused) share share_fused 2 --engine fused --steps 2000 --warmup 200
                share share_fused 4 --engine fused --model mlp --steps 2000 --warmup 200 ;;
     engines)   jstep engines 300 python3 bench.py --engine fused --steps 2000 --warmup 200
@@ -75,8 +89,12 @@ for s in "$@"; do
     apps)      step mp_toy 300 python3 model_parallel.py toy
                step mp_resnet 600 python3 model_parallel.py resnet --repeat 5 --json $O/${T}_mp_resnet.json --fig $O/${T}_mp_vs_single.png
                step dp_toy 300 python3 data_parallel.py --quiet ;;
+    int8)      jstep int8 300 python3 benchmarks/int8_bench.py ;;
+    probe)     jstep probe 300 python3 benchmarks/pipeline_stream_probe.py ;;
+    exch)      step exch 120 bash -c "tools/bin/exchange_bench > $O/${T}_exchange.jsonl" ;;
     resnet)    jstep resnet_ddp 600 python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5
                jstep resnet_ddp 600 python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5 --impl torch ;;
+    prof_resnet) prof resnet 600 python3 benchmarks/resnet_ddp.py --steps 3 --warmup 2 ;;
     prof)      prof driver 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
                prof reference 300 python3 bench.py --engine reference --steps 200 --warmup 20 ;;
     pmc_tp)    pmc tp1 "$P1" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side

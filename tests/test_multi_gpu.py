@@ -219,6 +219,7 @@ def test_stream_pipeline_two_gpus_matches_single_queue_pipeline():
     as the reference's single-queue pipeline schedule."""
     from pytorch_distributed_training_tutorials_amd.models.mp_resnet import PipelineParallelResNet50
 
+    torch.backends.cudnn.deterministic = True  # MIOpen's default wgrad solvers vary run to run (~9 %)
     torch.manual_seed(3)
     a = PipelineParallelResNet50(split_size=4, num_classes=10, dev0="cuda:0", dev1="cuda:1", streams=True)
     b = PipelineParallelResNet50(split_size=4, num_classes=10, dev0="cuda:0", dev1="cuda:1", streams=False)
@@ -232,6 +233,7 @@ def test_stream_pipeline_two_gpus_matches_single_queue_pipeline():
         torch.cuda.synchronize("cuda:0")
         torch.cuda.synchronize("cuda:1")
         outs.append((y.detach().cpu(), [p.grad.detach().cpu() for p in m.parameters()]))
-    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-4, atol=1e-5)
-    for ga, gb in zip(outs[0][1], outs[1][1]):
-        torch.testing.assert_close(ga, gb, rtol=1e-3, atol=1e-5)
+    torch.backends.cudnn.deterministic = False
+    torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-6)
+    worst = max(((ga - gb).abs().max() / (gb.abs().max() + 1e-30)).item() for ga, gb in zip(outs[0][1], outs[1][1]))
+    assert worst <= 1e-5, worst
