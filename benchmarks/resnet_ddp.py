@@ -109,7 +109,7 @@ def main(argv=None):
             "dtype": a.dtype, "data": "synthetic ImageNet-shaped (generated on device)",
             "config": {"model": "resnet50", "per_device_batch": a.batch_size, "image": a.image,
                        "parallelism": f"dp{world}", "channels_last": not a.no_channels_last},
-            "impl": a.impl, "miopen_find": "exhaustive (cudnn.benchmark)" if torch.backends.cudnn.benchmark else "heuristic",
+            "impl": a.impl, "bn_dir": os.environ.get("PTDT_BN_DIR", "0"), "miopen_find": "exhaustive (cudnn.benchmark)" if torch.backends.cudnn.benchmark else "heuristic",
             "buckets_MB": [round(b / 2 ** 20, 2) for b in ddp.bucket_sizes_bytes()] if a.impl == "native" else None,
             "final_loss": float(loss.detach()),
         }), flush=True)

@@ -896,7 +896,7 @@ const float* opt_f32(const c10::optional<Tensor>& t, int64_t C, const char* name
 std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> weight, c10::optional<Tensor> bias,
                                  c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var,
                                  c10::optional<Tensor> num_batches_tracked, c10::optional<Tensor> residual, bool relu,
-                                 double momentum, double eps, c10::optional<Tensor> tickets) {
+                                 double momentum, double eps, c10::optional<Tensor> tickets, bool want_mask) {
   int64_t M;
   int C;
   bn_rows(x, &M, &C);
@@ -934,15 +934,20 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> weight, c10::op
   a.p.invstd = st + C;
   a.p.scale = st + 2 * C;
   a.p.shift = st + 3 * C;
+  Tensor mask;
+  if (want_mask && relu && a.residual != nullptr) {  // one byte per 16-B vector of x
+    mask = at::empty({M * C / (x.scalar_type() == at::kFloat ? 4 : 8)}, x.options().dtype(at::kByte));
+    a.mask_out = mask.data_ptr<uint8_t>();
+  }
   hip_check(bn_forward_train(a, cur_stream(x)), "bn_forward_train");
-  return {y, stats};
+  return {y, stats, mask};
 }
 
 // Backward: returns (dx, dweight, dbias, dres); dres undefined unless want_dres.
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::optional<Tensor> weight, Tensor stats,
                            bool relu, bool want_dres, bool want_dweight, c10::optional<Tensor> tickets,
                            c10::optional<Tensor> dweight_out, c10::optional<Tensor> dbias_out,
-                           c10::optional<Tensor> dy2) {
+                           c10::optional<Tensor> dy2, c10::optional<Tensor> mask) {
   int64_t M;
   int C;
   bn_rows(x, &M, &C);
@@ -957,7 +962,12 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::op
     a.dy2 = dy2->data_ptr();
   }
   a.x = x.data_ptr();
-  if (relu && y.has_value() && y->defined()) {  // else: the mask is recomputed from x (no residual)
+  if (relu && mask.has_value() && mask->defined()) {  // the forward's bit mask (needs want_dres)
+    TORCH_CHECK(want_dres && mask->is_cuda() && mask->scalar_type() == at::kByte &&
+                    mask->numel() == M * C / (x.scalar_type() == at::kFloat ? 4 : 8),
+                "batchnorm: mask must be the forward's [M*C/V] byte mask, with want_dres");
+    a.mask = mask->data_ptr<uint8_t>();
+  } else if (relu && y.has_value() && y->defined()) {  // else: the mask is recomputed from x (no residual)
     same_rows(*y, x, "y");
     a.y = y->data_ptr();
   }
@@ -1164,10 +1174,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_relu", &bn_relu);
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("num_batches_tracked"), py::arg("residual"), py::arg("relu"),
-        py::arg("momentum"), py::arg("eps"), py::arg("tickets") = py::none());
+        py::arg("momentum"), py::arg("eps"), py::arg("tickets") = py::none(), py::arg("want_mask") = false);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("weight"), py::arg("stats"),
         py::arg("relu"), py::arg("want_dres"), py::arg("want_dweight"), py::arg("tickets") = py::none(),
-        py::arg("dweight_out") = py::none(), py::arg("dbias_out") = py::none(), py::arg("dy2") = py::none());
+        py::arg("dweight_out") = py::none(), py::arg("dbias_out") = py::none(), py::arg("dy2") = py::none(),
+        py::arg("mask") = py::none());
   m.def("maxpool2d_fwd", &maxpool2d_fwd);
   m.def("maxpool2d_bwd", &maxpool2d_bwd);
   m.def("bn_apply", &bn_apply_, py::arg("x"), py::arg("residual"), py::arg("scale"), py::arg("shift"),

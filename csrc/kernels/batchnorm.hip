@@ -38,6 +38,7 @@
 // -- is recomputed from x with the forward's own fmaf(x, scale, shift), sparing
 // one of the three reads in both backward passes.
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
@@ -47,9 +48,46 @@ namespace {
 
 constexpr int kThreads = 256;   // apply kernels
 constexpr int kRed = 512;       // reduction kernels
-constexpr int kMaxTC = 8;       // channel vectors per block row: 64 bf16 / 32 f32 channels per tile
 constexpr int kRedBlocks = 384; // ~1.5 reduction blocks per CU
 constexpr int kMaxGx = 256;     // row blocks per channel tile (bounds the last block's combine)
+
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return (e && e[0]) ? atoi(e) : dflt;
+}
+// channel vectors per block row of a reduction (a tile of TC*V channels): 32 (whole 512-B rows
+// of a C = 256 bf16 tensor per 32 lanes) for tall tensors, where the wider tile measured up to
+// 13 % faster, 8 below (more row blocks to fill the chip; profiles/r3_bn_sweep.md).
+// PTDT_BN_TC forces one width.
+constexpr int64_t kWideRows = 262144;
+int forced_tc() {
+  static const int v = [] {
+    const int t = env_int("PTDT_BN_TC", 0);
+    return (t == 4 || t == 8 || t == 16 || t == 32 || t == 64) ? t : 0;
+  }();
+  return v;
+}
+int max_tc(int64_t M) {
+  const int f = forced_tc();
+  return f ? f : (M >= kWideRows ? 32 : 8);
+}
+int min_tc() {  // the narrowest tile any M may get: sizes the ticket array
+  const int f = forced_tc();
+  return f ? f : 8;
+}
+// vectors per thread in flight in the elementwise passes (PTDT_BN_AU: 1, 2, 4)
+int apply_unroll() {
+  static const int v = [] {
+    const int u = env_int("PTDT_BN_AU", 1);
+    return (u == 1 || u == 2 || u == 4) ? u : 1;
+  }();
+  return v;
+}
+// cap on elementwise workgroups (grid-stride beyond it); PTDT_BN_APPLY_BLOCKS, 0 = uncapped
+int apply_block_cap() {
+  static const int v = env_int("PTDT_BN_APPLY_BLOCKS", 4096);
+  return v;
+}
 
 template <typename T>
 struct VecIO {
@@ -102,8 +140,8 @@ template <typename T>
 Geom geom(int64_t M, int C) {
   constexpr int V = VecIO<T>::V;
   Geom g;
-  const int cv = C / V;
-  g.TC = cv < kMaxTC ? cv : kMaxTC;
+  const int cv = C / V, mt = max_tc(M);
+  g.TC = cv < mt ? cv : mt;
   g.RPI = kRed / g.TC;
   g.gy = (cv + g.TC - 1) / g.TC;
   int64_t want = (M + (int64_t)g.RPI * 16 - 1) / ((int64_t)g.RPI * 16);  // >= 16 rows per thread
@@ -227,6 +265,10 @@ __global__ void __launch_bounds__(kRed) bn_stats_kernel(const T* __restrict__ x,
   const int tid = threadIdx.x, rr = tid / TC, tc = tid % TC;
   const int c0 = (blockIdx.y * TC + tc) * V;  // this thread's channels c0..c0+V
   const bool active = rr < RPI && c0 < C;
+  // il bit 1: sweep the rows last to first (pass_dirs())
+  const bool rev = (il & 2) != 0;
+  il &= 1;
+  auto row = [&](int64_t r) { return rev ? M - 1 - r : r; };
   // il: rows interleaved across the row blocks in RPI-row chunks (block b: chunks b, b + gx, ...),
   // so the grid sweeps the tensor front to back together, as the elementwise passes do; else each
   // block owns one contiguous slab of rows_per_block rows (gx separate streams)
@@ -243,7 +285,7 @@ __global__ void __launch_bounds__(kRed) bn_stats_kernel(const T* __restrict__ x,
     for (; r + (U - 1) * rs < re; r += U * rs) {  // U independent 16-B loads in flight
       float a[U][V];
 #pragma unroll
-      for (int u = 0; u < U; ++u) VecIO<T>::load(x + (r + u * rs) * C + c0, a[u]);
+      for (int u = 0; u < U; ++u) VecIO<T>::load(x + row(r + u * rs) * C + c0, a[u]);
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -255,7 +297,7 @@ __global__ void __launch_bounds__(kRed) bn_stats_kernel(const T* __restrict__ x,
     }
     for (; r < re; r += rs) {
       float a[V];
-      VecIO<T>::load(x + r * C + c0, a);
+      VecIO<T>::load(x + row(r) * C + c0, a);
 #pragma unroll
       for (int v = 0; v < V; ++v) {
         const float d = a[v] - K[v];
@@ -299,10 +341,14 @@ __global__ void __launch_bounds__(kRed) bn_stats_kernel(const T* __restrict__ x,
   }
 }
 
-template <typename T, bool RELU, bool RES>
+// MASKOUT: also write the ReLU mask, one byte per V-vector (bit v: y > 0), for a backward that
+// then reads 1/16 (bf16) of a tensor instead of y
+// Elementwise passes: each thread keeps AU vectors (stride apart) in flight per iteration.
+template <typename T, bool RELU, bool RES, bool MASKOUT = false, int AU = 1>
 __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const T* __restrict__ x, const T* __restrict__ res,
                                                             T* __restrict__ y, const float* __restrict__ scale,
-                                                            const float* __restrict__ shift, int64_t nvec, int C) {
+                                                            const float* __restrict__ shift, int64_t nvec, int C,
+                                                            int rev, uint8_t* __restrict__ mask) {
   constexpr int V = VecIO<T>::V;
   extern __shared__ float sh[];  // scale[C], shift[C]
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -312,37 +358,63 @@ __global__ void __launch_bounds__(kThreads) bn_apply_kernel(const T* __restrict_
   __syncthreads();
   const int cv = C / V;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-    const int c0 = (int)(i % cv) * V;
-    float a[V];
-    VecIO<T>::load(x + i * V, a);
-    float rv[V];
-    if constexpr (RES) VecIO<T>::load(res + i * V, rv);
+  auto vid = [&](int64_t i) { return rev ? nvec - 1 - i : i; };  // rev: last vector first
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nvec; i0 += AU * stride) {
+    float a[AU][V], rv[AU][V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-      float o = fmaf(a[v], sh[c0 + v], sh[C + c0 + v]);
-      if constexpr (RES) o += rv[v];
-      if constexpr (RELU) o = fmaxf(o, 0.f);
-      a[v] = o;
+    for (int u = 0; u < AU; ++u) {
+      const int64_t i = vid(i0 + u * stride);
+      if (i0 + u * stride < nvec) {
+        VecIO<T>::load(x + i * V, a[u]);
+        if constexpr (RES) VecIO<T>::load(res + i * V, rv[u]);
+      }
     }
-    VecIO<T>::store(y + i * V, a);
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      if (i0 + u * stride >= nvec) break;
+      const int64_t i = vid(i0 + u * stride);
+      const int c0 = (int)(i % cv) * V;
+      unsigned bits = 0;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float o = fmaf(a[u][v], sh[c0 + v], sh[C + c0 + v]);
+        if constexpr (RES) o += rv[u][v];
+        if constexpr (RELU) o = fmaxf(o, 0.f);
+        if constexpr (MASKOUT) bits |= (o > 0.f ? 1u : 0u) << v;
+        a[u][v] = o;
+      }
+      VecIO<T>::store(y + i * V, a[u]);
+      if constexpr (MASKOUT) mask[i] = (uint8_t)bits;
+    }
   }
 }
 
 // MASK: 0 no ReLU, 1 ReLU mask from the forward output y, 2 ReLU mask recomputed
 // from x (y > 0 <=> fmaf(x, scale, shift) > 0 bit-exactly, as the forward applied
 // it): BNs without a residual skip reading y in both backward passes.
+// MASK 3: the forward's bit mask (one byte per V-vector); `y` carries the bit as 0 / 1.
 template <int MASK, int V>
 __device__ __forceinline__ float masked_dy(float g, float x, float y, float sc, float sf) {
-  if constexpr (MASK == 1) return y > 0.f ? g : 0.f;
+  if constexpr (MASK == 1 || MASK == 3) return y > 0.f ? g : 0.f;
   if constexpr (MASK == 2) return fmaf(x, sc, sf) > 0.f ? g : 0.f;
   return g;
 }
 
-template <typename T, int MASK, bool ADD2>
+// T-rounded value (what a T tensor holds): identity for f32
+template <typename T>
+__device__ __forceinline__ float round_to(float v) {
+  if constexpr (sizeof(T) == 4) return v;
+  return bf16_to_f32(f32_to_bf16(v));
+}
+
+// GOUT: the masked gradient g = mask (dy + dy2), rounded to T, is also written (to gout): it IS
+// the residual gradient, and the apply pass then reads g and x only (bn_bwd_apply_g_kernel)
+// instead of dy, dy2, x and the mask. The sums use the rounded g, so both passes agree.
+template <typename T, int MASK, bool ADD2, bool GOUT = false>
 __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
                                                              const T* __restrict__ x,
-                                                             const T* __restrict__ y, int64_t M, int C, int TC,
+                                                             const T* __restrict__ y, const uint8_t* __restrict__ mk,
+                                                             T* __restrict__ gout, int64_t M, int C, int TC,
                                                              int RPI, int64_t rows_per_block, int il, float* ws,
                                                              int* tickets, BnBwdParams p) {
   constexpr int V = VecIO<T>::V;
@@ -352,6 +424,9 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
   const int tid = threadIdx.x, rr = tid / TC, tc = tid % TC;
   const int c0 = (blockIdx.y * TC + tc) * V;
   const bool active = rr < RPI && c0 < C;
+  const bool rev = (il & 2) != 0;
+  il &= 1;
+  auto row = [&](int64_t r) { return rev ? M - 1 - r : r; };
   const int64_t rs = il ? (int64_t)gridDim.x * RPI : RPI;  // row order: as in bn_stats_kernel
   const int64_t rb = il ? (int64_t)blockIdx.x * RPI : (int64_t)blockIdx.x * rows_per_block;
   const int64_t re = il ? M : min(M, rb + rows_per_block);
@@ -367,15 +442,37 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
       sf[v] = MASK == 2 ? p.shift[c0 + v] : 0.f;
     }
     int64_t r = rb + rr;
+    const int cv = C / V;
+    // ReLU mask operand o[v] (0 / 1 bits for MASK 3, y for MASK 1)
+    auto load_mask = [&](int64_t row, int64_t off, float (&o)[V]) {
+      if constexpr (MASK == 1) {
+        VecIO<T>::load(y + off, o);
+      } else if constexpr (MASK == 3) {
+        const unsigned b = mk[row * cv + c0 / V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) o[v] = (float)((b >> v) & 1u);
+      }
+    };
+    auto finish = [&](float (&g)[V], const float (&a)[V], const float (&o)[V], int64_t off) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float gg = masked_dy<MASK, V>(g[v], a[v], (MASK == 1 || MASK == 3) ? o[v] : 0.f, sc[v], sf[v]);
+        if constexpr (GOUT) gg = round_to<T>(gg);
+        g[v] = gg;
+        acc[0][v] += gg;
+        acc[1][v] = fmaf(gg, a[v] - mu[v], acc[1][v]);
+      }
+      if constexpr (GOUT) VecIO<T>::store(gout + off, g);
+    };
     for (; r + (U - 1) * rs < re; r += U * rs) {
       float g[U][V], a[U][V], o[U][V], g2[ADD2 ? U : 1][V];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int64_t off = (r + u * rs) * C + c0;
+        const int64_t off = row(r + u * rs) * C + c0;
         VecIO<T>::load(dy + off, g[u]);
         if constexpr (ADD2) VecIO<T>::load(dy2 + off, g2[u]);
         VecIO<T>::load(x + off, a[u]);
-        if constexpr (MASK == 1) VecIO<T>::load(y + off, o[u]);
+        load_mask(row(r + u * rs), off, o[u]);
       }
       if constexpr (ADD2) {
 #pragma unroll
@@ -384,17 +481,11 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
           for (int v = 0; v < V; ++v) g[u][v] += g2[u][v];
       }
 #pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-          const float gg = masked_dy<MASK, V>(g[u][v], a[u][v], MASK == 1 ? o[u][v] : 0.f, sc[v], sf[v]);
-          acc[0][v] += gg;
-          acc[1][v] = fmaf(gg, a[u][v] - mu[v], acc[1][v]);
-        }
+      for (int u = 0; u < U; ++u) finish(g[u], a[u], o[u], row(r + u * rs) * C + c0);
     }
     for (; r < re; r += rs) {
       float g[V], a[V], o[V];
-      const int64_t off = r * C + c0;
+      const int64_t off = row(r) * C + c0;
       VecIO<T>::load(dy + off, g);
       if constexpr (ADD2) {
         float g2[V];
@@ -403,13 +494,8 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
         for (int v = 0; v < V; ++v) g[v] += g2[v];
       }
       VecIO<T>::load(x + off, a);
-      if constexpr (MASK == 1) VecIO<T>::load(y + off, o);
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        const float gg = masked_dy<MASK, V>(g[v], a[v], MASK == 1 ? o[v] : 0.f, sc[v], sf[v]);
-        acc[0][v] += gg;
-        acc[1][v] = fmaf(gg, a[v] - mu[v], acc[1][v]);
-      }
+      load_mask(row(r), off, o);
+      finish(g, a, o, off);
     }
   }
   float part[2];
@@ -436,12 +522,51 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
   if (tid == 0) rearm(tickets + blockIdx.y);
 }
 
-template <typename T, int MASK, bool RES, bool ADD2>
+// dx = A g + B x + C from the reduce pass's materialised g (GOUT): 2 reads + 1 write
+template <typename T, int AU = 1>
+__global__ void __launch_bounds__(kThreads) bn_bwd_apply_g_kernel(const T* __restrict__ g, const T* __restrict__ x,
+                                                                  T* __restrict__ dx, BnBwdParams p, int64_t nvec,
+                                                                  int C, int rev) {
+  constexpr int V = VecIO<T>::V;
+  extern __shared__ float sh[];  // A[C], B[C], C[C]
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    sh[c] = p.coef_a[c];
+    sh[C + c] = p.coef_b[c];
+    sh[2 * C + c] = p.coef_c[c];
+  }
+  __syncthreads();
+  const int cv = C / V;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  auto vid = [&](int64_t i) { return rev ? nvec - 1 - i : i; };  // rev: last vector first
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nvec; i0 += AU * stride) {
+    float gg[AU][V], a[AU][V];
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      const int64_t i = vid(i0 + u * stride);
+      if (i0 + u * stride < nvec) {
+        VecIO<T>::load(g + i * V, gg[u]);
+        VecIO<T>::load(x + i * V, a[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+      if (i0 + u * stride >= nvec) break;
+      const int64_t i = vid(i0 + u * stride);
+      const int c0 = (int)(i % cv) * V;
+#pragma unroll
+      for (int v = 0; v < V; ++v)
+        a[u][v] = fmaf(sh[c0 + v], gg[u][v], fmaf(sh[C + c0 + v], a[u][v], sh[2 * C + c0 + v]));
+      VecIO<T>::store(dx + i * V, a[u]);
+    }
+  }
+}
+
+template <typename T, int MASK, bool RES, bool ADD2, int AU = 1>
 __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const T* __restrict__ dy, const T* __restrict__ dy2,
                                                                 const T* __restrict__ x,
                                                                 const T* __restrict__ y, T* __restrict__ dx,
                                                                 T* __restrict__ dres, BnBwdParams p, int64_t nvec,
-                                                                int C) {
+                                                                int C, int rev) {
   constexpr int V = VecIO<T>::V;
   extern __shared__ float sh[];  // A[C], B[C], C[C] (+ scale[C], shift[C] for MASK 2)
   for (int c = threadIdx.x; c < C; c += blockDim.x) {
@@ -456,33 +581,66 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const T* __restr
   __syncthreads();
   const int cv = C / V;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nvec; i += stride) {
-    const int c0 = (int)(i % cv) * V;
-    float g[V], a[V], o[V];
-    VecIO<T>::load(dy + i * V, g);
-    if constexpr (ADD2) {
-      float g2[V];
-      VecIO<T>::load(dy2 + i * V, g2);
+  auto vid = [&](int64_t i) { return rev ? nvec - 1 - i : i; };  // rev: last vector first
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < nvec; i0 += AU * stride) {
+    float g[AU][V], a[AU][V], o[AU][V], g2[ADD2 ? AU : 1][V];
 #pragma unroll
-      for (int v = 0; v < V; ++v) g[v] += g2[v];
+    for (int u = 0; u < AU; ++u) {
+      const int64_t i = vid(i0 + u * stride);
+      if (i0 + u * stride < nvec) {
+        VecIO<T>::load(dy + i * V, g[u]);
+        if constexpr (ADD2) VecIO<T>::load(dy2 + i * V, g2[u]);
+        VecIO<T>::load(x + i * V, a[u]);
+        if constexpr (MASK == 1) VecIO<T>::load(y + i * V, o[u]);
+      }
     }
-    VecIO<T>::load(x + i * V, a);
-    if constexpr (MASK == 1) VecIO<T>::load(y + i * V, o);
 #pragma unroll
-    for (int v = 0; v < V; ++v) {
-      g[v] = masked_dy<MASK, V>(g[v], a[v], MASK == 1 ? o[v] : 0.f, MASK == 2 ? sh[3 * C + c0 + v] : 0.f,
+    for (int u = 0; u < AU; ++u) {
+      if (i0 + u * stride >= nvec) break;
+      const int64_t i = vid(i0 + u * stride);
+      const int c0 = (int)(i % cv) * V;
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        float gv = g[u][v];
+        if constexpr (ADD2) gv += g2[u][v];
+        gv = masked_dy<MASK, V>(gv, a[u][v], MASK == 1 ? o[u][v] : 0.f, MASK == 2 ? sh[3 * C + c0 + v] : 0.f,
                                 MASK == 2 ? sh[4 * C + c0 + v] : 0.f);
-      a[v] = fmaf(sh[c0 + v], g[v], fmaf(sh[C + c0 + v], a[v], sh[2 * C + c0 + v]));
+        g[u][v] = gv;
+        a[u][v] = fmaf(sh[c0 + v], gv, fmaf(sh[C + c0 + v], a[u][v], sh[2 * C + c0 + v]));
+      }
+      VecIO<T>::store(dx + i * V, a[u]);
+      if constexpr (RES) VecIO<T>::store(dres + i * V, g[u]);
     }
-    VecIO<T>::store(dx + i * V, a);
-    if constexpr (RES) VecIO<T>::store(dres + i * V, g);
   }
 }
 
 int apply_grid(int64_t nvec) {
-  int64_t b = (nvec + kThreads * 4 - 1) / (kThreads * 4);  // >= 4 vectors per thread
-  if (b > 4096) b = 4096;
+  const int au = apply_unroll(), cap = apply_block_cap();
+  int64_t per = (int64_t)kThreads * (cap > 0 ? 4 : au);  // >= 4 vectors per thread when capped
+  int64_t b = (nvec + per - 1) / per;
+  if (cap > 0 && b > cap) b = cap;
   return (int)(b < 1 ? 1 : b);
+}
+
+// Sweep direction of each pass (PTDT_BN_DIR bits: 1 stats, 2 forward apply, 4 backward reduce,
+// 8 backward apply; set = last row first). Consecutive passes over one tensor in opposite
+// directions re-read the most recently touched lines first, which the 256 MiB Infinity Cache
+// still holds (MI355X_MICROARCH.md "Infinity Cache").
+int pass_dirs() {
+  static const int v = env_int("PTDT_BN_DIR", 0);
+  return v;
+}
+int dir(int bit) { return (pass_dirs() & bit) ? 1 : 0; }
+
+// runtime AU -> template
+template <typename F>
+hipError_t with_au(F&& f) {
+  switch (apply_unroll()) {
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    default: f(std::integral_constant<int, 1>{}); break;
+  }
+  return hipGetLastError();
 }
 
 template <typename T>
@@ -492,7 +650,7 @@ hipError_t fwd_impl(const BnFwdArgs& a, hipStream_t s) {
   const Geom g = geom<T>(a.M, a.C);
   const size_t sh_red = (size_t)2 * kRed * V * sizeof(float) + 16;
   hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(g.gx, g.gy), dim3(kRed), sh_red, s, static_cast<const T*>(a.x),
-                     a.M, a.C, g.TC, g.RPI, g.rows_per_block, interleave_rows(), a.workspace, a.tickets, a.p);
+                     a.M, a.C, g.TC, g.RPI, g.rows_per_block, interleave_rows() | (dir(1) << 1), a.workspace, a.tickets, a.p);
   PTDT_HIP_CHECK(hipGetLastError());
   const int64_t nvec = a.M * a.C / V;
   const size_t sh_ap = (size_t)2 * a.C * sizeof(float);
@@ -500,14 +658,20 @@ hipError_t fwd_impl(const BnFwdArgs& a, hipStream_t s) {
   const T* r = static_cast<const T*>(a.residual);
   T* y = static_cast<T*>(a.y);
   const dim3 grid(apply_grid(nvec)), blk(kThreads);
-  if (a.relu) {
-    if (r) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), grid, blk, sh_ap, s, x, r, y, a.p.scale, a.p.shift, nvec, a.C);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), grid, blk, sh_ap, s, x, r, y, a.p.scale, a.p.shift, nvec, a.C);
-  } else {
-    if (r) hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), grid, blk, sh_ap, s, x, r, y, a.p.scale, a.p.shift, nvec, a.C);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), grid, blk, sh_ap, s, x, r, y, a.p.scale, a.p.shift, nvec, a.C);
-  }
-  return hipGetLastError();
+  const float *sc = a.p.scale, *sf = a.p.shift;
+  uint8_t* mo = a.mask_out;
+  const int C = a.C;
+  return with_au([&](auto au) {
+    constexpr int AU = decltype(au)::value;
+    if (a.relu) {
+      if (r && mo) hipLaunchKernelGGL((bn_apply_kernel<T, true, true, true, AU>), grid, blk, sh_ap, s, x, r, y, sc, sf, nvec, C, dir(2), mo);
+      else if (r) hipLaunchKernelGGL((bn_apply_kernel<T, true, true, false, AU>), grid, blk, sh_ap, s, x, r, y, sc, sf, nvec, C, dir(2), nullptr);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, true, false, false, AU>), grid, blk, sh_ap, s, x, r, y, sc, sf, nvec, C, dir(2), nullptr);
+    } else {
+      if (r) hipLaunchKernelGGL((bn_apply_kernel<T, false, true, false, AU>), grid, blk, sh_ap, s, x, r, y, sc, sf, nvec, C, dir(2), nullptr);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, false, false, false, AU>), grid, blk, sh_ap, s, x, r, y, sc, sf, nvec, C, dir(2), nullptr);
+    }
+  });
 }
 
 template <typename T>
@@ -521,14 +685,16 @@ hipError_t apply_impl(const void* x, const void* res, void* y, const float* scal
   const T* r = static_cast<const T*>(res);
   T* yy = static_cast<T*>(y);
   const dim3 grid(apply_grid(nvec)), blk(kThreads);
-  if (relu) {
-    if (r) hipLaunchKernelGGL((bn_apply_kernel<T, true, true>), grid, blk, sh_ap, s, xx, r, yy, scale, shift, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, true, false>), grid, blk, sh_ap, s, xx, r, yy, scale, shift, nvec, C);
-  } else {
-    if (r) hipLaunchKernelGGL((bn_apply_kernel<T, false, true>), grid, blk, sh_ap, s, xx, r, yy, scale, shift, nvec, C);
-    else hipLaunchKernelGGL((bn_apply_kernel<T, false, false>), grid, blk, sh_ap, s, xx, r, yy, scale, shift, nvec, C);
-  }
-  return hipGetLastError();
+  return with_au([&](auto au) {
+    constexpr int AU = decltype(au)::value;
+    if (relu) {
+      if (r) hipLaunchKernelGGL((bn_apply_kernel<T, true, true, false, AU>), grid, blk, sh_ap, s, xx, r, yy, scale, shift, nvec, C, 0, nullptr);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, true, false, false, AU>), grid, blk, sh_ap, s, xx, r, yy, scale, shift, nvec, C, 0, nullptr);
+    } else {
+      if (r) hipLaunchKernelGGL((bn_apply_kernel<T, false, true, false, AU>), grid, blk, sh_ap, s, xx, r, yy, scale, shift, nvec, C, 0, nullptr);
+      else hipLaunchKernelGGL((bn_apply_kernel<T, false, false, false, AU>), grid, blk, sh_ap, s, xx, r, yy, scale, shift, nvec, C, 0, nullptr);
+    }
+  });
 }
 
 template <typename T, int MASK, bool ADD2>
@@ -539,21 +705,33 @@ hipError_t bwd_launch(const BnBwdArgs& a, const Geom& g, hipStream_t s) {
   const T* dy2 = static_cast<const T*>(a.dy2);
   const T* x = static_cast<const T*>(a.x);
   const T* y = static_cast<const T*>(a.y);
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK, ADD2>), dim3(g.gx, g.gy), dim3(kRed), sh_red, s, dy, dy2, x, y,
-                     a.M, a.C, g.TC, g.RPI, g.rows_per_block, interleave_rows(), a.workspace, a.tickets, a.p);
-  PTDT_HIP_CHECK(hipGetLastError());
   const int64_t nvec = a.M * a.C / V;
-  const size_t sh_ap = (size_t)(MASK == 2 ? 5 : 3) * a.C * sizeof(float);
   T* dx = static_cast<T*>(a.dx);
   T* dr = static_cast<T*>(a.dres);
   const dim3 grid(apply_grid(nvec)), blk(kThreads);
-  if (dr)
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, MASK, true, ADD2>), grid, blk, sh_ap, s, dy, dy2, x, y, dx, dr, a.p,
-                       nvec, a.C);
-  else
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, MASK, false, ADD2>), grid, blk, sh_ap, s, dy, dy2, x, y, dx, dr, a.p,
-                       nvec, a.C);
-  return hipGetLastError();
+  if (dr) {  // the residual gradient is wanted: the reduce pass writes g there, the apply reads g and x
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK, ADD2, true>), dim3(g.gx, g.gy), dim3(kRed), sh_red, s, dy, dy2,
+                       x, y, a.mask, dr, a.M, a.C, g.TC, g.RPI, g.rows_per_block, interleave_rows() | (dir(4) << 1), a.workspace,
+                       a.tickets, a.p);
+    PTDT_HIP_CHECK(hipGetLastError());
+    return with_au([&](auto au) {
+      hipLaunchKernelGGL((bn_bwd_apply_g_kernel<T, decltype(au)::value>), grid, blk, (size_t)3 * a.C * sizeof(float),
+                         s, static_cast<const T*>(dr), x, dx, a.p, nvec, a.C, dir(8));
+    });
+  }
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK, ADD2>), dim3(g.gx, g.gy), dim3(kRed), sh_red, s, dy, dy2, x, y,
+                     a.mask, nullptr, a.M, a.C, g.TC, g.RPI, g.rows_per_block, interleave_rows() | (dir(4) << 1), a.workspace,
+                     a.tickets, a.p);
+  PTDT_HIP_CHECK(hipGetLastError());
+  if constexpr (MASK == 3) {
+    return hipErrorInvalidValue;  // bit masks come with a residual (RES): the g path above
+  } else {
+    const size_t sh_ap = (size_t)(MASK == 2 ? 5 : 3) * a.C * sizeof(float);
+    return with_au([&](auto au) {
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, MASK, false, ADD2, decltype(au)::value>), grid, blk, sh_ap, s, dy,
+                         dy2, x, y, dx, dr, a.p, nvec, a.C, dir(8));
+    });
+  }
 }
 
 template <typename T, int MASK>
@@ -567,6 +745,10 @@ hipError_t bwd_impl(const BnBwdArgs& a, hipStream_t s) {
   if (a.C % V != 0) return hipErrorInvalidValue;
   const Geom g = geom<T>(a.M, a.C);
   if (!a.relu) return bwd_launch2<T, 0>(a, g, s);
+  if (a.mask != nullptr) {
+    if (a.dres == nullptr) return hipErrorInvalidValue;
+    return bwd_launch2<T, 3>(a, g, s);
+  }
   if (a.y != nullptr) return bwd_launch2<T, 1>(a, g, s);
   if (a.p.scale == nullptr || a.p.shift == nullptr) return hipErrorInvalidValue;
   return bwd_launch2<T, 2>(a, g, s);
@@ -580,8 +762,8 @@ int64_t bn_workspace_floats(int64_t M, int C, int dtype) {
 }
 int bn_num_tickets(int C, int dtype) {
   const int V = dtype == kF32 ? 4 : 8;
-  const int cv = C / V;
-  const int TC = cv < kMaxTC ? cv : kMaxTC;
+  const int cv = C / V, mt = min_tc();
+  const int TC = cv < mt ? cv : mt;
   return (cv + TC - 1) / TC;
 }
 

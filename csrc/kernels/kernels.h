@@ -323,6 +323,7 @@ struct BnFwdArgs {
   int dtype; int64_t M; int C; int relu;
   float* workspace; int* tickets;
   BnParams p;
+  uint8_t* mask_out;  // relu + residual: the ReLU mask, one byte per 16-B vector (bit v: y > 0), or null
 };
 struct BnBwdParams {
   const float* weight; const float* mean; const float* invstd;
@@ -337,6 +338,7 @@ struct BnBwdArgs {
   int dtype; int64_t M; int C; int relu;
   float* workspace; int* tickets;
   BnBwdParams p;
+  const uint8_t* mask;  // the forward's mask_out (instead of y; needs dres), or null
 };
 int64_t bn_workspace_floats(int64_t M, int C, int dtype);
 int bn_num_tickets(int C, int dtype);

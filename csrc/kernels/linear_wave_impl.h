@@ -301,6 +301,87 @@ __device__ __forceinline__ bool ll_exchange_u(bool push, uint64_t PTDT_GLOBAL* p
                                  err, max_polls);
 }
 
+// Packed LL exchange for layout F (tools/exchange_bench.hip variant 6): the rank's npw
+// values (DOUT*Din weights + the biases) are staged in LDS and travel as npw CONSECUTIVE
+// words per peer -- lane f of the NT store / poll instructions handles (peer f / npw, word
+// f % npw), so every peer's words go out in ~2 cache lines and all peers' stores and polls
+// are in flight together. ll_exchange instead stores each lane's KP-value chunk to its row
+// slot's peer (6 store instructions hitting the same 1-2 lines per peer for Linear(20,1)):
+// uncached stores cost per transaction, and the exchange measured ~30 % longer at W = 2 and
+// ~2x at W = 8 (profiles/r3_exchange_bench.jsonl). After the polls, every lane sums ITS
+// chunk's words over the ranks in rank order from LDS: the same bits on every rank, and
+// the same order as the standalone xgmi_allreduce_avg kernel.
+// PackPlan: per-lane (peer, word) of the NT instructions, computed once per launch.
+template <int NT>
+struct PackPlan {
+  int pr[NT], wd[NT];  // peer rank (-1: idle lane), word index
+};
+template <int NT>
+__device__ __forceinline__ PackPlan<NT> pack_plan(int npw, int world, int my_rank, int lane) {
+  PackPlan<NT> pp;
+  const int nf = npw * (world - 1);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    const int f = lane + 64 * t;
+    const int pi = f / npw;
+    pp.wd[t] = f - pi * npw;
+    pp.pr[t] = f < nf ? (pi < my_rank ? pi : pi + 1) : -1;
+  }
+  return pp;
+}
+// stg: LDS [npw] (own values, written by the caller), pol: LDS [world][npw]. Returns false
+// after a poll timeout (sets *err). drop: fault injection -- pushes to the peers are skipped.
+template <int NT>
+__device__ __forceinline__ bool ll_exchange_packed(const PackPlan<NT>& pp, const XgmiArgs& x, uint32_t seq, int npw,
+                                                   const float* stg, float* pol, int lane, bool drop) {
+  const int parity = (int)(seq & 1u);
+  const uint64_t hi = (uint64_t)seq << 32;
+  if (!drop) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      if (pp.pr[t] < 0) continue;
+      uint64_t PTDT_GLOBAL* base = nullptr;  // peers[] selected with uniform compares (no scratch copy)
+#pragma unroll
+      for (int r = 0; r < kXgmiMaxRanks; ++r)
+        if (pp.pr[t] == r) base = (uint64_t PTDT_GLOBAL*)x.peers[r];
+      __hip_atomic_store(base + (int64_t)(parity * x.world + x.rank) * x.max_elems + pp.wd[t],
+                         hi | __float_as_uint(stg[pp.wd[t]]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+  const uint64_t PTDT_GLOBAL* const local = (const uint64_t PTDT_GLOBAL*)x.local;
+  const int alt = x.rank + 1 == x.world ? 0 : x.rank + 1;  // idle lanes re-read a real slot
+  uint64_t w[NT];
+  auto issue = [&]() {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const bool on = pp.pr[t] >= 0;
+      w[t] = __hip_atomic_load(local + (int64_t)(parity * x.world + (on ? pp.pr[t] : alt)) * x.max_elems +
+                                   (on ? pp.wd[t] : 0),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  };
+  issue();
+  bool ok = true;
+  for (uint32_t polls = 0;; ++polls) {
+    bool m = false;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) m |= pp.pr[t] >= 0 && (uint32_t)(w[t] >> 32) != seq;
+    if (__builtin_amdgcn_ballot_w64(m) == 0) break;
+    if (polls >= x.max_polls) {  // a peer is gone: fail loudly, never hang
+      __hip_atomic_store((int PTDT_GLOBAL*)x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      ok = false;
+      break;
+    }
+    issue();
+  }
+#pragma unroll
+  for (int t = 0; t < NT; ++t)
+    if (pp.pr[t] >= 0) pol[pp.pr[t] * npw + pp.wd[t]] = __uint_as_float((uint32_t)w[t]);
+  for (int f = lane; f < npw; f += 64) pol[x.rank * npw + f] = stg[f];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops complete in order
+  return ok;
+}
+
 template <int R, int KP, int DOUT, int RY>
 struct Batch {
   float x[R][KP];
@@ -1134,7 +1215,8 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
 #pragma unroll
         for (int k = 0; k < KP; ++k) v[c][k] = i == my_rank ? gW[c][k] : 0.f;
       }
-      // (ll_exchange_u / a separate pusher or poller wave measured no faster: tools/exchange_bench.hip)
+      // (ll_exchange_u / ll_exchange_packed / a separate pusher or poller wave measured no faster at
+      //  W = 8: tools/exchange_bench.hip, profiles/r3_exchange_bench*.jsonl)
       const bool ok = ll_exchange<KP, DOUT>(i < world && i != my_rank, push_dst, poll_src, my_rank, i, world,
                                             max_elems, seq, k0, Din, hb, q == 0, 4 * KP != Din, gW, gb, v, vb,
                                             ar.err, ar.max_polls, ar.drop_push != 0u && seq >= ar.drop_push);

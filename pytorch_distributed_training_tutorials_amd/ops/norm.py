@@ -10,6 +10,9 @@ run on csrc/kernels/batchnorm.hip: statistics and the normalise / residual /
 ReLU epilogue in two launches, the ReLU mask, both parameter gradients, the
 input gradient and the residual gradient in two more -- instead of MIOpen's BN
 kernels plus separate clamp, add, threshold-backward and tensor-op passes.
+With a residual, the forward also writes the ReLU mask as bits (1/16 of the
+activation in bf16) and the backward's reduce pass writes the masked gradient
+(the residual gradient itself), so its apply pass reads that and x only.
 Eval mode applies the running statistics in one launch. Anything else (NCHW,
 CPU, momentum=None, odd channel counts) uses PyTorch's batch_norm with the same
 semantics. Parameters, buffers and state_dict keys are nn.BatchNorm2d's.
@@ -64,24 +67,27 @@ class _BatchNormActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, relu: bool, momentum: float,
                 eps: float, tickets, link_in, link_out):
-        y, stats = native().bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, residual, relu, momentum,
-                                         eps, tickets)
+        # with a residual the ReLU mask travels as bits (one byte per 16-B vector, 1/16 of y in
+        # bf16); without one it is recomputed from x and the saved scale/shift (bit-exact)
+        want_mask = relu and residual is not None
+        y, stats, mask = native().bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, residual, relu,
+                                               momentum, eps, tickets, want_mask)
         ctx.tickets = tickets
         ctx.params = (weight, bias)
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.link_in, ctx.link_out = link_in, link_out
-        # ReLU mask in the backward: from y with a residual; without one it is recomputed
-        # from x and the saved scale/shift (bit-exact), so y need not be read (or kept)
-        ctx.save_for_backward(x, y if (relu and residual is not None) else None, weight, stats)
+        ctx.save_for_backward(x, mask if want_mask else None, weight, stats)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, stats = ctx.saved_tensors
+        x, mask, weight, stats = ctx.saved_tensors
         want_dw = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
         link_in, link_out = ctx.link_in, ctx.link_out
-        want_dres = ctx.has_res and (ctx.needs_input_grad[3] or link_in is not None)
+        # a bit mask is read by the backward's materialised-gradient path, which writes the
+        # residual gradient: request it whenever the mask exists
+        want_dres = ctx.has_res and (ctx.needs_input_grad[3] or link_in is not None or mask is not None)
         dy = _like(dy, x)
         dy2 = None
         if link_out is not None:  # a later block's residual gradient of our output
@@ -94,13 +100,12 @@ class _BatchNormActFn(torch.autograd.Function):
             for k, p in enumerate(ctx.params):
                 if p is not None and p.grad is None and getattr(p, "_ptdt_grad_sink", None) is not None:
                     sinks[k] = p._ptdt_grad_sink()
-        dx, dw, db, dres = native().bn_bwd(dy, x, y, weight, stats, ctx.relu, want_dres, want_dw,
-                                           ctx.tickets, sinks[0], sinks[1], dy2)
+        dx, dw, db, dres = native().bn_bwd(dy, x, None, weight, stats, ctx.relu, want_dres, want_dw,
+                                           ctx.tickets, sinks[0], sinks[1], dy2, mask)
         if link_in is not None:  # delivered to the residual's producer instead of autograd
             link_in.dres, dres = dres, None
         return (dx if ctx.needs_input_grad[0] else None, dw if want_dw else None, db if want_dw else None,
-                dres if ctx.has_res and ctx.needs_input_grad[3] else None, None, None, None, None, None, None, None,
-                None, None)
+                dres if (dres is not None and ctx.needs_input_grad[3]) else None, *([None] * 9))
 
 
 def _tickets_of(bn, x):

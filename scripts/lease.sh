@@ -101,6 +101,16 @@ for s in "$@"; do
                pmc tp2 "$P2" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side ;;
     pmc_wave)  pmc wave1 "$P1" python3 bench.py --steps 20000 --warmup 1 --no_mlp_side
                pmc wave2 "$P2" python3 bench.py --steps 20000 --warmup 1 --no_mlp_side ;;
+    bnsweep)   # BN kernel geometry / sweep-direction sweep (benchmarks/bn_kernel_bench.py), one process per setting
+               for cfg in ${BNCFGS:-"PTDT_BN_DIR=0" "PTDT_BN_DIR=10" "PTDT_BN_DIR=5" "PTDT_BN_DIR=2" "PTDT_BN_DIR=8" "PTDT_BN_TC=8"}; do
+                 jstep bnk 120 env $cfg python3 benchmarks/bn_kernel_bench.py
+               done ;;
+    resdir)    # ResNet-50 DDP step under each BN sweep-direction setting
+               for d in ${BNDIRS:-0 10 5}; do
+                 jstep resnet_dir 600 env PTDT_BN_DIR=$d python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5
+               done ;;
+    bntest)    # BN numerics under non-default geometry
+               tstep pytest_bn 300 env PTDT_BN_DIR=15 PTDT_BN_AU=4 PTDT_BN_APPLY_BLOCKS=0 $PYTEST tests/test_norm.py ;;
     run:*)     step "run" 600 bash -c "${s#run:}" ;;  # ad-hoc: run:'python3 benchmarks/x.py'
     *)         echo "unknown stage $s"; exit 2 ;;
   esac

@@ -10,7 +10,9 @@
 // stores in order on gfx9), 3 = a second wave polls and sums (every rank self-pushes) and
 // hands the sum back through LDS, so the training wave never waits for a poll round trip
 // after its stores, 4 = the rank's 21 values as 21 consecutive words (one store and one poll
-// instruction per peer, LDS redistribution), 5 = one word per peer (the protocol's floor).
+// instruction per peer, LDS redistribution; peers polled one after another), 5 = one word per
+// peer (the protocol's floor), 6 = packed as 4 with every peer's stores and polls in flight
+// together (lane f: peer f / 21, word f % 21) and the rank-order sums read from LDS.
 // Prints cycles (s_memtime) per iteration and checks that every rank ends with identical weights.
 // Build: hipcc --offload-arch=gfx950 -O3 -fno-slp-vectorize -Icsrc tools/exchange_bench.hip -o tools/bin/exchange_bench
 #include <hip/hip_runtime.h>
@@ -36,7 +38,7 @@ constexpr int KP = 5, DOUT = 1, DIN = 20;
 template <int VARIANT>
 __global__ void __launch_bounds__(128) k_exchange(uint64_t* buf, int world, int max_elems, int iters, int work,
                                                   int* err, long long* cycles, float* out) {
-  __shared__ float hand[2][64 * (KP + 1)];  // per-parity chunk / sum hand-over between the two waves
+  __shared__ float hand[2][64 * (KP + 1)];  // per-parity hand-over / staging (variants 2-6)
   const int rank = blockIdx.x;
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = threadIdx.x & 63, q = lane >> 4, i = lane & 15, k0 = q * KP;
@@ -48,7 +50,7 @@ __global__ void __launch_bounds__(128) k_exchange(uint64_t* buf, int world, int 
     if (i == r && r < world) push_dst = (uint64_t PTDT_GLOBAL*)(buf + r * region);
   const float inv_w = 1.f / (float)world;
   if (wave == 1) {  // helper wave of variants 2 / 3
-    if (VARIANT < 2 || VARIANT > 3 || world == 1) return;
+    if (VARIANT < 2 || VARIANT > 3 || world == 1) return;  // (4-6: single wave)
     const float zero[1][KP] = {}, zb[1] = {};
     for (uint32_t seq = 1; seq <= (uint32_t)iters; ++seq) {
       float* h = hand[seq & 1];
@@ -111,7 +113,75 @@ __global__ void __launch_bounds__(128) k_exchange(uint64_t* buf, int world, int 
         ok = lw::ll_poll_chunk<KP, DOUT>(local, rank, i, world, max_elems, seq, k0, DIN, true, false, gW, gb, v, vb,
                                          err, 1u << 20);
       }
-      if constexpr (VARIANT == 4 || VARIANT == 5) {
+      if constexpr (VARIANT == 6) {
+        // packed, every peer in parallel: the rank's 21 values are staged in LDS, lane f of the
+        // push/poll instructions handles (peer f / 21, word f % 21) -- 21 consecutive words per
+        // peer, all peers' stores and polls in flight together -- and each lane then sums its
+        // chunk's 6 words over the ranks (rank order) from LDS
+        constexpr int NPW = 21;
+        const int parity = (int)(seq & 1u);
+        const uint64_t hi = (uint64_t)seq << 32;
+        float* stg = hand[seq & 1];                 // [21] own values
+        float* pol = hand[seq & 1] + 32;            // [world][21] every rank's values (rank order)
+        if (i == 0) {
+#pragma unroll
+          for (int k = 0; k < KP; ++k) stg[q * KP + k] = gW[0][k];
+          if (q == 0) stg[20] = gb[0];
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const int npeer = world - 1;
+        const int nf = NPW * npeer;                 // <= 147 for world 8: 3 instructions
+        float own[3];
+        int pr[3], wd[3];
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const int f = lane + 64 * t;
+          const int pi = f / NPW;
+          wd[t] = f - pi * NPW;
+          pr[t] = f < nf ? (pi < rank ? pi : pi + 1) : -1;
+          own[t] = stg[wd[t]];
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+          if (pr[t] >= 0) {
+            uint64_t PTDT_GLOBAL* dst =
+                (uint64_t PTDT_GLOBAL*)(buf + pr[t] * region) + (int64_t)(parity * world + rank) * max_elems + wd[t];
+            __hip_atomic_store(dst, hi | __float_as_uint(own[t]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        uint64_t w[3];
+        auto issue = [&]() {
+#pragma unroll
+          for (int t = 0; t < 3; ++t) {
+            const int src = pr[t] >= 0 ? pr[t] : (rank + 1 == world ? 0 : rank + 1);
+            w[t] = __hip_atomic_load(local + (int64_t)(parity * world + src) * max_elems + (pr[t] >= 0 ? wd[t] : 0),
+                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        };
+        issue();
+        for (uint32_t n = 0; n < (1u << 20); ++n) {
+          bool m = false;
+#pragma unroll
+          for (int t = 0; t < 3; ++t) m |= pr[t] >= 0 && (uint32_t)(w[t] >> 32) != seq;
+          if (__builtin_amdgcn_ballot_w64(m) == 0) break;
+          issue();
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+          if (pr[t] >= 0) pol[pr[t] * NPW + wd[t]] = __uint_as_float((uint32_t)w[t]);
+        if (lane < NPW) pol[rank * NPW + lane] = stg[lane];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        float sw[KP], sb = 0.f;
+#pragma unroll
+        for (int k = 0; k < KP; ++k) sw[k] = 0.f;
+        for (int p = 0; p < world; ++p) {  // rank order: identical bits on every rank
+#pragma unroll
+          for (int k = 0; k < KP; ++k) sw[k] += pol[p * NPW + q * KP + k];
+          sb += pol[p * NPW + 20];
+        }
+#pragma unroll
+        for (int k = 0; k < KP; ++k) gW[0][k] = sw[k] * inv_w;
+        gb[0] = sb * inv_w;
+      } else if constexpr (VARIANT == 4 || VARIANT == 5) {
         // 4: the rank's 21 values (20 weights + bias) travel as 21 consecutive LL words: ONE store
         //    instruction per peer (lanes 0..20) and ONE poll load per peer, redistributed through LDS;
         // 5: a single word per peer (the protocol's floor; the "gradient" is lane 0's value only)
@@ -221,6 +291,7 @@ int main() {
       if (run<3>(buf, world, max_elems, iters, work, err, cyc, out)) return 1;
       if (run<4>(buf, world, max_elems, iters, work, err, cyc, out)) return 1;
       if (run<5>(buf, world, max_elems, iters, work, err, cyc, out)) return 1;
+      if (run<6>(buf, world, max_elems, iters, work, err, cyc, out)) return 1;
     }
   }
   return 0;
