@@ -39,6 +39,9 @@ def main(argv=None):
                     help="native DDP reducer + fused optimizer, or stock torch DDP + torch.optim.SGD (comparator)")
     ap.add_argument("--no_shadow", action="store_true",
                     help="cast the fp32 weights in every forward instead of using FusedSGD's bf16 shadows")
+    ap.add_argument("--tag", default=None, help="free-form label copied into the JSON line")
+    ap.add_argument("--no_graph", action="store_true",
+                    help="native impl: launch every step eagerly instead of replaying one captured hipGraph per step")
     ap.add_argument("--no_cudnn_benchmark", action="store_true",
                     help="keep MIOpen's heuristic solver choice (default: exhaustive find per conv shape)")
     a = ap.parse_args(argv)
@@ -75,19 +78,25 @@ def main(argv=None):
         x = x.contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (a.batch_size,), device=dev)
     amp = a.dtype == "bf16"
+    graphed = a.impl == "native" and not a.no_graph
 
     def step():
         if a.impl == "native":
             ddp.zero_grad()
         else:
             opt.zero_grad()
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+        # no autocast weight cache under capture (the cast kernels must be in the graph)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp, cache_enabled=not graphed):
             out = ddp(x)
         loss = cross_entropy(out.float(), y)
         loss.backward()
         opt.step()
         return loss
 
+    if graphed:  # utils/graphs.py: eager warm-up steps on a side stream, then one hipGraph per step
+        from pytorch_distributed_training_tutorials_amd.utils.graphs import GraphedStep
+
+        step = GraphedStep(step, dev, comm=comm, warmup=max(3, a.warmup))
     for _ in range(a.warmup):
         step()
     comm.barrier()
@@ -109,9 +118,9 @@ def main(argv=None):
             "dtype": a.dtype, "data": "synthetic ImageNet-shaped (generated on device)",
             "config": {"model": "resnet50", "per_device_batch": a.batch_size, "image": a.image,
                        "parallelism": f"dp{world}", "channels_last": not a.no_channels_last},
-            "impl": a.impl, "bn_dir": os.environ.get("PTDT_BN_DIR", "0"), "miopen_find": "exhaustive (cudnn.benchmark)" if torch.backends.cudnn.benchmark else "heuristic",
+            "impl": a.impl, "hipgraph": graphed, "bn_dir": os.environ.get("PTDT_BN_DIR", "0"), "miopen_find": "exhaustive (cudnn.benchmark)" if torch.backends.cudnn.benchmark else "heuristic",
             "buckets_MB": [round(b / 2 ** 20, 2) for b in ddp.bucket_sizes_bytes()] if a.impl == "native" else None,
-            "final_loss": float(loss.detach()),
+            "final_loss": float(loss.detach()), **({"tag": a.tag} if a.tag else {}),
         }), flush=True)
     env.destroy_process_group()
 

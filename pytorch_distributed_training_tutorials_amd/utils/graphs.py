@@ -1,0 +1,76 @@
+"""Whole-step hipGraph capture for eager training loops.
+
+A ResNet-50 DDP step issues ~600 kernels from Python (autograd, the native
+reducer's bucket hooks, MIOpen, the fused optimizer). On MI355X the GPU then
+idles wherever the host falls behind: in the round-3 kernel trace of
+``benchmarks/resnet_ddp.py`` 1.4 ms of a 19.2 ms step were gaps of 5 us or more
+(after the loss, after the optimizer, around MIOpen helper launches;
+profiles/r3_resnet_graph.md). Capturing the step once and replaying it removes
+every host launch from the loop: one graph launch per step.
+
+What makes a step capturable here (all true of this package's pieces):
+  * no host reads inside the step (FusedSGD/FusedAdam keep their step counters on
+    the device, BN tickets re-arm in-kernel, DDP's world-1 reducer issues nothing);
+  * static inputs: the caller refreshes the tensors the step reads (``x``, ``y``)
+    in place before each replay;
+  * collectives on the captured streams: the reducer's comm stream joins the
+    capture through its ready/done events, and every captured RCCL collective is
+    followed by a device completion mark the communicator's watchdog follows
+    (:class:`ops.fused_step.WatchedGraph`), so a stalled replay aborts instead of
+    hanging;
+  * one-time host work (MIOpen exhaustive find, DDP's bucket rebuild after
+    iteration 0, optimizer state allocation) happens in the eager warm-up steps,
+    which run on a side stream before capture (the torch.cuda.graph recipe).
+
+Reference loop being accelerated: ``Trainer._run_batch`` ddp_gpus.py:34-39 /
+the ResNet-50 train loop NB03:969-992.
+"""
+from __future__ import annotations
+
+from typing import Callable
+
+import torch
+
+from ..ops.fused_step import WatchedGraph
+
+
+class GraphedStep:
+    """``step = GraphedStep(fn, device, comm=comm)``; ``out = step()`` replays.
+
+    ``fn`` runs one full training step (zero_grad, forward, backward, optimizer) and
+    returns its outputs (e.g. the loss tensor). ``warmup`` eager calls run first on a
+    side stream -- they ARE training steps (the trajectory simply starts with them).
+    The returned outputs are static tensors overwritten by every replay."""
+
+    def __init__(self, fn: Callable[[], object], device: torch.device, comm=None, warmup: int = 3):
+        if device.type != "cuda":
+            raise ValueError("GraphedStep needs a GPU device")
+        self.fn = fn
+        self.device = device
+        stream = torch.cuda.Stream(device)
+        stream.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(stream):
+            for _ in range(max(1, warmup)):
+                fn()
+        torch.cuda.current_stream(device).wait_stream(stream)
+        torch.cuda.synchronize(device)
+        rc = getattr(comm, "handle", None) if comm is not None else None
+        before = rc.captured if rc is not None else 0
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):
+            self.outputs = fn()
+        torch.cuda.synchronize(device)
+        self.graph = WatchedGraph(g, rc, (rc.captured - before) if rc is not None else 0)
+        self.replays = 0
+
+    @property
+    def n_collectives(self) -> int:
+        return self.graph.n_collectives
+
+    def __call__(self):
+        self.graph.replay()
+        self.replays += 1
+        return self.outputs
+
+    def reset(self):
+        self.graph.reset()

@@ -109,6 +109,13 @@ for s in "$@"; do
                for d in ${BNDIRS:-0 10 5}; do
                  jstep resnet_dir 600 env PTDT_BN_DIR=$d python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5
                done ;;
+    resgraph)  # ResNet-50 DDP: whole-step hipGraph (default) vs eager launches, same box
+               jstep resnet_graph 600 python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5
+               jstep resnet_graph 600 python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5 --no_graph ;;
+    resenv)    # ResNet-50 DDP under MIOpen solver switches (RESENVS: space-separated VAR=V[,VAR=V] sets)
+               for cfg in ${RESENVS:-"X=0"}; do
+                 jstep resnet_env 600 env ${cfg//,/ } python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5 --tag "$cfg"
+               done ;;
     bntest)    # BN numerics under non-default geometry
                tstep pytest_bn 300 env PTDT_BN_DIR=15 PTDT_BN_AU=4 PTDT_BN_APPLY_BLOCKS=0 $PYTEST tests/test_norm.py ;;
     run:*)     step "run" 600 bash -c "${s#run:}" ;;  # ad-hoc: run:'python3 benchmarks/x.py'
