@@ -53,7 +53,9 @@ def timed(fn, iters):
 def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--kinds", default="res,relu,lin", help="comma list of BN kinds to run")
     a = ap.parse_args()
+    kinds = set(a.kinds.split(","))
     from pytorch_distributed_training_tutorials_amd._ext import native
 
     C_ = native()
@@ -61,6 +63,8 @@ def main():
     knobs = {k: os.environ.get(k, "default") for k in ("PTDT_BN_TC", "PTDT_BN_AU", "PTDT_BN_APPLY_BLOCKS", "PTDT_BN_DIR")}
     total = 0.0
     for kind, C, HW, count in CASES:
+        if kind not in kinds:
+            continue
         shape = (B, C, HW, HW)
         mk = lambda: torch.randn(shape, device=dev, dtype=torch.bfloat16).contiguous(  # noqa: E731
             memory_format=torch.channels_last)

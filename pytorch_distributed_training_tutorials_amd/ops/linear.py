@@ -19,10 +19,21 @@ nn.Linear's [out, in] weight, the backward GEMMs on K-contiguous copies (the
 transposes cost a few % of the GEMM), with the ReLU mask and bias gradient as
 separate elementwise / column-sum kernels.
 CPU tensors use ``torch.nn.functional.linear`` (plumbing tests only).
+
+Library GEMMs: the task's rule is "hand-written kernels for the fused hot ops,
+hipBLASLt only for plain library GEMMs". A large bf16 GEMM whose only epilogue is
+a bias (or nothing) is such a plain GEMM, and on those hipBLASLt measures ahead of
+gemm_big.hip (profiles/r2_gemm_bench.jsonl: 1.45-1.59 vs 1.14-1.20 PFLOP/s at
+4096^3 / 8192^3, 766 vs 560 TFLOP/s at 2048^3). ``PTDT_LINEAR_GEMM`` picks the
+engine for those shapes: ``auto`` (default; hipBLASLt through torch.matmul for
+plain bf16 GEMMs of >= 2^24 MACs, the native kernels for everything fused or
+small -- fp32, ReLU epilogues and masks, split-K toy shapes), ``native`` (always
+gemm_big.hip) or ``library``.
 """
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -51,6 +62,19 @@ def _big(M: int, N: int, K: int, dtype) -> bool:
     """Use the LDS-DMA kernel: bf16 with enough work (K not a multiple of its 64-deep
     K-tile is zero-padded by gemm_nt_big, e.g. ResNet fc's dx with K = 1000 classes)."""
     return dtype == torch.bfloat16 and K >= 64 and M * N * K >= _BIG_MIN_MACS
+
+
+def _engine() -> str:
+    e = os.environ.get("PTDT_LINEAR_GEMM", "auto").lower()
+    if e not in ("auto", "native", "library"):
+        raise ValueError(f"PTDT_LINEAR_GEMM must be auto, native or library, got {e!r}")
+    return e
+
+
+def _library(relu: bool = False) -> bool:
+    """Plain big bf16 GEMM on hipBLASLt? (``_big`` is checked by the caller.)"""
+    e = _engine()
+    return e == "library" or (e == "auto" and not relu)
 
 
 def plan_big(M: int, N: int, K: int) -> tuple[int, int]:
@@ -135,7 +159,11 @@ class _LinearFn(torch.autograd.Function):
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         M, K = x2.shape
-        if _big(M, weight.shape[0], K, x2.dtype):
+        if _big(M, weight.shape[0], K, x2.dtype) and _library(relu):
+            y = F.linear(x2, weight, bias.to(x2.dtype) if bias is not None else None)  # hipBLASLt (+bias epilogue)
+            if relu:
+                y = y.relu_()
+        elif _big(M, weight.shape[0], K, x2.dtype):
             y = gemm_nt_big(x2, weight, x.dtype, bias=bias, relu=relu)
         else:
             y = gemm(x2, weight.t(), bias=bias, relu=relu, out_dtype=x.dtype)
@@ -160,11 +188,18 @@ class _LinearFn(torch.autograd.Function):
         if big_dx or big_dw:
             C_ = native()
             g = C_.relu_bwd(dy2, mask) if mask is not None else dy2
+            lib = _library()
             if ctx.needs_input_grad[0]:
-                dx = (gemm_nt_big(g, weight.t(), x2.dtype) if big_dx else
-                      gemm(g, weight, out_dtype=x2.dtype)).reshape(ctx.in_shape)
+                if big_dx and lib:
+                    dx = torch.matmul(g, weight).reshape(ctx.in_shape)
+                else:
+                    dx = (gemm_nt_big(g, weight.t(), x2.dtype) if big_dx else
+                          gemm(g, weight, out_dtype=x2.dtype)).reshape(ctx.in_shape)
             if ctx.needs_input_grad[1]:
-                dw = gemm_nt_big(g.t(), x2.t(), weight.dtype) if big_dw else gemm(g.t(), x2, out_dtype=weight.dtype)
+                if big_dw and lib:
+                    dw = torch.matmul(g.t(), x2)
+                else:
+                    dw = gemm_nt_big(g.t(), x2.t(), weight.dtype) if big_dw else gemm(g.t(), x2, out_dtype=weight.dtype)
             if ctx.has_bias and ctx.needs_input_grad[2]:
                 cs = torch.empty(Nout, device=dy.device, dtype=torch.float32)
                 C_.col_sum_(g, cs, False)

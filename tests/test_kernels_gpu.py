@@ -274,12 +274,16 @@ def test_linear_autograd(native, dev, dtype, relu):
     torch.testing.assert_close(b.grad.float(), br.grad, rtol=tol, atol=tol * 4)
 
 
+@pytest.mark.parametrize("engine", ["native", "auto"])
 @pytest.mark.parametrize("relu", [False, True])
-def test_linear_big_bf16_path(native, dev, relu):
-    """bf16 Linear large enough for the 256x256 kernel (forward, dx, dW, db) vs fp32 autograd."""
+def test_linear_big_bf16_path(native, dev, relu, engine, monkeypatch):
+    """bf16 Linear large enough for the 256x256 kernel (forward, dx, dW, db) vs fp32 autograd;
+    ``native``: every GEMM on gemm_big.hip, ``auto``: plain GEMMs on hipBLASLt, fused ones native."""
     import importlib
 
+    monkeypatch.setenv("PTDT_LINEAR_GEMM", engine)
     L = importlib.import_module("pytorch_distributed_training_tutorials_amd.ops.linear")  # module, not the op
+    assert L._library(relu) == (engine == "auto" and not relu)
     torch.manual_seed(5)
     M, K, N = 512, 384, 320
     assert L._big(M, N, K, torch.bfloat16) and L._big(N, K, M, torch.bfloat16)
