@@ -501,6 +501,29 @@ void bucket_copy(std::vector<Tensor> ts, Tensor flat, double scale, bool unpack)
   });
 }
 
+// dsts[i] (f32) = srcs[i] (bf16), one multi-tensor launch per <= 32 pairs; pairs must share shape and strides
+void cast_multi_(std::vector<Tensor> dsts, std::vector<Tensor> srcs) {
+  TORCH_CHECK(dsts.size() == srcs.size(), "cast_multi_: one source per destination");
+  if (dsts.empty()) return;
+  c10::hip::HIPGuard guard(dsts[0].device().index());
+  for_tensor_chunks(dsts.size(), [&](size_t a, size_t b) {
+    TensorList tl{};
+    tl.n = (int)(b - a);
+    for (size_t i = a; i < b; ++i) {
+      TORCH_CHECK(dsts[i].scalar_type() == at::kFloat && srcs[i].scalar_type() == at::kBFloat16,
+                  "cast_multi_: f32 destinations, bf16 sources");
+      TORCH_CHECK(dsts[i].device() == dsts[0].device() && srcs[i].device() == dsts[0].device(),
+                  "cast_multi_: one device");
+      check_dense_like(dsts[i], dsts[i], "destination");
+      check_dense_like(dsts[i], srcs[i], "source");
+      tl.numel[i - a] = dsts[i].numel();
+      tl.p[i - a] = dsts[i].data_ptr();
+      tl.g[i - a] = srcs[i].data_ptr();
+    }
+    hip_check(cast_bf16_f32_multi(tl, cur_stream(dsts[0])), "cast_bf16_f32_multi");
+  });
+}
+
 void scale_(Tensor x, double s) {
   check_gpu(x, "x");
   c10::hip::HIPGuard guard(x.device().index());
@@ -1147,6 +1170,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("adam_multi_", &adam_multi_);
   m.def("bucket_copy", &bucket_copy);
   m.def("scale_", &scale_);
+  m.def("cast_multi_", &cast_multi_, py::arg("dsts"), py::arg("srcs"));
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("mse_fwd", &mse_fwd);

@@ -130,6 +130,23 @@ int interleave_rows() {
   return v;
 }
 
+// reduction geometry knobs (profiles/r3_bn_sweep.md): minimum rows per thread (PTDT_BN_RPT) and the
+// cap on reduction workgroups (PTDT_BN_RED_BLOCKS; the grid is at most cap / channel tiles row blocks)
+int red_rows_per_thread() {
+  static const int v = [] {
+    const int r = env_int("PTDT_BN_RPT", 16);
+    return r >= 1 && r <= 256 ? r : 16;
+  }();
+  return v;
+}
+int red_block_cap() {
+  static const int v = [] {
+    const int c = env_int("PTDT_BN_RED_BLOCKS", kRedBlocks);
+    return c >= 64 && c <= 4096 ? c : kRedBlocks;
+  }();
+  return v;
+}
+
 struct Geom {
   int TC, RPI;       // channel vectors per row, rows per block iteration
   int gx, gy;        // row blocks, channel tiles
@@ -144,8 +161,9 @@ Geom geom(int64_t M, int C) {
   g.TC = cv < mt ? cv : mt;
   g.RPI = kRed / g.TC;
   g.gy = (cv + g.TC - 1) / g.TC;
-  int64_t want = (M + (int64_t)g.RPI * 16 - 1) / ((int64_t)g.RPI * 16);  // >= 16 rows per thread
-  int64_t cap = kRedBlocks / g.gy;
+  const int rpt = red_rows_per_thread();
+  int64_t want = (M + (int64_t)g.RPI * rpt - 1) / ((int64_t)g.RPI * rpt);  // >= rpt rows per thread
+  int64_t cap = red_block_cap() / g.gy;
   if (cap > kMaxGx) cap = kMaxGx;
   if (cap < 1) cap = 1;
   g.gx = (int)(want < 1 ? 1 : (want > cap ? cap : want));

@@ -186,6 +186,8 @@ struct CopyList {
 hipError_t bucket_pack(const CopyList& cl, void* flat, int dtype, float scale, hipStream_t s);
 hipError_t bucket_unpack(const CopyList& cl, const void* flat, int dtype, float scale, hipStream_t s);
 hipError_t scale_inplace(void* x, int64_t n, int dtype, float scale, hipStream_t s);
+// tl.p[t] (f32) = tl.g[t] (bf16) elementwise, every tensor dense with matching layouts
+hipError_t cast_bf16_f32_multi(const TensorList& tl, hipStream_t s);
 
 // --------------------------------------------------------------------------
 // Losses (csrc/kernels/loss.hip). Row-wise log-softmax CE (soft or index

@@ -167,6 +167,19 @@ __global__ void __launch_bounds__(kBlock) pack_kernel(CopyList cl, T* flat, floa
   }
 }
 
+// dst[t][i] = f32(src[t][i]): bf16 weight gradients (autocast convolutions) into their f32 DDP bucket
+// slots, one launch per bucket instead of one copy per parameter (ops/conv.py deferred casts)
+__global__ void __launch_bounds__(kBlock) cast_bf16_f32_multi_kernel(TensorList tl) {
+  int t;
+  int64_t start;
+  locate_chunk(tl.numel, tl.n, blockIdx.x, t, start);
+  if (t >= tl.n) return;
+  float* __restrict__ d = static_cast<float*>(tl.p[t]);
+  const uint16_t* __restrict__ src = static_cast<const uint16_t*>(tl.g[t]);
+  const int64_t end = min(start + (int64_t)kChunk, tl.numel[t]);
+  for (int64_t i = start + threadIdx.x; i < end; i += kBlock) d[i] = bf16_to_f32(src[i]);
+}
+
 template <typename T>
 __global__ void __launch_bounds__(kBlock) scale_kernel(T* x, int64_t n, float scale) {
   const int64_t stride = (int64_t)gridDim.x * kBlock;
@@ -251,6 +264,13 @@ hipError_t bucket_unpack(const CopyList& cl, const void* flat, int dtype, float 
     hipLaunchKernelGGL(pack_kernel<float>, dim3(nb), dim3(kBlock), 0, s, cl, (float*)flat, scale, 1);
   else
     hipLaunchKernelGGL(pack_kernel<uint16_t>, dim3(nb), dim3(kBlock), 0, s, cl, (uint16_t*)flat, scale, 1);
+  return hipGetLastError();
+}
+
+hipError_t cast_bf16_f32_multi(const TensorList& tl, hipStream_t s) {
+  const int nb = chunk_blocks(tl);
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(cast_bf16_f32_multi_kernel, dim3(nb), dim3(kBlock), 0, s, tl);
   return hipGetLastError();
 }
 

@@ -24,11 +24,14 @@ Library GEMMs: the task's rule is "hand-written kernels for the fused hot ops,
 hipBLASLt only for plain library GEMMs". A large bf16 GEMM whose only epilogue is
 a bias (or nothing) is such a plain GEMM, and on those hipBLASLt measures ahead of
 gemm_big.hip (profiles/r2_gemm_bench.jsonl: 1.45-1.59 vs 1.14-1.20 PFLOP/s at
-4096^3 / 8192^3, 766 vs 560 TFLOP/s at 2048^3). ``PTDT_LINEAR_GEMM`` picks the
-engine for those shapes: ``auto`` (default; hipBLASLt through torch.matmul for
-plain bf16 GEMMs of >= 2^24 MACs, the native kernels for everything fused or
-small -- fp32, ReLU epilogues and masks, split-K toy shapes), ``native`` (always
-gemm_big.hip) or ``library``.
+4096^3 / 8192^3, 766 vs 560 TFLOP/s at 2048^3). It is not ahead everywhere:
+hipBLASLt picks a weak tiling for 4096x11008x4096 (917 vs 1070 TFLOP/s native) and
+ties at 1024^3. ``PTDT_LINEAR_GEMM`` picks the engine for plain bf16 GEMMs of
+>= 2^24 MACs: ``auto`` (default) times both engines once per (M, N, K, transpose
+form) on first use -- like MIOpen's find / cudnn.benchmark -- and keeps the faster
+(during hipGraph capture an untuned shape takes hipBLASLt); ``native`` (always
+gemm_big.hip) or ``library`` (always hipBLASLt). Everything fused or small stays on
+the native kernels: fp32, ReLU epilogues and masks, split-K toy shapes.
 """
 from __future__ import annotations
 
@@ -71,10 +74,37 @@ def _engine() -> str:
     return e
 
 
-def _library(relu: bool = False) -> bool:
-    """Plain big bf16 GEMM on hipBLASLt? (``_big`` is checked by the caller.)"""
+_TUNED: dict = {}
+
+
+def _time(fn, reps: int = 3) -> float:
+    fn()  # warm-up (and the hipBLASLt heuristic query)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e)
+
+
+def _library(relu: bool = False, key=None, native_fn=None, library_fn=None) -> bool:
+    """Plain big bf16 GEMM on hipBLASLt? (``_big`` is checked by the caller.) Under ``auto`` a
+    shape ``key`` with both engines' thunks is timed once and the winner cached."""
     e = _engine()
-    return e == "library" or (e == "auto" and not relu)
+    if e != "auto":
+        return e == "library"
+    if relu:
+        return False
+    if key is None or native_fn is None or library_fn is None:
+        return True
+    hit = _TUNED.get(key)
+    if hit is not None:
+        return hit
+    if torch.cuda.is_current_stream_capturing():
+        return True  # no timing inside a capture; the shape stays untuned
+    _TUNED[key] = _time(library_fn) <= _time(native_fn)
+    return _TUNED[key]
 
 
 def plan_big(M: int, N: int, K: int) -> tuple[int, int]:
@@ -159,11 +189,15 @@ class _LinearFn(torch.autograd.Function):
         if not x2.is_contiguous():
             x2 = x2.contiguous()
         M, K = x2.shape
-        if _big(M, weight.shape[0], K, x2.dtype) and _library(relu):
-            y = F.linear(x2, weight, bias.to(x2.dtype) if bias is not None else None)  # hipBLASLt (+bias epilogue)
+        big = _big(M, weight.shape[0], K, x2.dtype)
+        lib_b = bias.to(x2.dtype) if (big and bias is not None) else bias
+        if big and _library(relu, ("nt", M, weight.shape[0], K),
+                            lambda: gemm_nt_big(x2, weight, x.dtype, bias=bias),
+                            lambda: F.linear(x2, weight, lib_b)):
+            y = F.linear(x2, weight, lib_b)  # hipBLASLt (+bias epilogue)
             if relu:
                 y = y.relu_()
-        elif _big(M, weight.shape[0], K, x2.dtype):
+        elif big:
             y = gemm_nt_big(x2, weight, x.dtype, bias=bias, relu=relu)
         else:
             y = gemm(x2, weight.t(), bias=bias, relu=relu, out_dtype=x.dtype)
@@ -188,15 +222,16 @@ class _LinearFn(torch.autograd.Function):
         if big_dx or big_dw:
             C_ = native()
             g = C_.relu_bwd(dy2, mask) if mask is not None else dy2
-            lib = _library()
             if ctx.needs_input_grad[0]:
-                if big_dx and lib:
+                if big_dx and _library(False, ("nn", M, Kin, Nout), lambda: gemm_nt_big(g, weight.t(), x2.dtype),
+                                       lambda: torch.matmul(g, weight)):
                     dx = torch.matmul(g, weight).reshape(ctx.in_shape)
                 else:
                     dx = (gemm_nt_big(g, weight.t(), x2.dtype) if big_dx else
                           gemm(g, weight, out_dtype=x2.dtype)).reshape(ctx.in_shape)
             if ctx.needs_input_grad[1]:
-                if big_dw and lib:
+                if big_dw and _library(False, ("tn", Nout, Kin, M), lambda: gemm_nt_big(g.t(), x2.t(), weight.dtype),
+                                       lambda: torch.matmul(g.t(), x2)):
                     dw = torch.matmul(g.t(), x2)
                 else:
                     dw = gemm_nt_big(g.t(), x2.t(), weight.dtype) if big_dw else gemm(g.t(), x2, out_dtype=weight.dtype)

@@ -18,6 +18,7 @@ rebuild in rank 0's observed ready order after the first iteration.
 from __future__ import annotations
 
 import contextlib
+import os
 import weakref
 
 import torch
@@ -103,6 +104,7 @@ class DistributedDataParallel(nn.Module):
         # the bucket slot when .grad is None, which zero_grad arranges for exactly these params
         self._sink_params = []
         self._forwards = 0
+        self._defer, self._pending, self._remaining = False, {}, {}
         if self.device.type == "cuda":
             from ..ops.conv import Conv2d
             from ..ops.linear import Linear
@@ -111,9 +113,16 @@ class DistributedDataParallel(nn.Module):
             sink_ids = {id(m.weight) for m in module.modules() if isinstance(m, (Conv2d, Linear))}
             sink_ids |= {id(t) for m in module.modules() if isinstance(m, BatchNorm2d)
                          for t in (m.weight, m.bias) if t is not None}
+            # deferred weight-gradient casts (ops/conv.py): a bucket's bf16 gradients are converted
+            # into its slots by one launch, issued when the bucket's LAST parameter is marked ready
+            # (before its all-reduce). Needs every parameter to report (no find_unused_parameters).
+            self._defer = (not find_unused_parameters and os.environ.get("PTDT_DEFER_GRAD_CAST", "1") != "0")
+            self._index_buckets()
             for i, p in enumerate(params):
                 if id(p) in sink_ids:
                     p._ptdt_grad_sink = self._make_sink(i, p)
+                    if self._defer:
+                        p._ptdt_grad_defer = self._make_defer(i)
                     self._sink_params.append(p)
 
     # --------------------------------------------------------------- internals
@@ -145,6 +154,29 @@ class DistributedDataParallel(nn.Module):
             return ddp.reducer.grad_view(i)
         return sink
 
+    def _make_defer(self, i: int):
+        """Record (bucket slot, bf16 gradient) of parameter ``i`` for its bucket's batched cast."""
+        ref = weakref.ref(self)
+
+        def defer(dst, src):
+            ddp = ref()
+            if ddp is None or src.dtype != torch.bfloat16 or dst.dtype != torch.float32 or src.stride() != dst.stride():
+                return False
+            ddp._pending.setdefault(ddp._bucket_of[i], []).append((dst, src))
+            return True
+        return defer
+
+    def _index_buckets(self):
+        self._buckets = [list(b) for b in self.reducer.buckets()]
+        self._bucket_of = {int(i): b for b, ps in enumerate(self._buckets) for i in ps}
+
+    def _flush_casts(self, b=None):
+        keys = [b] if b is not None else list(self._pending)
+        for k in keys:
+            pend = self._pending.pop(k, None)
+            if pend:
+                native().cast_multi_([d for d, _ in pend], [s for _, s in pend])
+
     def _make_hook(self, i: int):
         ref = weakref.ref(self)  # as in _make_sink: parameters must not keep the wrapper alive
 
@@ -155,11 +187,18 @@ class DistributedDataParallel(nn.Module):
             if not ddp._queued and ddp.reducer.in_backward:
                 ddp._queued = True
                 torch.autograd.Variable._execution_engine.queue_callback(ddp._finalize)
+            if ddp._defer:
+                b = ddp._bucket_of.get(i)
+                left = ddp._remaining.get(b, 0) - 1
+                ddp._remaining[b] = left
+                if left <= 0 and b in ddp._pending:  # the bucket completes with this mark: fill its slots
+                    ddp._flush_casts(b)
             ddp.reducer.mark_ready(i)
         return hook
 
     def _finalize(self):
         self._queued = False
+        self._flush_casts()  # anything a bucket never completed (e.g. no_sync accumulation)
         self.reducer.finalize()
 
     def _maybe_rebuild(self):
@@ -168,6 +207,8 @@ class DistributedDataParallel(nn.Module):
         order = self.comm.broadcast_object(list(self.reducer.ready_order()), 0)
         if len(order) == len(self._params):
             self.reducer.rebuild(bucketing.plan(self._params, order, self._first_cap, self._cap, self.world_size))
+            if hasattr(self, "_bucket_of"):
+                self._index_buckets()
         self._rebuilt = True
 
     # --------------------------------------------------------------- API
@@ -180,6 +221,9 @@ class DistributedDataParallel(nn.Module):
         if torch.is_grad_enabled():
             self.reducer.prepare_for_backward(self.require_backward_grad_sync)
             self._forwards += 1  # a new forward: every grad sink may be claimed once again
+            if self._defer:
+                self._flush_casts()
+                self._remaining = {b: len(ps) for b, ps in enumerate(self._buckets)}
         return self.module(*args, **kwargs)
 
     @contextlib.contextmanager
@@ -203,6 +247,8 @@ class DistributedDataParallel(nn.Module):
         for p in getattr(self, "_sink_params", ()):
             if getattr(p, "_ptdt_grad_sink", None) is not None:
                 del p._ptdt_grad_sink
+            if getattr(p, "_ptdt_grad_defer", None) is not None:
+                del p._ptdt_grad_defer
         self._sink_params = []
 
     def __del__(self):

@@ -103,7 +103,7 @@ for s in "$@"; do
                pmc wave2 "$P2" python3 bench.py --steps 20000 --warmup 1 --no_mlp_side ;;
     bnsweep)   # BN kernel geometry / sweep-direction sweep (benchmarks/bn_kernel_bench.py), one process per setting
                for cfg in ${BNCFGS:-"PTDT_BN_DIR=0" "PTDT_BN_DIR=10" "PTDT_BN_DIR=5" "PTDT_BN_DIR=2" "PTDT_BN_DIR=8" "PTDT_BN_TC=8"}; do
-                 jstep bnk 120 env $cfg python3 benchmarks/bn_kernel_bench.py
+                 jstep bnk 120 env ${cfg//,/ } python3 benchmarks/bn_kernel_bench.py
                done ;;
     resdir)    # ResNet-50 DDP step under each BN sweep-direction setting
                for d in ${BNDIRS:-0 10 5}; do

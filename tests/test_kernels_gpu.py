@@ -301,6 +301,9 @@ def test_linear_big_bf16_path(native, dev, relu, engine, monkeypatch):
     for got, ref, k in ((y, yr, K), (x.grad, xr.grad, N), (w.grad, wr.grad, M), (b.grad, br.grad, M)):
         tol = 2e-2 * math.sqrt(k) / 4
         torch.testing.assert_close(got.float(), ref, rtol=tol, atol=tol)
+    if engine == "auto":  # every plain GEMM of the layer was timed on both engines and the winner cached
+        forms = {k[0] for k in L._TUNED if k[1:] in ((M, N, K), (M, K, N), (N, K, M))}
+        assert forms == ({"nn", "tn"} if relu else {"nt", "nn", "tn"})
 
 
 def test_linear_under_autocast(native, dev):
