@@ -44,11 +44,13 @@ class SinkCast(torch.autograd.Function):
         w = ctx.w
         sink = getattr(w, "_ptdt_grad_sink", None)
         out = sink() if (sink is not None and w.grad is None) else None  # None: slot already claimed
+        defer = getattr(w, "_ptdt_grad_defer", None)
         if out is not None:
-            defer = getattr(w, "_ptdt_grad_defer", None)
             if defer is None or not defer(out, g):
                 out.copy_(g)  # bf16 -> fp32 conversion straight into the bucket
             return out, None, None
+        if defer is not None and sink is not None and w.grad is None:
+            defer(None, None)  # a tied weight's other use deferred its cast: land it before autograd adds
         return g.to(w.dtype), None, None
 
 

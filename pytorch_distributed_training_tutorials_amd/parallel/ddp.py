@@ -155,14 +155,30 @@ class DistributedDataParallel(nn.Module):
         return sink
 
     def _make_defer(self, i: int):
-        """Record (bucket slot, bf16 gradient) of parameter ``i`` for its bucket's batched cast."""
+        """Record parameter ``i``'s bf16 gradient for its bucket's batched cast into the slot.
+
+        Only the index is kept, never the slot view the sink handed to autograd: an extra
+        reference to that view would make AccumulateGrad copy it instead of adopting it.
+        ``defer(None, None)`` (a second contribution to a tied weight arrived) casts the
+        pending gradient now, before autograd adds the other contribution into the slot."""
         ref = weakref.ref(self)
 
         def defer(dst, src):
             ddp = ref()
-            if ddp is None or src.dtype != torch.bfloat16 or dst.dtype != torch.float32 or src.stride() != dst.stride():
+            if ddp is None:
                 return False
-            ddp._pending.setdefault(ddp._bucket_of[i], []).append((dst, src))
+            b = ddp._bucket_of[i]
+            if dst is None:  # tied weight: flush this parameter's entry now
+                pend = ddp._pending.get(b, [])
+                for k, (j, g) in enumerate(pend):
+                    if j == i:
+                        del pend[k]
+                        ddp.reducer.grad_view(j).copy_(g)
+                        break
+                return True
+            if src.dtype != torch.bfloat16 or dst.dtype != torch.float32 or src.stride() != dst.stride():
+                return False
+            ddp._pending.setdefault(b, []).append((i, src))
             return True
         return defer
 
@@ -175,7 +191,7 @@ class DistributedDataParallel(nn.Module):
         for k in keys:
             pend = self._pending.pop(k, None)
             if pend:
-                native().cast_multi_([d for d, _ in pend], [s for _, s in pend])
+                native().cast_multi_([self.reducer.grad_view(j) for j, _ in pend], [g for _, g in pend])
 
     def _make_hook(self, i: int):
         ref = weakref.ref(self)  # as in _make_sink: parameters must not keep the wrapper alive

@@ -43,6 +43,57 @@ def test_sink_claimed_once_per_forward_sums_tied_uses():
     torch.testing.assert_close(w.grad, torch.full((4, 3), 4.0))
 
 
+def _deferring_sink(buf):
+    """parallel.ddp's sink + deferred-cast protocol on one slot: claimed once, the cast recorded
+    by index (no reference to the view autograd adopts) and landed by flush() or by defer(None, None)."""
+    claimed, pending = [], []
+
+    def sink():
+        if claimed:
+            return None
+        claimed.append(1)
+        return buf.view(4, 3)
+
+    def flush():
+        for g in pending:
+            buf.view(4, 3).copy_(g)
+        pending.clear()
+
+    def defer(dst, src):
+        if dst is None:
+            flush()
+        else:
+            pending.append(src)
+        return True
+    return sink, defer, flush, pending
+
+
+def test_deferred_cast_is_adopted_and_landed_by_flush():
+    w = nn.Parameter(torch.randn(4, 3))
+    buf = torch.zeros(12)
+    sink, defer, flush, pending = _deferring_sink(buf)
+    w._ptdt_grad_sink, w._ptdt_grad_defer = sink, defer
+    (SinkCast.apply(w, torch.bfloat16).float() * torch.arange(12.0).view(4, 3)).sum().backward()
+    assert len(pending) == 1 and w.grad.data_ptr() == buf.data_ptr()  # adopted, not copied
+    flush()  # the bucket-completion flush
+    torch.testing.assert_close(w.grad, torch.arange(12.0).view(4, 3))
+
+
+def test_deferred_cast_tied_weight_lands_before_the_sum():
+    """Two uses of one weight: the second backward finds the slot claimed and lands the first's
+    deferred cast before autograd adds the two contributions into the slot."""
+    w = nn.Parameter(torch.randn(4, 3))
+    buf = torch.zeros(12)
+    sink, defer, flush, pending = _deferring_sink(buf)
+    w._ptdt_grad_sink, w._ptdt_grad_defer = sink, defer
+    y1 = SinkCast.apply(w, torch.bfloat16)
+    y2 = SinkCast.apply(w, torch.bfloat16)
+    (y1.float().sum() * 1.0 + y2.float().sum() * 3.0).backward()
+    flush()
+    assert not pending
+    torch.testing.assert_close(w.grad, torch.full((4, 3), 4.0))
+
+
 def test_conv2d_is_a_drop_in_conv():
     a, b = Conv2d(3, 8, 3, padding=1), nn.Conv2d(3, 8, 3, padding=1)
     b.load_state_dict(a.state_dict())

@@ -283,6 +283,7 @@ def test_linear_big_bf16_path(native, dev, relu, engine, monkeypatch):
 
     monkeypatch.setenv("PTDT_LINEAR_GEMM", engine)
     L = importlib.import_module("pytorch_distributed_training_tutorials_amd.ops.linear")  # module, not the op
+    L._TUNED.clear()
     assert L._library(relu) == (engine == "auto" and not relu)
     torch.manual_seed(5)
     M, K, N = 512, 384, 320
