@@ -40,8 +40,11 @@ def main(argv=None):
     ap.add_argument("--no_shadow", action="store_true",
                     help="cast the fp32 weights in every forward instead of using FusedSGD's bf16 shadows")
     ap.add_argument("--tag", default=None, help="free-form label copied into the JSON line")
-    ap.add_argument("--no_graph", action="store_true",
-                    help="native impl: launch every step eagerly instead of replaying one captured hipGraph per step")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="native impl: replay one captured hipGraph per step (on), launch eagerly (off), or time "
+                         "both in this process after warm-up and keep the faster (auto: the eager loop's cost "
+                         "depends on the host, the graph's does not)")
+    ap.add_argument("--no_graph", action="store_true", help="= --graph off")
     ap.add_argument("--no_cudnn_benchmark", action="store_true",
                     help="keep MIOpen's heuristic solver choice (default: exhaustive find per conv shape)")
     a = ap.parse_args(argv)
@@ -78,7 +81,8 @@ def main(argv=None):
         x = x.contiguous(memory_format=torch.channels_last)
     y = torch.randint(0, 1000, (a.batch_size,), device=dev)
     amp = a.dtype == "bf16"
-    graphed = a.impl == "native" and not a.no_graph
+    mode = "off" if (a.no_graph or a.impl != "native") else a.graph
+    graphed = mode != "off"
 
     def step():
         if a.impl == "native":
@@ -93,10 +97,33 @@ def main(argv=None):
         opt.step()
         return loss
 
+    ab = None
     if graphed:  # utils/graphs.py: eager warm-up steps on a side stream, then one hipGraph per step
         from pytorch_distributed_training_tutorials_amd.utils.graphs import GraphedStep
 
-        step = GraphedStep(step, dev, comm=comm, warmup=max(3, a.warmup))
+        eager = step
+        gstep = GraphedStep(eager, dev, comm=comm, warmup=max(3, a.warmup))
+        step = gstep
+        if mode == "auto":  # interleaved A/B in this process: 3 rounds of 4 steps each way
+            ab = {"eager": [], "graph": []}
+            for _ in range(3):
+                for name, fn in (("eager", eager), ("graph", gstep)):
+                    comm.barrier()
+                    torch.cuda.synchronize(dev)
+                    t0 = time.perf_counter()
+                    for _ in range(4):
+                        fn()
+                    torch.cuda.synchronize(dev)
+                    ab[name].append((time.perf_counter() - t0) / 4 * 1e3)
+            med = {k: sorted(v)[1] for k, v in ab.items()}
+            win = "graph" if med["graph"] <= med["eager"] else "eager"
+            if world > 1:  # every rank must take the same path (the graph holds collectives)
+                flag = torch.tensor([1.0 if win == "graph" else 0.0], device=dev)
+                comm.all_reduce(flag, "min")
+                win = "graph" if float(flag.item()) == 1.0 else "eager"
+            graphed = win == "graph"
+            step = gstep if graphed else eager
+            ab = {k: round(v, 3) for k, v in med.items()}
     for _ in range(a.warmup):
         step()
     comm.barrier()
@@ -118,7 +145,7 @@ def main(argv=None):
             "dtype": a.dtype, "data": "synthetic ImageNet-shaped (generated on device)",
             "config": {"model": "resnet50", "per_device_batch": a.batch_size, "image": a.image,
                        "parallelism": f"dp{world}", "channels_last": not a.no_channels_last},
-            "impl": a.impl, "hipgraph": graphed, "bn_dir": os.environ.get("PTDT_BN_DIR", "0"), "miopen_find": "exhaustive (cudnn.benchmark)" if torch.backends.cudnn.benchmark else "heuristic",
+            "impl": a.impl, "hipgraph": graphed, "graph_mode": mode, **({"ab_ms_per_step": ab} if ab else {}), "bn_dir": os.environ.get("PTDT_BN_DIR", "0"), "miopen_find": "exhaustive (cudnn.benchmark)" if torch.backends.cudnn.benchmark else "heuristic",
             "buckets_MB": [round(b / 2 ** 20, 2) for b in ddp.bucket_sizes_bytes()] if a.impl == "native" else None,
             "final_loss": float(loss.detach()), **({"tag": a.tag} if a.tag else {}),
         }), flush=True)

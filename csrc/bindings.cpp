@@ -58,10 +58,20 @@ void check_gpu(const Tensor& t, const char* name) {
 
 // Elementwise optimizer operands: any dense memory order (channels_last conv
 // weights), as long as every operand of one parameter shares it.
+// same element order in memory: equal strides on every dimension of size > 1 (size-1 dimensions
+// carry arbitrary strides, e.g. a [C, K, 1, 1] tensor contiguous vs channels_last)
+bool same_memory_order(const Tensor& a, const Tensor& b) {
+  if (a.sizes() != b.sizes()) return false;
+  for (int64_t d = 0; d < a.dim(); ++d)
+    if (a.size(d) > 1 && a.stride(d) != b.stride(d)) return false;
+  return true;
+}
+
 void check_dense_like(const Tensor& p, const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.is_non_overlapping_and_dense(), name, " must be dense (non-overlapping)");
-  TORCH_CHECK(t.numel() == p.numel() && (t.strides() == p.strides() || (t.is_contiguous() && p.is_contiguous())),
+  TORCH_CHECK(t.numel() == p.numel() &&
+                  (t.strides() == p.strides() || (t.is_contiguous() && p.is_contiguous()) || same_memory_order(t, p)),
               name, " must have the parameter's memory layout");
 }
 

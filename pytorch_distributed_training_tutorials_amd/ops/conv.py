@@ -27,6 +27,8 @@ Reference call sites: the 53 convolutions of torchvision's ResNet-50
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -70,13 +72,35 @@ def cast_weight(w: torch.Tensor) -> torch.Tensor:
     return sh if sh is not None else w.to(dt)
 
 
+def _pad_rgb(x: torch.Tensor, w: torch.Tensor):
+    """3 input channels -> 4 (zero channel in the input, zero slice in the weight: the same
+    convolution). MIOpen's NHWC bf16 solvers handle a 7x7/2 stem on 3 channels poorly (C = 3 does
+    not fill an MFMA K step): at batch 128 forward + weight gradient take 450 us on 3 channels and
+    342 us on 4, the pad included (benchmarks/stem_probe.py, profiles/r3_stem_probe.jsonl). The
+    input's cast to the compute dtype happens in the same copy."""
+    n, _, h, wd = x.shape
+    xp = torch.empty((n, 4, h, wd), device=x.device, dtype=w.dtype, memory_format=torch.channels_last)
+    xp[:, 3:].zero_()
+    xp[:, :3].copy_(x)
+    return xp, torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 1))
+
+
 class Conv2d(nn.Conv2d):
-    """Drop-in ``nn.Conv2d`` (same parameters, init, state_dict) with the grad-sink weight cast."""
+    """Drop-in ``nn.Conv2d`` (same parameters, init, state_dict) with the grad-sink weight cast.
+    Under bf16 autocast a 3-channel channels_last input (an RGB stem) runs as a 4-channel
+    convolution (``PTDT_PAD_RGB=0`` disables it)."""
 
     def forward(self, x):
         w = cast_weight(self.weight)
         if w is not self.weight:
-            x = x.to(w.dtype)
             b = self.bias.to(w.dtype) if self.bias is not None else None
+            if (self.in_channels == 3 and self.groups == 1 and x.dim() == 4 and self.padding_mode == "zeros"
+                    and x.is_contiguous(memory_format=torch.channels_last) and _PAD_RGB):
+                x, w = _pad_rgb(x, w)
+            else:
+                x = x.to(w.dtype)
             return self._conv_forward(x, w, b)
         return self._conv_forward(x, self.weight, self.bias)
+
+
+_PAD_RGB = os.environ.get("PTDT_PAD_RGB", "1") != "0"

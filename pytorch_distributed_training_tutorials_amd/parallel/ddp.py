@@ -44,6 +44,17 @@ def _flatten_broadcast(tensors, c: comm_mod.Communicator, src: int = 0):
             off += n
 
 
+def _same_dense_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
+    """Same shape and element order in memory: dense, equal strides on every dimension of size > 1
+    (a [Cout, Cin, 1, 1] weight gradient is (Cin, 1, 1, 1) contiguous and (Cin, 1, Cin, Cin) in
+    channels_last -- one layout)."""
+    from ..ops.flat import is_dense
+
+    if a.shape != b.shape or not (is_dense(a) and is_dense(b)):
+        return False
+    return all(sa == sb for n, sa, sb in zip(a.shape, a.stride(), b.stride()) if n > 1)
+
+
 def _state_buffers(module: nn.Module):
     """Buffers that are model state (persistent): running statistics, counters. Non-persistent
     scratch (e.g. ops.norm.BatchNorm2d's kernel tickets) is neither synced nor checkpointed."""
@@ -176,7 +187,7 @@ class DistributedDataParallel(nn.Module):
                         ddp.reducer.grad_view(j).copy_(g)
                         break
                 return True
-            if src.dtype != torch.bfloat16 or dst.dtype != torch.float32 or src.stride() != dst.stride():
+            if src.dtype != torch.bfloat16 or dst.dtype != torch.float32 or not _same_dense_layout(src, dst):
                 return False
             ddp._pending.setdefault(b, []).append((i, src))
             return True

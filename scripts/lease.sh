@@ -110,8 +110,8 @@ for s in "$@"; do
                  jstep resnet_dir 600 env PTDT_BN_DIR=$d python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5
                done ;;
     resgraph)  # ResNet-50 DDP: whole-step hipGraph (default) vs eager launches, same box
-               jstep resnet_graph 600 python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5
-               jstep resnet_graph 600 python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5 --no_graph ;;
+               jstep resnet_graph 600 python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5 --graph on
+               jstep resnet_graph 600 python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5 --graph off ;;
     resenv)    # ResNet-50 DDP under MIOpen solver switches (RESENVS: space-separated VAR=V[,VAR=V] sets)
                for cfg in ${RESENVS:-"X=0"}; do
                  jstep resnet_env 600 env ${cfg//,/ } python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5 --tag "$cfg"

@@ -262,3 +262,38 @@ def test_fused_sgd_bf16_shadow_replaces_autocast_cast():
                 assert cast_weight(w).data_ptr() != w._ptdt_bf16.data_ptr()
     for a, b in zip(*outs):  # (MIOpen's weight-gradient solvers may sum in any order: not bitwise)
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_same_dense_layout_ignores_unit_dims():
+    """A 1x1-conv weight gradient from MIOpen may carry channels_last strides on its size-1 dims;
+    it is still the slot's layout (the deferred cast must not fall back to a per-tensor copy)."""
+    from pytorch_distributed_training_tutorials_amd.parallel.ddp import _same_dense_layout
+
+    base = torch.empty(64 * 256)
+    a = base.as_strided((64, 256, 1, 1), (256, 1, 1, 1))
+    b = base.as_strided((64, 256, 1, 1), (256, 1, 256, 256))
+    assert _same_dense_layout(a, b)
+    c = torch.empty(64, 256, 3, 3).contiguous(memory_format=torch.channels_last)
+    assert not _same_dense_layout(c, torch.empty(64, 256, 3, 3))
+    assert _same_dense_layout(c, torch.empty_like(c))
+
+
+@pytest.mark.gpu
+def test_rgb_stem_conv_padded_under_autocast():
+    """Conv2d with 3 input channels under bf16 autocast runs as a 4-channel convolution (zero input
+    channel, zero weight slice): same output and weight gradient as the plain bf16 convolution."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    conv = Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(dev).to(memory_format=torch.channels_last)
+    ref = nn.Conv2d(3, 64, 7, stride=2, padding=3, bias=False).to(dev).to(memory_format=torch.channels_last)
+    ref.load_state_dict(conv.state_dict())
+    x = torch.randn(4, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y, yr = conv(x), ref(x)
+    assert y.shape == yr.shape == (4, 64, 32, 32)
+    torch.testing.assert_close(y.float(), yr.float(), rtol=2e-2, atol=2e-2)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g)
+    assert conv.weight.grad.shape == (64, 3, 7, 7)
+    torch.testing.assert_close(conv.weight.grad, ref.weight.grad, rtol=2e-2, atol=5e-2)
