@@ -534,6 +534,20 @@ void cast_multi_(std::vector<Tensor> dsts, std::vector<Tensor> srcs) {
   });
 }
 
+// [N, 3, H, W] channels_last f32/bf16 -> [N, 4, H, W] channels_last bf16 with a zero 4th channel
+Tensor rgb4_pack_(Tensor x) {
+  TORCH_CHECK(x.is_cuda(), "rgb4_pack: x must be a GPU tensor");
+  TORCH_CHECK(x.dim() == 4 && x.size(1) == 3 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "rgb4_pack: x must be a channels_last [N, 3, H, W] tensor");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "rgb4_pack: f32 or bf16");
+  c10::hip::HIPGuard guard(x.device().index());
+  Tensor y = at::empty({x.size(0), 4, x.size(2), x.size(3)},
+                       x.options().dtype(at::kBFloat16).memory_format(at::MemoryFormat::ChannelsLast));
+  hip_check(rgb4_pack(x.data_ptr(), dt_of(x), static_cast<uint16_t*>(y.data_ptr()), x.numel() / 3, cur_stream(x)),
+            "rgb4_pack");
+  return y;
+}
+
 void scale_(Tensor x, double s) {
   check_gpu(x, "x");
   c10::hip::HIPGuard guard(x.device().index());
@@ -1181,6 +1195,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bucket_copy", &bucket_copy);
   m.def("scale_", &scale_);
   m.def("cast_multi_", &cast_multi_, py::arg("dsts"), py::arg("srcs"));
+  m.def("rgb4_pack", &rgb4_pack_);
   m.def("ce_fwd", &ce_fwd);
   m.def("ce_bwd", &ce_bwd);
   m.def("mse_fwd", &mse_fwd);

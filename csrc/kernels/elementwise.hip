@@ -83,6 +83,32 @@ __global__ void __launch_bounds__(kBlock) bn_relu_kernel(const T* x, const float
 
 }  // namespace
 
+// NHWC 3-channel pixels (f32 or bf16) -> NHWC 4-channel bf16 with a zero 4th channel: the RGB stem's
+// input for the 4-channel convolution (ops/conv.py), cast and padded in one pass (8 B stored per pixel).
+template <typename T>
+__global__ void __launch_bounds__(kBlock) rgb4_pack_kernel(const T* __restrict__ x, uint2* __restrict__ y, int64_t npix) {
+  const int64_t stride = (int64_t)gridDim.x * kBlock;
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < npix; p += stride) {
+    const T* px = x + 3 * p;
+    const uint32_t r = f32_to_bf16(Cvt<T>::load(px, 0)), g = f32_to_bf16(Cvt<T>::load(px, 1)),
+                   b = f32_to_bf16(Cvt<T>::load(px, 2));
+    y[p] = make_uint2(r | (g << 16), b);
+  }
+}
+
+hipError_t rgb4_pack(const void* x, int dtype, uint16_t* y, int64_t npix, hipStream_t s) {
+  if (npix <= 0) return hipSuccess;
+  int64_t blocks = (npix + kBlock - 1) / kBlock;
+  if (blocks > 8192) blocks = 8192;
+  if (dtype == kF32)
+    hipLaunchKernelGGL(rgb4_pack_kernel<float>, dim3((int)blocks), dim3(kBlock), 0, s, static_cast<const float*>(x),
+                       reinterpret_cast<uint2*>(y), npix);
+  else
+    hipLaunchKernelGGL(rgb4_pack_kernel<uint16_t>, dim3((int)blocks), dim3(kBlock), 0, s,
+                       static_cast<const uint16_t*>(x), reinterpret_cast<uint2*>(y), npix);
+  return hipGetLastError();
+}
+
 hipError_t relu_backward(const void* dy, const void* y, void* dx, int dtype, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   if (dtype == kF32)

@@ -247,6 +247,8 @@ hipError_t gemm_bf16_big(const BigGemmArgs& g, hipStream_t s);
 
 // Elementwise helpers (csrc/kernels/elementwise.hip)
 hipError_t relu_backward(const void* dy, const void* y, void* dx, int dtype, int64_t n, hipStream_t s);
+// NHWC [npix, 3] (f32 / bf16) -> NHWC [npix, 4] bf16, 4th channel zero (RGB stem padding)
+hipError_t rgb4_pack(const void* x, int dtype, uint16_t* y, int64_t npix, hipStream_t s);
 // out[0] = sum of all n elements (fp32 accumulate, deterministic), one workgroup.
 hipError_t sum_all(const void* x, int dtype, int64_t n, float* out, hipStream_t s);
 

@@ -78,10 +78,14 @@ def _pad_rgb(x: torch.Tensor, w: torch.Tensor):
     not fill an MFMA K step): at batch 128 forward + weight gradient take 450 us on 3 channels and
     342 us on 4, the pad included (benchmarks/stem_probe.py, profiles/r3_stem_probe.jsonl). The
     input's cast to the compute dtype happens in the same copy."""
-    n, _, h, wd = x.shape
-    xp = torch.empty((n, 4, h, wd), device=x.device, dtype=w.dtype, memory_format=torch.channels_last)
-    xp[:, 3:].zero_()
-    xp[:, :3].copy_(x)
+    if x.requires_grad or w.dtype != torch.bfloat16 or x.dtype not in (torch.float32, torch.bfloat16):
+        n, _, h, wd = x.shape
+        xp = torch.zeros((n, 4, h, wd), device=x.device, dtype=w.dtype, memory_format=torch.channels_last)
+        xp[:, :3] = x
+    else:  # one native pass: cast + pad (csrc/kernels/elementwise.hip rgb4_pack)
+        from .._ext import native
+
+        xp = native().rgb4_pack(x)
     return xp, torch.nn.functional.pad(w, (0, 0, 0, 0, 0, 1))
 
 
