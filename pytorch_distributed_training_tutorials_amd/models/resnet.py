@@ -22,7 +22,7 @@ import torch.nn as nn
 
 from ..ops.conv import Conv2d
 from ..ops.linear import Linear
-from ..ops.norm import BatchNorm2d, MaxPool2d
+from ..ops.norm import BatchNorm2d, MaxPool2d, grad_link
 
 
 def bn_act(bn: nn.Module, x: torch.Tensor, residual: torch.Tensor | None = None, relu: bool = False,
@@ -65,7 +65,9 @@ class Bottleneck(nn.Module):
         self.stride = stride
 
     def forward(self, x):
-        identity = x if self.downsample is None else self.downsample(x)
+        # downsample block: x feeds conv1 and the downsample conv; the downsample branch's input
+        # gradient is summed inside the producing BN's backward (ops.norm.grad_link), not by autograd
+        identity = x if self.downsample is None else self.downsample(grad_link(x))
         out = bn_act(self.bn1, self.conv1(x), relu=True)
         out = bn_act(self.bn2, self.conv2(out), relu=True)
         # identity shortcut: the residual gradient goes straight into the producing BN's backward

@@ -108,6 +108,36 @@ class _BatchNormActFn(torch.autograd.Function):
                 dres if (dres is not None and ctx.needs_input_grad[3]) else None, *([None] * 9))
 
 
+class _GradLinkFn(torch.autograd.Function):
+    """Identity whose backward hands its gradient to ``x``'s producing fused BN (the same
+    :class:`ResidualLink` an identity shortcut uses) instead of returning it to autograd."""
+
+    @staticmethod
+    def forward(ctx, x, link):
+        ctx.link = link
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        link = ctx.link
+        if link.dres is None:  # delivered: the producer adds it as dy2 inside its backward kernels
+            link.dres = g
+            return None, None
+        return g, None  # the link is taken (another consumer delivered): autograd adds this one
+
+
+def grad_link(x: torch.Tensor) -> torch.Tensor:
+    """``x`` for a second consumer branch whose gradient should be summed inside the backward of
+    the fused BN that produced ``x`` (one extra read there) rather than by autograd's add kernel
+    (two reads and a write of an activation). ResNet's downsample blocks feed their input to conv1
+    and to the downsample conv; with the link the two input gradients meet in the previous block's
+    bn3 backward. A tensor without a producing fused BN (or outside autograd) passes through."""
+    link = getattr(x, "_ptdt_res_link", None)
+    if link is None or not torch.is_grad_enabled() or not x.requires_grad:
+        return x
+    return _GradLinkFn.apply(x, link)
+
+
 def _tickets_of(bn, x):
     """The module's zeroed ticket array for the kernels' last-block hand-off (None: per-device one)."""
     t = getattr(bn, "_bn_tickets", None)

@@ -274,3 +274,56 @@ def test_residual_link_retain_graph_double_backward():
 
     for g2, g1 in zip(grads(True, 2), grads(False, 1)):
         torch.testing.assert_close(g2, 2 * g1, rtol=1e-4, atol=1e-5)
+
+
+def test_grad_link_delivers_branch_gradient_to_the_link():
+    """ops.norm.grad_link: the linked branch's gradient goes to the producer's ResidualLink
+    (summed later inside its backward kernels) instead of into autograd's sum."""
+    from pytorch_distributed_training_tutorials_amd.ops.norm import ResidualLink, grad_link
+
+    x = torch.randn(3, 4, requires_grad=True)
+    h = x * 1.0  # a non-leaf "producer output"
+    assert grad_link(h) is h  # no link: pass-through
+    h._ptdt_res_link = ResidualLink()
+    (h * 2.0).sum().backward(retain_graph=True)  # unlinked use only
+    torch.testing.assert_close(x.grad, torch.full((3, 4), 2.0))
+    x.grad = None
+    hl = grad_link(h)
+    ((h * 2.0).sum() + (hl * 3.0).sum()).backward()
+    torch.testing.assert_close(x.grad, torch.full((3, 4), 2.0))  # the linked branch is not in autograd's sum
+    torch.testing.assert_close(h._ptdt_res_link.dres, torch.full((3, 4), 3.0))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_grad_link_downsample_branch_matches_autograd_add(dtype):
+    """A fused BN's output consumed by two convolutions (a ResNet downsample block's conv1 and
+    downsample conv): with grad_link on one branch the two input gradients are summed inside
+    the producer BN's backward; gradients equal autograd's add (fp32) / are as close (bf16)."""
+    from pytorch_distributed_training_tutorials_amd.ops.norm import BatchNorm2d, grad_link
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    x0 = torch.randn(4, 64, 9, 7, device=dev).contiguous(memory_format=torch.channels_last)
+    r0 = torch.randn(4, 64, 9, 7, device=dev).contiguous(memory_format=torch.channels_last)
+    wa = torch.randn(32, 64, 1, 1, device=dev).contiguous(memory_format=torch.channels_last) * 0.2
+    wb = torch.randn(32, 64, 1, 1, device=dev).contiguous(memory_format=torch.channels_last) * 0.2
+
+    def grads(dt, link):
+        torch.manual_seed(1)
+        bn = BatchNorm2d(64).to(dev)
+        x = x0.to(dt).clone().requires_grad_(True)
+        y = bn(x, residual=r0.to(dt), relu=True)  # producer: a bn3 with residual (bit-mask path)
+        yb = grad_link(y) if link else y
+        out = torch.nn.functional.conv2d(y, wa.to(dt)) + 0.5 * torch.nn.functional.conv2d(yb, wb.to(dt))
+        (out.float() * torch.linspace(-1, 1, out.numel(), device=dev).view_as(out)).sum().backward()
+        return [t.grad.float().clone() for t in (x, bn.weight, bn.bias)]
+
+    if dtype == torch.float32:
+        for g0, g1 in zip(grads(dtype, False), grads(dtype, True)):
+            torch.testing.assert_close(g1, g0, rtol=1e-4, atol=1e-5)
+    else:
+        truth = grads(torch.float32, False)
+        for gt, g0, g1 in zip(truth, grads(dtype, False), grads(dtype, True)):
+            e0, e1 = (g0 - gt).norm().item(), (g1 - gt).norm().item()
+            assert e1 <= 1.5 * e0 + 1e-3 * gt.norm().item(), (e1, e0)
