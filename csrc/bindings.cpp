@@ -990,6 +990,113 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> weight, c10::op
   return {y, stats, mask};
 }
 
+// Training forward from precomputed statistics (conv1x1_bn_stats wrote stats = mean, invstd, scale,
+// shift and the running statistics): the apply pass only. Returns (y, mask).
+std::vector<Tensor> bn_fwd_apply(Tensor x, Tensor stats, c10::optional<Tensor> residual, bool relu, bool want_mask) {
+  int64_t M;
+  int C;
+  bn_rows(x, &M, &C);
+  c10::hip::HIPGuard guard(x.device().index());
+  TORCH_CHECK(stats.is_cuda() && stats.scalar_type() == at::kFloat && stats.is_contiguous() && stats.numel() == 4 * C,
+              "batchnorm: stats must be the [4, C] forward statistics");
+  BnFwdArgs a{};
+  a.x = x.data_ptr();
+  if (residual.has_value() && residual->defined()) {
+    same_rows(*residual, x, "residual");
+    a.residual = residual->data_ptr();
+  }
+  Tensor y = at::empty_like(x);
+  a.y = y.data_ptr();
+  a.dtype = dt_of(x);
+  a.M = M;
+  a.C = C;
+  a.relu = relu ? 1 : 0;
+  float* st = stats.data_ptr<float>();
+  a.p.mean = st;
+  a.p.invstd = st + C;
+  a.p.scale = st + 2 * C;
+  a.p.shift = st + 3 * C;
+  a.stats_ready = 1;
+  Tensor mask;
+  if (want_mask && relu && a.residual != nullptr) {
+    mask = at::empty({M * C / (x.scalar_type() == at::kFloat ? 4 : 8)}, x.options().dtype(at::kByte));
+    a.mask_out = mask.data_ptr<uint8_t>();
+  }
+  hip_check(bn_forward_train(a, cur_stream(x)), "bn_forward_apply");
+  return {y, mask};
+}
+
+// tile 0: the streaming kernel (conv1x1_bn.hip), else the tiled GEMM's block tile
+int64_t conv1x1_bn_num_tickets(int64_t M, int64_t N, int64_t tile, int64_t K) {
+  if (tile == 0) return conv1x1_bn_stream_num_tickets((int)M, (int)K, (int)N);
+  return gemm_bn_num_tickets((int)M, (int)N, (int)tile);
+}
+
+// 1x1 convolution (stride 1) + the training BatchNorm's batch statistics of its output:
+// y[M, N] = x[M, K] . w[N, K]^T in bf16 (x: the NHWC activation as rows, w: the [Cout, Cin] weight)
+// and stats [4, N] = mean, invstd, scale, shift; running statistics and num_batches_tracked updated.
+std::vector<Tensor> conv1x1_bn_stats(Tensor x, Tensor w, c10::optional<Tensor> weight, c10::optional<Tensor> bias,
+                                     c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var,
+                                     c10::optional<Tensor> num_batches_tracked, double momentum, double eps,
+                                     Tensor tickets, int64_t tile) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.device() == w.device(), "conv1x1_bn_stats: GPU operands");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "conv1x1_bn_stats: x [M, K], w [N, K]");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "conv1x1_bn_stats: bf16");
+  TORCH_CHECK(x.stride(1) == 1 && w.stride(1) == 1, "conv1x1_bn_stats: K-contiguous operands");
+  TORCH_CHECK(tile == 0 || tile == 128 || tile == 256, "conv1x1_bn_stats: tile 0 (streaming kernel), 128 or 256");
+  const int M = (int)x.size(0), N = (int)w.size(0), K = (int)x.size(1);
+  TORCH_CHECK(tile != 0 || (conv1x1_bn_stream_supported(K, N) && x.stride(0) == K && w.stride(0) == K),
+              "conv1x1_bn_stats: the streaming kernel has no (K, N) = (", K, ", ", N, ") instance");
+  TORCH_CHECK(x.size(0) < (1LL << 31) && N % 8 == 0, "conv1x1_bn_stats: N % 8 == 0");
+  TORCH_CHECK(gemm_bf16_big_supported(M, N, K, x.stride(0), w.stride(0), x.data_ptr(), w.data_ptr()),
+              "conv1x1_bn_stats: K % 64 == 0, 16-B aligned rows");
+  c10::hip::HIPGuard guard(x.device().index());
+  TORCH_CHECK(tickets.is_cuda() && tickets.device() == x.device() && tickets.scalar_type() == at::kInt &&
+                  tickets.is_contiguous() && tickets.numel() >= conv1x1_bn_num_tickets(M, N, tile, K),
+              "conv1x1_bn_stats: tickets must be a zeroed int32 tensor of >= ", conv1x1_bn_num_tickets(M, N, tile, K),
+              " elements");
+  Tensor y = at::empty({M, N}, x.options());
+  Tensor stats = at::empty({4, N}, x.options().dtype(at::kFloat));
+  Tensor ws = at::empty({tile == 0 ? conv1x1_bn_stream_ws_floats(M, K, N) : gemm_bn_ws_floats(M, N, (int)tile)},
+                        x.options().dtype(at::kFloat));
+  BigGemmArgs g{};
+  g.M = M, g.N = N, g.K = K;
+  g.A = x.data_ptr(), g.lda = x.stride(0);
+  g.Bt = w.data_ptr(), g.ldb = w.stride(0);
+  g.C = y.data_ptr(), g.ldc = N;
+  g.out_dtype = kBF16;
+  g.alpha = 1.f;
+  g.sched = 1;
+  g.tile = (int)tile;
+  g.split_k = 1;
+  GemmBnEpi e{};
+  e.ws = ws.data_ptr<float>();
+  e.tickets = tickets.data_ptr<int>();
+  e.p.weight = opt_f32(weight, N, "weight");
+  e.p.bias = opt_f32(bias, N, "bias");
+  e.p.running_mean = const_cast<float*>(opt_f32(running_mean, N, "running_mean"));
+  e.p.running_var = const_cast<float*>(opt_f32(running_var, N, "running_var"));
+  TORCH_CHECK((e.p.running_mean == nullptr) == (e.p.running_var == nullptr), "batchnorm: running_mean/var together");
+  if (num_batches_tracked.has_value() && num_batches_tracked->defined()) {
+    TORCH_CHECK(num_batches_tracked->is_cuda() && num_batches_tracked->scalar_type() == at::kLong &&
+                num_batches_tracked->numel() == 1, "batchnorm: num_batches_tracked must be a 1-element int64 tensor");
+    e.p.num_batches_tracked = num_batches_tracked->data_ptr<int64_t>();
+  }
+  e.p.momentum = (float)momentum;
+  e.p.eps = (float)eps;
+  float* st = stats.data_ptr<float>();
+  e.p.mean = st;
+  e.p.invstd = st + N;
+  e.p.scale = st + 2 * N;
+  e.p.shift = st + 3 * N;
+  if (tile == 0)
+    hip_check(conv1x1_bn_stream(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, K, N, e, cur_stream(x)),
+              "conv1x1_bn_stream");
+  else
+    hip_check(gemm_bn_stats(g, e, cur_stream(x)), "conv1x1_bn_stats");
+  return {y, stats};
+}
+
 // Backward: returns (dx, dweight, dbias, dres); dres undefined unless want_dres.
 std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::optional<Tensor> weight, Tensor stats,
                            bool relu, bool want_dres, bool want_dweight, c10::optional<Tensor> tickets,
@@ -1230,6 +1337,14 @@ PYBIND11_MODULE(_C, m) {
         py::arg("mask") = py::none());
   m.def("maxpool2d_fwd", &maxpool2d_fwd);
   m.def("maxpool2d_bwd", &maxpool2d_bwd);
+  m.def("bn_fwd_apply", &bn_fwd_apply, py::arg("x"), py::arg("stats"), py::arg("residual"), py::arg("relu"),
+        py::arg("want_mask"));
+  m.def("conv1x1_bn_stats", &conv1x1_bn_stats, py::arg("x"), py::arg("w"), py::arg("weight"), py::arg("bias"),
+        py::arg("running_mean"), py::arg("running_var"), py::arg("num_batches_tracked"), py::arg("momentum"),
+        py::arg("eps"), py::arg("tickets"), py::arg("tile") = 256);
+  m.def("conv1x1_bn_num_tickets", &conv1x1_bn_num_tickets, py::arg("M"), py::arg("N"), py::arg("tile") = 256,
+        py::arg("K") = 0);
+  m.def("conv1x1_bn_stream_supported", &conv1x1_bn_stream_supported, py::arg("K"), py::arg("N"));
   m.def("bn_apply", &bn_apply_, py::arg("x"), py::arg("residual"), py::arg("scale"), py::arg("shift"),
         py::arg("relu"));
 

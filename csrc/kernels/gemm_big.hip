@@ -263,24 +263,13 @@ __device__ __forceinline__ void store_tile_lds(const BigGemmArgs& g, const f32x4
 //          (vmcnt(0)) before the barrier closing slot 2t+1: its buffer's previous
 //          tile (t-1) was last read in slot 2t-1, and its first reader starts in
 //          slot 2t+2.
-template <class T, int OUT, int SCHED>
-__global__ void __launch_bounds__(T::NT) gemm_bf16_lds_kernel(BigGemmArgs g, int tm, int tn, int kt_per) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const int tile = xcd_remap(blockIdx.x, tm * tn);
-  const int bm = tile / tn, bn = tile % tn;
-  const int m0 = bm * T::BM, n0 = bn * T::BN;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid / T::WN, wc = wid % T::WN;
+// The K loop of one block tile (K-tiles kbase/BK .. +nk) into the wave's accumulators.
+template <class T, int SCHED>
+__device__ __forceinline__ void mainloop(f32x4_t (&acc)[T::FI][T::FJ], const BigGemmArgs& g, int m0, int n0, int nk,
+                                         int kbase, uint8_t* smem, int wid, int lane, int wr, int wc, int fr,
+                                         int fq) {
   const uint16_t* A = static_cast<const uint16_t*>(g.A);
   const uint16_t* Bt = static_cast<const uint16_t*>(g.Bt);
-  const int nk_all = g.K / BK;
-  const int kt_begin = blockIdx.y * kt_per;
-  const int nk = min(nk_all, kt_begin + kt_per) - kt_begin;  // >= 1 (host sizes the split)
-  const int kbase = kt_begin * BK;
-  const int fr = lane & 15, fq = lane >> 4;
-
-  f32x4_t acc[T::FI][T::FJ];
 #pragma unroll
   for (int i = 0; i < T::FI; ++i)
 #pragma unroll
@@ -358,6 +347,25 @@ __global__ void __launch_bounds__(T::NT) gemm_bf16_lds_kernel(BigGemmArgs g, int
       mfma_tile<T>(acc, f);
     }
   }
+}
+
+template <class T, int OUT, int SCHED>
+__global__ void __launch_bounds__(T::NT) gemm_bf16_lds_kernel(BigGemmArgs g, int tm, int tn, int kt_per) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tile = xcd_remap(blockIdx.x, tm * tn);
+  const int bm = tile / tn, bn = tile % tn;
+  const int m0 = bm * T::BM, n0 = bn * T::BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid / T::WN, wc = wid % T::WN;
+  const int nk_all = g.K / BK;
+  const int kt_begin = blockIdx.y * kt_per;
+  const int nk = min(nk_all, kt_begin + kt_per) - kt_begin;  // >= 1 (host sizes the split)
+  const int kbase = kt_begin * BK;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4_t acc[T::FI][T::FJ];
+  mainloop<T, SCHED>(acc, g, m0, n0, nk, kbase, smem, wid, lane, wr, wc, fr, fq);
 
   if constexpr (OUT == 2) {
     store_tile<T::FI, T::FJ, OUT>(g, acc, m0, n0, wr, wc, fr, fq);
@@ -366,6 +374,216 @@ __global__ void __launch_bounds__(T::NT) gemm_bf16_lds_kernel(BigGemmArgs g, int
     store_tile_lds<T::FI, T::FJ, OUT>(g, acc, m0, n0, wr, wc, fr, fq,
                                       reinterpret_cast<float*>(smem) + wid * epi_floats<T::FJ>());
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// 1x1 convolution + BatchNorm statistics (ops/convbn.py): the bf16 GEMM above on the NHWC
+// activation viewed as [M = N*H*W, Cin] against the [Cout, Cin] weight, whose epilogue also
+// produces the training BatchNorm's per-channel batch statistics of the bf16 output -- the
+// separate statistics pass over the conv output (one full read of it, bn_stats_kernel in
+// batchnorm.hip) disappears.
+//
+//   1. each wave reduces its FI*16-row x FJ*16-column sub-tile from the accumulators
+//      (bf16-rounded, exactly the stored values): per column the sum and the sum of squares
+//      about the wave's own column mean (two passes over registers, lanes combined with
+//      shuffles), written as one partial (row-disjoint, no atomics) per wave row;
+//   2. groups of G row tiles per column tile: the last workgroup of a group to finish (atomic
+//      ticket; partials handed over with sc1 stores/loads, see last_arrival) merges the group's partials in
+//      fixed order (Chan et al.'s pairwise update, in double) into one group partial;
+//   3. the last group of a column tile merges the group partials and writes mean, invstd,
+//      scale = w*invstd, shift = b - mean*scale (the [4, C] layout batchnorm.hip's backward
+//      reads), updates running_mean / running_var (unbiased) and num_batches_tracked.
+// Deterministic (fixed merge order whatever the arrival order) and robust for |mean| >> std
+// (centred partials). Tickets are re-armed by their last arriver for the next launch.
+__device__ __forceinline__ float bf16_round(float v) { return bf16_to_f32(f32_to_bf16(v)); }
+
+// (n, S, Q) <- (n, S, Q) merged with (np, Sp, Qp): S = sum, Q = sum of squares about the mean
+__device__ __forceinline__ void chan_merge(double& n, double& S, double& Q, double np, double Sp, double Qp) {
+  if (np <= 0.0) return;
+  if (n <= 0.0) {
+    n = np, S = Sp, Q = Qp;
+    return;
+  }
+  const double d = Sp / np - S / n;
+  Q += Qp + d * d * n * np / (n + np);
+  S += Sp;
+  n += np;
+}
+
+// Cross-workgroup hand-off of the statistics partials without L2 write-backs: every partial is
+// stored and loaded with sc1 (write-through / L1-bypassing agent-scope relaxed atomics), every
+// storing wave drains its stores (vmcnt(0)) before the workgroup barrier, then one lane adds to the
+// ticket and the add's returned value names the last arriver (MI355X_MICROARCH.md "Hand-offs
+// measured with sc1 loads", first row). An agent-scope release fence here would write back the
+// XCD L2's dirty lines -- the freshly stored output tiles -- once per workgroup: +110 us on a
+// 401408 x 256 conv (profiles/r3_convbn.md).
+typedef __attribute__((address_space(1))) float gfloat;
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store((gfloat*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load((gfloat*)p, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// true in exactly one workgroup per ticket (the count-th arriver); re-arms the ticket
+__device__ __forceinline__ bool last_arrival(int* ticket, int count, int* sh_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 partial stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == count - 1;
+    if (last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *sh_flag = last;
+  }
+  __syncthreads();
+  return *sh_flag != 0;
+}
+
+// Merge partials [p0, p1) (row counts from rows_of(p)) of this tile's BN columns; the NT/BN thread
+// groups take interleaved partials and are merged in group order through LDS. Result (n, S, Q)
+// valid in threads t < BN.
+template <class T, class RowsOf>
+__device__ __forceinline__ void merge_range(const float* wsS, const float* wsQ, int N, int n0, int p0, int p1,
+                                            RowsOf rows_of, double* sh, double& n, double& S, double& Q) {
+  constexpr int PARTS = T::NT / T::BN;
+  const int tid = threadIdx.x, col = tid % T::BN, part = tid / T::BN;
+  const int c = n0 + col;
+  n = S = Q = 0.0;
+  if (c < N) {
+    for (int p = p0 + part; p < p1; p += PARTS)
+      chan_merge(n, S, Q, (double)rows_of(p), (double)ld_sc1(wsS + (int64_t)p * N + c),
+                 (double)ld_sc1(wsQ + (int64_t)p * N + c));
+  }
+  __syncthreads();  // LDS scratch free
+  if (part > 0) {
+    sh[(part * 3 + 0) * T::BN + col] = n;
+    sh[(part * 3 + 1) * T::BN + col] = S;
+    sh[(part * 3 + 2) * T::BN + col] = Q;
+  }
+  __syncthreads();
+  if (part == 0) {
+#pragma unroll
+    for (int q = 1; q < PARTS; ++q)
+      chan_merge(n, S, Q, sh[(q * 3 + 0) * T::BN + col], sh[(q * 3 + 1) * T::BN + col],
+                 sh[(q * 3 + 2) * T::BN + col]);
+  }
+}
+
+template <class T, int SCHED>
+__global__ void __launch_bounds__(T::NT) gemm_bn_stats_kernel(BigGemmArgs g, GemmBnEpi e, int tm, int tn) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const int tile = xcd_remap(blockIdx.x, tm * tn);
+  const int bm = tile / tn, bn = tile % tn;
+  const int m0 = bm * T::BM, n0 = bn * T::BN;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid / T::WN, wc = wid % T::WN;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int N = g.N;
+
+  f32x4_t acc[T::FI][T::FJ];
+  mainloop<T, SCHED>(acc, g, m0, n0, g.K / BK, 0, smem, wid, lane, wr, wc, fr, fq);
+
+  // 1. wave partials: rows wrow0 .. wrow0 + FI*16 (nvalid of them inside M), columns of lane fr
+  constexpr int WROWS = T::FI * 16;
+  const int P = tm * T::WM;  // wave-row partials per column
+  const int wrow0 = m0 + wr * WROWS;
+  const int nvalid = max(0, min(g.M - wrow0, WROWS));
+  float s[T::FJ], q[T::FJ];
+#pragma unroll
+  for (int j = 0; j < T::FJ; ++j) {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < T::FI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (wrow0 + i * 16 + 4 * fq + r < g.M) a += bf16_round(acc[i][j][r]);
+    a += __shfl_xor(a, 16);
+    a += __shfl_xor(a, 32);
+    s[j] = a;
+  }
+  const float inv_n = nvalid > 0 ? 1.f / (float)nvalid : 0.f;
+#pragma unroll
+  for (int j = 0; j < T::FJ; ++j) {
+    const float mu = s[j] * inv_n;
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < T::FI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (wrow0 + i * 16 + 4 * fq + r < g.M) {
+          const float d = bf16_round(acc[i][j][r]) - mu;
+          a = fmaf(d, d, a);
+        }
+    a += __shfl_xor(a, 16);
+    a += __shfl_xor(a, 32);
+    q[j] = a;
+  }
+  float* wsS = e.ws;
+  float* wsQ = e.ws + (int64_t)P * N;
+  if (fq == 0) {
+    const int p = bm * T::WM + wr;
+#pragma unroll
+    for (int j = 0; j < T::FJ; ++j) {
+      const int c = n0 + wc * (T::FJ * 16) + j * 16 + fr;
+      if (c < N) {
+        st_sc1(wsS + (int64_t)p * N + c, s[j]);
+        st_sc1(wsQ + (int64_t)p * N + c, q[j]);
+      }
+    }
+  }
+
+  // the bf16 output tile (coalesced through LDS)
+  __builtin_amdgcn_s_barrier();  // every wave's fragment reads done: the LDS is scratch now
+  store_tile_lds<T::FI, T::FJ, 0>(g, acc, m0, n0, wr, wc, fr, fq,
+                                  reinterpret_cast<float*>(smem) + wid * epi_floats<T::FJ>());
+
+  // 2. group merge by the group's last row tile
+  double* sh = reinterpret_cast<double*>(smem);
+  int* flag = reinterpret_cast<int*>(smem + 3 * T::NT * sizeof(double));
+  const int G = e.group, ng = (tm + G - 1) / G;
+  const int gi = bm / G;
+  const int g_first = gi * G, g_count = min(G, tm - g_first);
+  __syncthreads();  // epilogue scratch reads done before the LDS is reused
+  if (!last_arrival(e.tickets + gi * tn + bn, g_count, flag)) return;
+  double n, S, Q;
+  auto wave_rows = [&](int p) { return max(0, min(g.M - (p / T::WM) * T::BM - (p % T::WM) * WROWS, WROWS)); };
+  merge_range<T>(wsS, wsQ, N, n0, g_first * T::WM, (g_first + g_count) * T::WM, wave_rows, sh, n, S, Q);
+  float* gS = e.ws + (int64_t)2 * P * N;
+  float* gQ = gS + (int64_t)ng * N;
+  {
+    const int c = n0 + tid;
+    if (tid < T::BN && c < N) {
+      st_sc1(gS + (int64_t)gi * N + c, (float)S);
+      st_sc1(gQ + (int64_t)gi * N + c, (float)Q);
+    }
+  }
+
+  // 3. column-tile merge by the last group, final coefficients
+  if (!last_arrival(e.tickets + ng * tn + bn, ng, flag)) return;
+  const int64_t grows = (int64_t)G * T::BM;
+  auto group_rows = [&](int p) { return (int)max((int64_t)0, min((int64_t)g.M - p * grows, grows)); };
+  merge_range<T>(gS, gQ, N, n0, 0, ng, group_rows, sh, n, S, Q);
+  const int c = n0 + tid;
+  if (tid < T::BN && c < N) {
+    const BnParams& p = e.p;
+    const double Md = (double)g.M;
+    const double mean = S / Md;
+    const double var = Q / Md > 0.0 ? Q / Md : 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)p.eps));
+    const float w = p.weight ? p.weight[c] : 1.f, b = p.bias ? p.bias[c] : 0.f;
+    p.mean[c] = (float)mean;
+    p.invstd[c] = invstd;
+    p.scale[c] = w * invstd;
+    p.shift[c] = b - (float)mean * w * invstd;
+    if (p.running_mean) {
+      const double unbiased = g.M > 1 ? var * Md / (Md - 1.0) : var;
+      p.running_mean[c] = (float)((1.0 - p.momentum) * p.running_mean[c] + p.momentum * mean);
+      p.running_var[c] = (float)((1.0 - p.momentum) * p.running_var[c] + p.momentum * unbiased);
+    }
+  }
+  if (tid == 0 && bn == 0 && e.p.num_batches_tracked) *e.p.num_batches_tracked += 1;
 }
 
 
@@ -575,7 +793,60 @@ hipError_t launch_out(const BigGemmArgs& g, int split, hipStream_t s) {
   return g.out_dtype == kF32 ? launch<T, 1, SCHED>(g, 1, s) : launch<T, 0, SCHED>(g, 1, s);
 }
 
+template <class T>
+constexpr int bn_lds_bytes() {
+  return lds_bytes<T>() > 3 * T::NT * 8 + 16 ? lds_bytes<T>() : 3 * T::NT * 8 + 16;
+}
+
+int bn_group(int tm) {
+  int G = 1;
+  while (G * G < tm) ++G;  // ceil(sqrt(tm)): group merges and the final merge read alike
+  return G;
+}
+
+template <class T>
+hipError_t launch_bn(const BigGemmArgs& g, GemmBnEpi e, hipStream_t s) {
+  const void* fn = reinterpret_cast<const void*>(&gemm_bn_stats_kernel<T, T::NT == 512 ? 1 : 0>);
+  constexpr int lds = bn_lds_bytes<T>();
+  static bool attr_set = false;
+  if (!attr_set) {
+    PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+    attr_set = true;
+  }
+  const int tm = (g.M + T::BM - 1) / T::BM, tn = (g.N + T::BN - 1) / T::BN;
+  e.group = bn_group(tm);
+  hipLaunchKernelGGL((gemm_bn_stats_kernel<T, T::NT == 512 ? 1 : 0>), dim3(tm * tn), dim3(T::NT), lds, s, g, e, tm,
+                     tn);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+int64_t gemm_bn_ws_floats(int M, int N, int tile) {
+  const int bm = tile == 128 ? 128 : 256, wm = 2;
+  const int tm = (M + bm - 1) / bm;
+  const int ng = (tm + bn_group(tm) - 1) / bn_group(tm);
+  return (int64_t)2 * N * ((int64_t)tm * wm + ng);
+}
+
+int gemm_bn_num_tickets(int M, int N, int tile) {
+  const int bm = tile == 128 ? 128 : 256;
+  const int tm = (M + bm - 1) / bm, tn = (N + bm - 1) / bm;
+  const int ng = (tm + bn_group(tm) - 1) / bn_group(tm);
+  return (ng + 1) * tn;
+}
+
+hipError_t gemm_bn_stats(const BigGemmArgs& g, GemmBnEpi e, hipStream_t s) {
+  if (!gemm_bf16_big_supported(g.M, g.N, g.K, g.lda, g.ldb, g.A, g.Bt)) return hipErrorInvalidValue;
+  if (g.out_dtype != kBF16 || g.split_k > 1 || g.ldc % 8 != 0 || e.ws == nullptr || e.tickets == nullptr ||
+      e.p.mean == nullptr || e.p.invstd == nullptr || e.p.scale == nullptr || e.p.shift == nullptr)
+    return hipErrorInvalidValue;
+  BigGemmArgs a = g;
+  a.alpha = 1.f, a.beta = 0.f, a.relu = 0, a.bias = nullptr;
+  if (g.tile == 128) return launch_bn<T128>(a, e, s);
+  if (g.tile == 256) return launch_bn<T256>(a, e, s);
+  return hipErrorInvalidValue;
+}
 
 bool gemm_bf16_big_supported(int M, int N, int K, int64_t lda, int64_t ldb, const void* A, const void* Bt) {
   return M > 0 && N > 0 && K >= BK && K % BK == 0 && lda % 8 == 0 && ldb % 8 == 0 &&

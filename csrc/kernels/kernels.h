@@ -328,7 +328,28 @@ struct BnFwdArgs {
   float* workspace; int* tickets;
   BnParams p;
   uint8_t* mask_out;  // relu + residual: the ReLU mask, one byte per 16-B vector (bit v: y > 0), or null
+  int stats_ready;    // p.scale/shift already hold this batch's coefficients (gemm_bn_stats): apply pass only
 };
+// 1x1 convolution + BatchNorm batch statistics (gemm_big.hip gemm_bn_stats): C = A . Bt^T in bf16
+// (bias/ReLU/beta unused) and the statistics of C's columns into p.mean/invstd/scale/shift, running
+// stats updated. ws: gemm_bn_ws_floats(); tickets: gemm_bn_num_tickets() zeroed ints (re-armed).
+struct GemmBnEpi {
+  float* ws;
+  int* tickets;
+  int group;  // row tiles per merge group (host: gemm_bn_stats fills it)
+  BnParams p;
+};
+int64_t gemm_bn_ws_floats(int M, int N, int tile);
+int gemm_bn_num_tickets(int M, int N, int tile);
+hipError_t gemm_bn_stats(const BigGemmArgs& g, GemmBnEpi e, hipStream_t s);
+// Streaming variant for the memory-bound shapes (conv1x1_bn.hip): X [M, K] and W [N, K] bf16 with
+// unit row strides K, Y [M, N] bf16; supported (K, N) pairs only; ws / tickets sized by the helpers.
+bool conv1x1_bn_stream_supported(int K, int N);
+int64_t conv1x1_bn_stream_ws_floats(int M, int K, int N);
+int conv1x1_bn_stream_num_tickets(int M, int K, int N);
+hipError_t conv1x1_bn_stream(const void* X, const void* W, void* Y, int M, int K, int N, GemmBnEpi e,
+                             hipStream_t s);
+
 struct BnBwdParams {
   const float* weight; const float* mean; const float* invstd;
   const float* scale; const float* shift;   // forward scale/shift: ReLU mask from x when y is null

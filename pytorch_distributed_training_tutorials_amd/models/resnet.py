@@ -21,6 +21,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.conv import Conv2d
+from ..ops.convbn import conv_bn_act
 from ..ops.linear import Linear
 from ..ops.norm import BatchNorm2d, MaxPool2d, grad_link
 
@@ -64,14 +65,21 @@ class Bottleneck(nn.Module):
         self.downsample = downsample
         self.stride = stride
 
+    def _down(self, x):
+        ds = self.downsample
+        if isinstance(ds, nn.Sequential) and len(ds) == 2 and isinstance(ds[0], nn.Conv2d):
+            return conv_bn_act(ds[0], ds[1], x)  # stride 1 (layer1): BN statistics in the conv epilogue
+        return ds(x)
+
     def forward(self, x):
         # downsample block: x feeds conv1 and the downsample conv; the downsample branch's input
         # gradient is summed inside the producing BN's backward (ops.norm.grad_link), not by autograd
-        identity = x if self.downsample is None else self.downsample(grad_link(x))
-        out = bn_act(self.bn1, self.conv1(x), relu=True)
+        identity = x if self.downsample is None else self._down(grad_link(x))
+        # 1x1 convs: the BN statistics come from the GEMM epilogue (ops.convbn) where it applies
+        out = conv_bn_act(self.conv1, self.bn1, x, relu=True)
         out = bn_act(self.bn2, self.conv2(out), relu=True)
         # identity shortcut: the residual gradient goes straight into the producing BN's backward
-        return bn_act(self.bn3, self.conv3(out), residual=identity, relu=True, link=self.downsample is None)
+        return conv_bn_act(self.conv3, self.bn3, out, residual=identity, relu=True, link=self.downsample is None)
 
 
 class ResNet(nn.Module):

@@ -1,0 +1,126 @@
+"""1x1 convolution + training BatchNorm with the statistics computed in the convolution's
+epilogue: ``ReLU?(BN(conv1x1(x)) + residual?)``.
+
+A stride-1 1x1 convolution over an NHWC (channels_last) activation is a GEMM,
+``Y[N*H*W, Cout] = X[N*H*W, Cin] . W[Cout, Cin]^T``, with both operands already
+K-contiguous in memory. ``gemm_bn_stats`` (csrc/kernels/gemm_big.hip) runs that
+GEMM on the LDS-DMA MFMA kernel and, while the output tile is still in registers,
+reduces it to per-channel sums and centred sums of squares; row-tile partials are
+merged in fixed order by the last workgroups to finish (two ticket levels), which
+also write the BN coefficients and update the running statistics. The BN then
+runs only its apply pass (``bn_fwd_apply``): the separate statistics pass -- a full
+read of the conv output -- is gone. In torchvision's ResNet-50 that is every bn1
+and bn3 and the layer1 downsample BN (bf16, batch 128: ~0.75 ms of statistics
+passes per step, profiles/r3_bn_kernels.md).
+
+Backward is unchanged: the BN's native backward, then the convolution's data and
+weight gradients on MIOpen (``aten.convolution_backward``, as autograd would
+call it). Forward numerics: the statistics are those of the stored bf16 output
+(what the separate pass would read), merged in double.
+
+Anything else -- stride 2, eval mode, fp32, NCHW, odd channel counts, CPU --
+takes the unfused ``bn_act(bn, conv(x))``. ``PTDT_CONVBN=0`` disables the fusion.
+
+Reference call sites: the Bottleneck convolutions + BatchNorms of torchvision's
+ResNet-50 (NB03:560-570, NB03:807-833).
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.nn as nn
+
+from .._ext import native
+from .conv import cast_weight
+from .norm import BatchNorm2d, batch_norm_act
+
+_ENABLED = os.environ.get("PTDT_CONVBN", "1") != "0"
+
+
+_STREAM = os.environ.get("PTDT_CONVBN_STREAM", "1") != "0"
+
+
+def _tile(M: int, N: int, K: int) -> int:
+    """0: the streaming kernel (memory-bound (K, N) instances: weights resident in LDS); else the
+    tiled GEMM's block tile: 256x256 when those tiles fill the chip (>= 192 of them), else 128x128."""
+    if _STREAM and native().conv1x1_bn_stream_supported(K, N):
+        return 0
+    return 256 if (-(-M // 256)) * (-(-N // 256)) >= 192 else 128
+
+
+class _Conv1x1StatsFn(torch.autograd.Function):
+    """y = conv1x1(x, w) (NHWC bf16) and the [4, Cout] BN statistics of y (non-differentiable)."""
+
+    @staticmethod
+    def forward(ctx, x, w, bn_weight, bn_bias, running_mean, running_var, nbt, momentum: float, eps: float,
+                tickets, tile: int):
+        n, cin, h, wd = x.shape
+        cout = w.shape[0]
+        x2 = x.permute(0, 2, 3, 1).reshape(n * h * wd, cin)  # channels_last storage: a view
+        y2, stats = native().conv1x1_bn_stats(x2, w.reshape(cout, cin), bn_weight, bn_bias, running_mean,
+                                              running_var, nbt, momentum, eps, tickets, tile)
+        ctx.save_for_backward(x, w)
+        ctx.mark_non_differentiable(stats)
+        return y2.view(n, h, wd, cout).permute(0, 3, 1, 2), stats
+
+    @staticmethod
+    def backward(ctx, gy, _gstats):
+        x, w = ctx.saved_tensors
+        gy = gy.contiguous(memory_format=torch.channels_last)
+        mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False]
+        dx, dw, _ = torch.ops.aten.convolution_backward(gy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
+                                                        mask)
+        return dx, dw, *([None] * 9)
+
+
+def _fusable(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual) -> bool:
+    if not (_ENABLED and isinstance(bn, BatchNorm2d) and bn.training and bn.momentum is not None):
+        return False
+    if not (isinstance(conv, nn.Conv2d) and conv.kernel_size == (1, 1) and conv.stride == (1, 1)
+            and conv.padding == (0, 0) and conv.dilation == (1, 1) and conv.groups == 1 and conv.bias is None
+            and conv.padding_mode == "zeros"):
+        return False
+    if not (x.is_cuda and x.dim() == 4 and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16 and x.dtype == torch.bfloat16
+            and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0):
+        return False
+    cin, cout = conv.in_channels, conv.out_channels
+    if cin % 64 or cout % 8 or x.shape[0] * x.shape[2] * x.shape[3] >= 2 ** 31:
+        return False
+    if residual is not None:  # the BN's native path needs the residual in the output's layout
+        n, _, h, w = x.shape
+        if not (residual.dtype == torch.bfloat16 and tuple(residual.shape) == (n, cout, h, w)
+                and residual.is_contiguous(memory_format=torch.channels_last) and residual.data_ptr() % 16 == 0):
+            return False
+    return True
+
+
+def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: torch.Tensor | None = None,
+                relu: bool = False, link: bool = False) -> torch.Tensor:
+    """``ReLU?(bn(conv(x)) + residual)``; a stride-1 1x1 ``conv`` feeding an ops.norm.BatchNorm2d in
+    training under bf16 autocast computes the BN statistics in its GEMM epilogue."""
+    if not _fusable(conv, bn, x, residual):
+        from ..models.resnet import bn_act
+
+        return bn_act(bn, conv(x), residual, relu, link)
+    w = cast_weight(conv.weight)
+    track = bn.track_running_stats
+    M = x.shape[0] * x.shape[2] * x.shape[3]
+    tile = _tile(M, conv.out_channels, conv.in_channels)
+    tickets = bn._gemm_tickets
+    need = native().conv1x1_bn_num_tickets(M, conv.out_channels, tile, conv.in_channels)
+    if tickets.numel() < need or tickets.device != x.device:
+        raise RuntimeError(f"conv_bn_act: BN ticket buffer too small ({tickets.numel()} < {need}) or off-device")
+    y, stats = _Conv1x1StatsFn.apply(x, w, bn.weight, bn.bias, bn.running_mean if track else None,
+                                     bn.running_var if track else None, bn.num_batches_tracked if track else None,
+                                     float(bn.momentum), float(bn.eps), tickets, tile)
+    return batch_norm_act(y, bn, residual, relu, link, stats=stats)
+
+
+def conv1x1_stats_probe(x2: torch.Tensor, w2: torch.Tensor, tile: int | None = None):
+    """Callable running the fused GEMM + statistics kernel alone on [M, K] x [N, K]^T (benchmarks)."""
+    M, N, K = x2.shape[0], w2.shape[0], x2.shape[1]
+    t = _tile(M, N, K) if tile is None else tile
+    tickets = torch.zeros(native().conv1x1_bn_num_tickets(M, N, t, K), dtype=torch.int32, device=x2.device)
+    return lambda: native().conv1x1_bn_stats(x2, w2, None, None, None, None, None, 0.1, 1e-5, tickets, t)

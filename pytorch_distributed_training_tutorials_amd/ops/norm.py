@@ -66,12 +66,16 @@ class ResidualLink:
 class _BatchNormActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, relu: bool, momentum: float,
-                eps: float, tickets, link_in, link_out):
+                eps: float, tickets, link_in, link_out, stats_in=None):
         # with a residual the ReLU mask travels as bits (one byte per 16-B vector, 1/16 of y in
         # bf16); without one it is recomputed from x and the saved scale/shift (bit-exact)
         want_mask = relu and residual is not None
-        y, stats, mask = native().bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, residual, relu,
-                                               momentum, eps, tickets, want_mask)
+        if stats_in is not None:  # statistics from the producing 1x1 conv's epilogue (ops/convbn.py)
+            stats = stats_in
+            y, mask = native().bn_fwd_apply(x, stats, residual, relu, want_mask)
+        else:
+            y, stats, mask = native().bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, residual, relu,
+                                                   momentum, eps, tickets, want_mask)
         ctx.tickets = tickets
         ctx.params = (weight, bias)
         ctx.relu = relu
@@ -105,7 +109,7 @@ class _BatchNormActFn(torch.autograd.Function):
         if link_in is not None:  # delivered to the residual's producer instead of autograd
             link_in.dres, dres = dres, None
         return (dx if ctx.needs_input_grad[0] else None, dw if want_dw else None, db if want_dw else None,
-                dres if (dres is not None and ctx.needs_input_grad[3]) else None, *([None] * 9))
+                dres if (dres is not None and ctx.needs_input_grad[3]) else None, *([None] * 10))
 
 
 class _GradLinkFn(torch.autograd.Function):
@@ -147,13 +151,17 @@ def _tickets_of(bn, x):
 
 
 def batch_norm_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: torch.Tensor | None = None,
-                   relu: bool = False, link: bool = False) -> torch.Tensor:
+                   relu: bool = False, link: bool = False, stats: torch.Tensor | None = None) -> torch.Tensor:
     """``ReLU?(bn(x) + residual)`` with ``bn``'s parameters, buffers and train/eval mode.
 
     ``link=True``: when ``residual`` is the output of another fused BN, its gradient
     is handed to that BN's backward kernels (:class:`ResidualLink`) instead of being
     added to the residual's other gradients by autograd. Only for a residual whose
-    producer is a fused BN (a ResNet identity shortcut)."""
+    producer is a fused BN (a ResNet identity shortcut).
+
+    ``stats``: this batch's [4, C] statistics (mean, invstd, scale, shift) already computed --
+    and the running statistics already updated -- by the kernel that produced ``x``
+    (ops/convbn.py); only the apply pass runs. Training mode, native layout only."""
     fast = _rows_layout_ok(x) and (residual is None or (residual.dtype == x.dtype and residual.shape == x.shape
                                                         and residual.stride() == x.stride()
                                                         and residual.data_ptr() % 16 == 0))
@@ -164,10 +172,13 @@ def batch_norm_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residua
         link_out = ResidualLink() if torch.is_grad_enabled() else None
         y = _BatchNormActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean if track else None,
                                   bn.running_var if track else None, bn.num_batches_tracked if track else None,
-                                  relu, float(bn.momentum), float(bn.eps), _tickets_of(bn, x), link_in, link_out)
+                                  relu, float(bn.momentum), float(bn.eps), _tickets_of(bn, x), link_in, link_out,
+                                  stats)
         if link_out is not None:
             y._ptdt_res_link = link_out
         return y
+    if stats is not None:
+        raise RuntimeError("batch_norm_act: precomputed statistics need the native training path")
     needs_grad = torch.is_grad_enabled() and (x.requires_grad or (residual is not None and residual.requires_grad))
     if fast and not use_batch_stats and not needs_grad:  # eval: one launch with the running statistics
         scale = torch.rsqrt(bn.running_var.float() + bn.eps)
@@ -201,6 +212,9 @@ class BatchNorm2d(nn.BatchNorm2d):
         # channel tile (>= 32 channels); non-persistent: not part of the state_dict
         self.register_buffer("_bn_tickets", torch.zeros(max(1, -(-num_features // 32)), dtype=torch.int32),
                              persistent=False)
+        # tickets of the statistics merge when a 1x1 conv's epilogue computes this BN's statistics
+        # (ops/convbn.py; (merge groups + 1) x column tiles, re-armed in-kernel)
+        self.register_buffer("_gemm_tickets", torch.zeros(1024, dtype=torch.int32), persistent=False)
 
     def forward(self, x, residual=None, relu: bool = False, link: bool = False):
         self._check_input_dim(x)

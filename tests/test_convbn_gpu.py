@@ -1,0 +1,164 @@
+"""1x1 convolution with the BatchNorm statistics in its GEMM epilogue (ops/convbn.py,
+csrc/kernels/gemm_big.hip gemm_bn_stats) vs fp32 PyTorch references: the GEMM output,
+the per-channel batch statistics of the stored bf16 output, the BN coefficients and
+running statistics; determinism; and the fused Bottleneck / ResNet-50 training step
+against the unfused path (separate statistics pass) it replaces."""
+import pytest
+import torch
+import torch.nn as nn
+
+pytestmark = pytest.mark.gpu
+
+# (M, K, N): ResNet-50 shapes at small batch, edge tiles (M % 256 != 0), several column tiles
+KSHAPES = [(6272, 512, 2048), (3136, 64, 256), (1000, 256, 64), (25088, 1024, 256), (300, 128, 520),
+           (777, 64, 8), (777, 64, 64), (12544, 256, 128), (100000, 64, 256)]
+
+
+def _ref_stats(y: torch.Tensor):
+    yf = y.float()
+    mean = yf.mean(0, dtype=torch.float64)
+    var = ((yf.double() - mean) ** 2).mean(0)
+    return mean, var
+
+
+@pytest.mark.parametrize("M,K,N", KSHAPES)
+@pytest.mark.parametrize("tile", [0, 128, 256])
+def test_gemm_bn_stats_matches_reference(native, dev, M, K, N, tile):
+    """tile 0: the streaming kernel (conv1x1_bn.hip), 128 / 256: the tiled GEMM (gemm_big.hip)."""
+    if tile == 0 and not native.conv1x1_bn_stream_supported(K, N):
+        pytest.skip("no streaming instance for this (K, N)")
+    if tile != 0 and M > 50000:
+        pytest.skip("large-M case is for the streaming kernel")
+    g = torch.Generator(device=dev).manual_seed(M + N + tile)
+    x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
+    weight = torch.rand(N, device=dev, generator=g) + 0.5
+    bias = torch.randn(N, device=dev, generator=g)
+    rm, rv = torch.randn(N, device=dev, generator=g), torch.rand(N, device=dev, generator=g) + 0.5
+    rm0, rv0 = rm.clone(), rv.clone()
+    nbt = torch.zeros((), dtype=torch.long, device=dev)
+    tickets = torch.zeros(native.conv1x1_bn_num_tickets(M, N, tile, K), dtype=torch.int32, device=dev)
+    y, stats = native.conv1x1_bn_stats(x, w, weight, bias, rm, rv, nbt, 0.1, 1e-5, tickets, tile)
+    ref = x.float() @ w.float().t()
+    assert y.dtype == torch.bfloat16 and y.shape == (M, N)
+    torch.testing.assert_close(y.float(), ref, rtol=1e-2, atol=1e-2)
+    mean, var = _ref_stats(y)  # statistics of the stored bf16 values
+    torch.testing.assert_close(stats[0].double(), mean, rtol=1e-5, atol=1e-5)
+    invstd = 1.0 / torch.sqrt(var + 1e-5)
+    torch.testing.assert_close(stats[1].double(), invstd, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(stats[2], (weight.double() * invstd).float(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(stats[3], (bias.double() - mean * weight.double() * invstd).float(), rtol=1e-5,
+                               atol=1e-5)
+    torch.testing.assert_close(rm, (0.9 * rm0.double() + 0.1 * mean).float(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(rv, (0.9 * rv0.double() + 0.1 * var * M / (M - 1)).float(), rtol=1e-5, atol=1e-6)
+    assert int(nbt) == 1
+    assert int(tickets.abs().sum()) == 0  # re-armed for the next launch
+
+
+@pytest.mark.parametrize("tile,M,K,N", [(256, 25088, 256, 512), (0, 25088, 64, 256), (0, 25088, 256, 128)])
+def test_gemm_bn_stats_deterministic_and_offset_robust(native, dev, tile, M, K, N):
+    """|mean| >> std per channel (a constant input column carrying a large weight): the centred
+    partials (tiled) / the running-mean pivot (streaming: here 0.9x the batch mean, as a lagging
+    running mean would be) keep the variance; two launches agree bitwise."""
+    g = torch.Generator(device=dev).manual_seed(7)
+    x = torch.randn(M, K, device=dev, generator=g) * 0.01
+    x[:, 0] = 1.0
+    w = torch.randn(N, K, device=dev, generator=g) * 0.05
+    w[:, 0] = 64.0 + torch.arange(N, device=dev) % 7
+    x, w = x.to(torch.bfloat16), w.to(torch.bfloat16)
+    mean, var = _ref_stats((x.float() @ w.float().t()).to(torch.bfloat16))
+    rm1, rv1 = (0.9 * mean).float(), torch.ones(N, device=dev)
+    rm2, rv2 = rm1.clone(), rv1.clone()
+    tickets = torch.zeros(native.conv1x1_bn_num_tickets(M, N, tile, K), dtype=torch.int32, device=dev)
+    y1, s1 = native.conv1x1_bn_stats(x, w, None, None, rm1, rv1, None, 0.1, 1e-5, tickets, tile)
+    y2, s2 = native.conv1x1_bn_stats(x, w, None, None, rm2, rv2, None, 0.1, 1e-5, tickets, tile)
+    assert torch.equal(y1, y2) and torch.equal(s1, s2) and torch.equal(rm1, rm2)
+    mean, var = _ref_stats(y1)
+    assert float(mean.abs().min()) > 30 * float(var.sqrt().max())  # the regime the centring is for
+    torch.testing.assert_close(s1[1].double(), 1.0 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=0)
+
+
+def _block_pair(dev, inplanes, planes, downsample):
+    from pytorch_distributed_training_tutorials_amd.models.resnet import Bottleneck, conv1x1
+    from pytorch_distributed_training_tutorials_amd.ops.norm import BatchNorm2d
+
+    torch.manual_seed(3)
+    ds = nn.Sequential(conv1x1(inplanes, planes * 4), BatchNorm2d(planes * 4)) if downsample else None
+    a = Bottleneck(inplanes, planes, downsample=ds).to(dev).to(memory_format=torch.channels_last)
+    for m in a.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            nn.init.uniform_(m.weight, 0.5, 1.5)
+            nn.init.uniform_(m.bias, -0.2, 0.2)
+    import copy
+
+    return a, copy.deepcopy(a)
+
+
+@pytest.mark.parametrize("inplanes,planes,downsample", [(256, 64, False), (64, 64, True)])
+def test_bottleneck_fused_matches_unfused(dev, monkeypatch, inplanes, planes, downsample):
+    """Same block, same input: conv+BN fused (statistics from the GEMM epilogue) vs the unfused
+    path (MIOpen conv + the BN's own statistics pass) -- outputs, every gradient, running stats."""
+    from pytorch_distributed_training_tutorials_amd.ops import convbn
+
+    fused, plain = _block_pair(dev, inplanes, planes, downsample)
+    x = torch.randn(8, inplanes, 28, 28, device=dev).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    outs, grads = [], []
+    for blk, on in ((fused, True), (plain, False)):
+        monkeypatch.setattr(convbn, "_ENABLED", on)
+        xi = x.clone().requires_grad_()
+        with torch.autocast("cuda", torch.bfloat16):
+            y = blk(xi)
+        (y.float() ** 2).mean().backward()
+        outs.append(y.float())
+        grads.append([xi.grad.float()] + [p.grad.float() for p in blk.parameters()])
+    torch.testing.assert_close(outs[0], outs[1], rtol=2e-2, atol=2e-2)
+    for ga, gb in zip(*grads):
+        scale = max(float(gb.abs().max()), 1e-6)
+        assert float((ga - gb).abs().max()) / scale < 3e-2
+    for (na, a), (nb, b) in zip(fused.named_buffers(), plain.named_buffers()):
+        if "tickets" in na:
+            assert int(a.abs().sum()) == 0, na
+        elif a.dtype == torch.long:
+            assert torch.equal(a, b), na
+        else:
+            torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3, msg=na)
+
+
+def test_resnet50_step_uses_fused_kernels(dev, monkeypatch):
+    """ResNet-50 training forward at batch 4 under bf16 autocast: the fused path is taken for
+    every stride-1 1x1 conv (bn1, bn3 and layer1's downsample: 33 of 53 BNs), and the loss and
+    parameter gradients agree with the unfused model."""
+    import copy
+
+    from pytorch_distributed_training_tutorials_amd.models.resnet import resnet50
+    from pytorch_distributed_training_tutorials_amd.ops import convbn
+
+    torch.manual_seed(0)
+    m1 = resnet50(num_classes=10).to(dev).to(memory_format=torch.channels_last)
+    m2 = copy.deepcopy(m1)
+    calls = {"n": 0}
+    real = convbn._Conv1x1StatsFn.apply
+
+    def counted(*a):
+        calls["n"] += 1
+        return real(*a)
+
+    # batch 4 at 96x96: layer4's BNs still normalise over only 36 rows, so bf16 rounding differences
+    # between the two conv implementations move the loss by ~1 %
+    x = torch.randn(4, 3, 96, 96, device=dev).contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (4,), device=dev)
+    losses = []
+    for m, on in ((m1, True), (m2, False)):
+        monkeypatch.setattr(convbn, "_ENABLED", on)
+        monkeypatch.setattr(convbn._Conv1x1StatsFn, "apply", counted)
+        with torch.autocast("cuda", torch.bfloat16):
+            loss = nn.functional.cross_entropy(m(x).float(), t)
+        loss.backward()
+        losses.append(float(loss.detach()))
+    assert calls["n"] == 33
+    assert abs(losses[0] - losses[1]) < 5e-2 * max(1.0, abs(losses[1]))
+    g1 = torch.cat([p.grad.flatten().float() for p in m1.parameters()])
+    g2 = torch.cat([p.grad.flatten().float() for p in m2.parameters()])
+    cos = float(torch.nn.functional.cosine_similarity(g1, g2, dim=0))
+    assert cos > 0.99, cos

@@ -184,3 +184,21 @@ def test_fused_adam_state_dict_resume_and_torch_interchange():
         run(cls, 2, b, sd)
         for x, y in zip(b, ref):
             torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6)
+
+
+def test_conv_bn_act_falls_back_off_gpu():
+    """ops.convbn.conv_bn_act on CPU tensors is exactly the unfused bn_act(bn, conv(x))."""
+    import copy
+
+    from pytorch_distributed_training_tutorials_amd.models.resnet import bn_act, conv1x1
+    from pytorch_distributed_training_tutorials_amd.ops.convbn import _fusable, conv_bn_act
+    from pytorch_distributed_training_tutorials_amd.ops.norm import BatchNorm2d
+
+    torch.manual_seed(0)
+    conv, bn = conv1x1(64, 32), BatchNorm2d(32)
+    conv2, bn2 = copy.deepcopy(conv), copy.deepcopy(bn)
+    x = torch.randn(2, 64, 5, 5)
+    assert not _fusable(conv, bn, x, None)
+    y = conv_bn_act(conv, bn, x, relu=True)
+    torch.testing.assert_close(y, bn_act(bn2, conv2(x), relu=True))
+    torch.testing.assert_close(bn.running_var, bn2.running_var)
