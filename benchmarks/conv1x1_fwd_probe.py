@@ -34,6 +34,8 @@ def main():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--sweep", action="store_true",
+                    help="streaming kernel only: time every pipeline configuration (PTDT_C1_CFG 0-3) per shape")
     a = ap.parse_args()
     torch.backends.cudnn.benchmark = True
     from pytorch_distributed_training_tutorials_amd._ext import native
@@ -42,6 +44,27 @@ def main():
     C = native()
     dev = torch.device("cuda", 0)
     tot = {}
+    if a.sweep:
+        from pytorch_distributed_training_tutorials_amd.ops.convbn import conv1x1_stats_probe
+
+        for hw, cin, cout, cnt in SHAPES:
+            if not C.conv1x1_bn_stream_supported(cin, cout):
+                continue
+            M = a.batch * hw * hw
+            x2 = torch.randn(M, cin, device=dev).to(torch.bfloat16)
+            w2 = (torch.randn(cout, cin, device=dev) * 0.05).to(torch.bfloat16)
+            rec = {"H": hw, "Cin": cin, "Cout": cout, "M": M, "per_step": cnt}
+            res = {}
+            for _ in range(a.rounds):
+                for cfg in range(4):
+                    os.environ["PTDT_C1_CFG"] = str(cfg)
+                    res.setdefault(cfg, []).append(timed(conv1x1_stats_probe(x2, w2, 0)))
+            os.environ.pop("PTDT_C1_CFG")
+            for cfg, ts in res.items():
+                rec[f"cfg{cfg}_us"] = round(statistics.median(ts), 1)
+            rec["GBps_cfg0"] = round(2 * M * (cin + cout) / (rec["cfg0_us"] * 1e-6) / 1e9)
+            print(json.dumps(rec), flush=True)
+        return
     for hw, cin, cout, cnt in SHAPES:
         M = a.batch * hw * hw
         x4 = torch.randn(a.batch, cin, hw, hw, device=dev, dtype=torch.bfloat16).contiguous(

@@ -31,6 +31,8 @@ namespace {
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 typedef __attribute__((address_space(3))) void lds_void;
 typedef __attribute__((address_space(1))) const void gbl_void;
 typedef __attribute__((address_space(1))) float gfloat;
@@ -94,13 +96,16 @@ __device__ __forceinline__ float row_bcast(const float (&r)[R]) {
                                                                0x150 + (I & 15), 0xF, 0xF, false));
 }
 
-template <int K, int N, int NW>
+template <int K, int N, int NW, int NB>
 struct C1 {
   static constexpr int NT = NW * 64;
   static constexpr int BM = 16 * NW;         // rows per block (16 per wave)
   static constexpr int WB = N * K * 2;       // resident weights
   static constexpr int AB = BM * K * 2;      // one X block
-  static constexpr int NBUF = WB + 3 * AB <= 160 * 1024 ? 3 : 2;  // X blocks in flight + 1
+  // X blocks in flight + 1: NB, or fewer where the LDS does not hold them
+  static constexpr int NBUF = WB + NB * AB <= 160 * 1024 ? NB : (WB + 3 * AB <= 160 * 1024 ? 3 : 2);
+  // workgroups per CU: two waves per SIMD (the register budget), and the LDS
+  static constexpr int PER_CU = (8 / NW) * (WB + NBUF * AB) <= 160 * 1024 ? 8 / NW : 1;
   static constexpr int DMA = AB / (NT * 16); // LDS-DMAs per thread per block
   static constexpr int NP = N / 32;          // channel pairs (2 col-frags, 32 channels)
   static constexpr int KS = K / 32;          // MFMA k-steps
@@ -109,18 +114,19 @@ struct C1 {
   static constexpr int CP = CH / 32;            // pairs per chunk
   static constexpr int PR = (8 * NP + 15) / 16; // pivot registers per lane (see below)
   static_assert(AB % (NT * 16) == 0 && N % 32 == 0 && K % 64 == 0, "shape");
-  static_assert(LDS <= 160 * 1024, "LDS");
+  static constexpr bool FITS = LDS <= 160 * 1024;  // dispatch() only launches configurations that fit
 };
 
 // weight row of col-frag j's MFMA row fr (see the header): channel 32p + 8(fr/4) + 4(j%2) + fr%4
 __device__ __forceinline__ int w_channel(int j, int fr) { return 32 * (j >> 1) + 8 * (fr >> 2) + 4 * (j & 1) + (fr & 3); }
 
-template <int K, int N, int NW>
+template <int K, int N, int NW, int NB>
 __global__ void __launch_bounds__(NW * 64, 2) conv1x1_bn_stream_kernel(const uint16_t* __restrict__ X,
                                                                        const uint16_t* __restrict__ W,
                                                                        uint16_t* __restrict__ Y, int M,
                                                                        GemmBnEpi e, int nblk) {
-  using S = C1<K, N, NW>;
+  using S = C1<K, N, NW, NB>;
+  static_assert(S::FITS, "LDS");
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* wl = smem;
   uint8_t* al = smem + S::WB;
@@ -182,9 +188,9 @@ __global__ void __launch_bounds__(NW * 64, 2) conv1x1_bn_stream_kernel(const uin
     // retire block t: issued after its DMAs are the stores of blocks t-D .. t-1 (NP each per thread)
     // and the DMAs of the blocks t+1 .. t+D that exist (blocks < D were drained in the prologue)
     const int ahead = min(D, nt - 1 - t);
-    if (ahead == D) vm_wait<D * S::NP + D * S::DMA>();
-    else if (ahead == D - 1) vm_wait<D * S::NP + (D - 1) * S::DMA>();
-    else vm_wait<D * S::NP>();  // ahead == 0 < D - 1 (D = 2)
+    static_for<0, D + 1>([&](auto ac) {
+      if (ahead == decltype(ac)::value) vm_wait<D * S::NP + decltype(ac)::value * S::DMA>();
+    });
     bar();  // every wave's part of block t is in LDS
     const uint8_t* at = al + (t % S::NBUF) * S::AB;
     bf16x8_t xb[S::KS];
@@ -212,21 +218,28 @@ __global__ void __launch_bounds__(NW * 64, 2) conv1x1_bn_stream_kernel(const uin
       static_for<0, S::CP>([&](auto ppc) {
         constexpr int pp = decltype(ppc)::value;
         constexpr int p = ch * S::CP + pp;
-        uint32_t h[8];
+        uint32_t h2[4];  // bf16 pairs: v_cvt_pk_bf16_f32 (gfx950, round to nearest even)
+        static_for<0, 4>([&](auto qc) {
+          constexpr int q2 = decltype(qc)::value;
+          const auto& a = acc[2 * pp + (q2 >> 1)];
+          const f32x2_t f = {a[(2 * q2) & 3], a[(2 * q2 + 1) & 3]};
+          h2[q2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2_t));
+        });
         static_for<0, 8>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
-          const float v = q < 4 ? acc[2 * pp][q & 3] : acc[2 * pp + 1][q & 3];
-          h[q] = f32_to_bf16(v);
-          // pivot of channel 32p + 8fq + q: value 8p + q of the row (see the prologue)
-          const float d = valid ? bf16_to_f32((uint16_t)h[q]) - row_bcast<8 * p + q>(pivr) : 0.f;
+          const float y = __uint_as_float((q & 1) ? (h2[q >> 1] & 0xffff0000u) : (h2[q >> 1] << 16));
+          // pivot of channel 32p + 8fq + q: value 8p + q of the row (see the prologue). Broadcast by
+          // every lane, outside the `valid` select: a DPP read from a lane masked off in EXEC returns 0
+          const float piv = row_bcast<8 * p + q>(pivr);
+          const float d = valid ? y - piv : 0.f;
           s1[p][q] += d;
           s2[p][q] = fmaf(d, d, s2[p][q]);
         });
         uint4 u;
-        u.x = h[0] | (h[1] << 16);
-        u.y = h[2] | (h[3] << 16);
-        u.z = h[4] | (h[5] << 16);
-        u.w = h[6] | (h[7] << 16);
+        u.x = h2[0];
+        u.y = h2[1];
+        u.z = h2[2];
+        u.w = h2[3];
         *reinterpret_cast<uint4*>(Y + ms * N + 32 * p + 8 * fq) = u;
       });
     });
@@ -315,8 +328,12 @@ __global__ void __launch_bounds__(NW * 64, 2) conv1x1_bn_stream_kernel(const uin
   if (tid == 0 && bp.num_batches_tracked) *bp.num_batches_tracked += 1;
 }
 
-constexpr int kWgPerCu = 2;
 constexpr int kCus = 256;
+
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && v[0]) ? atoi(v) : dflt;
+}
 
 int stream_group(int G) {
   int g = 1;
@@ -324,30 +341,59 @@ int stream_group(int G) {
   return g;
 }
 
-template <int K, int N, int NW>
+template <class S>
+int grid_of(int M) {
+  const int nblk = (M + S::BM - 1) / S::BM;
+  return nblk < kCus * S::PER_CU ? nblk : kCus * S::PER_CU;
+}
+
+template <int K, int N, int NW, int NB>
 hipError_t launch_stream(const void* X, const void* W, void* Y, int M, GemmBnEpi e, hipStream_t s) {
-  using S = C1<K, N, NW>;
-  const void* fn = reinterpret_cast<const void*>(&conv1x1_bn_stream_kernel<K, N, NW>);
+  using S = C1<K, N, NW, NB>;
+  const void* fn = reinterpret_cast<const void*>(&conv1x1_bn_stream_kernel<K, N, NW, NB>);
   static bool attr_set = false;
   if (!attr_set) {
     PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS));
     attr_set = true;
   }
-  const int nblk = (M + S::BM - 1) / S::BM;
-  const int per_cu = S::LDS * 2 <= 160 * 1024 ? kWgPerCu : 1;
-  const int G = nblk < kCus * per_cu ? nblk : kCus * per_cu;
+  const int G = grid_of<S>(M);
   e.group = stream_group(G);
-  hipLaunchKernelGGL((conv1x1_bn_stream_kernel<K, N, NW>), dim3(G), dim3(S::NT), S::LDS, s,
+  hipLaunchKernelGGL((conv1x1_bn_stream_kernel<K, N, NW, NB>), dim3(G), dim3(S::NT), S::LDS, s,
                      static_cast<const uint16_t*>(X), static_cast<const uint16_t*>(W), static_cast<uint16_t*>(Y), M,
-                     e, nblk);
+                     e, (M + S::BM - 1) / S::BM);
   return hipGetLastError();
+}
+
+// pipeline configurations (waves per workgroup, X buffers): 0 = (4, 3), 1 = (4, 5), 2 = (8, 2), 3 = (8, 3).
+// PTDT_C1_CFG overrides the per-shape default (benchmarks/conv1x1_fwd_probe.py --sweep).
+int cfg_for(int K, int N) {
+  const int forced = env_int("PTDT_C1_CFG", -1);  // read per call: benchmarks sweep it in one process
+  if (forced >= 0 && forced <= 3) return forced;
+  // measured (profiles/r3_convbn.md): 8 waves x 2 buffers for K = 64 (32.3 vs 37.0 us at 64 -> 64,
+  // 69.6 vs 75.7 at 64 -> 256), all equal for K = 256
+  (void)N;
+  return K == 64 ? 2 : 0;
 }
 
 // (K, N) instantiations: ResNet-50 layer1's stride-1 1x1 convolutions
 template <class F>
 bool dispatch(int K, int N, F&& f) {
+  const int cfg = cfg_for(K, N);
+  auto go = [&](auto k, auto n) {
+    auto run = [&](auto nw, auto nb) {
+      constexpr int kk = decltype(k)::value, nn = decltype(n)::value;
+      if constexpr (C1<kk, nn, decltype(nw)::value, decltype(nb)::value>::FITS) f(k, n, nw, nb);
+      else f(k, n, std::integral_constant<int, 4>{}, std::integral_constant<int, 3>{});
+    };
+    switch (cfg) {
+      case 1: run(std::integral_constant<int, 4>{}, std::integral_constant<int, 5>{}); break;
+      case 2: run(std::integral_constant<int, 8>{}, std::integral_constant<int, 2>{}); break;
+      case 3: run(std::integral_constant<int, 8>{}, std::integral_constant<int, 3>{}); break;
+      default: run(std::integral_constant<int, 4>{}, std::integral_constant<int, 3>{}); break;
+    }
+  };
 #define PTDT_C1(k, n) \
-  if (K == k && N == n) { f(std::integral_constant<int, k>{}, std::integral_constant<int, n>{}); return true; }
+  if (K == k && N == n) { go(std::integral_constant<int, k>{}, std::integral_constant<int, n>{}); return true; }
   PTDT_C1(64, 64) PTDT_C1(64, 256) PTDT_C1(256, 64) PTDT_C1(256, 128)
 #undef PTDT_C1
   return false;
@@ -356,16 +402,13 @@ bool dispatch(int K, int N, F&& f) {
 }  // namespace
 
 bool conv1x1_bn_stream_supported(int K, int N) {
-  return dispatch(K, N, [](auto, auto) {});
+  return dispatch(K, N, [](auto, auto, auto, auto) {});
 }
 
 int conv1x1_bn_stream_grid(int M, int K, int N) {
   int G = 0;
-  dispatch(K, N, [&](auto k, auto n) {
-    using S = C1<decltype(k)::value, decltype(n)::value, 4>;
-    const int nblk = (M + S::BM - 1) / S::BM;
-    const int per_cu = S::LDS * 2 <= 160 * 1024 ? kWgPerCu : 1;
-    G = nblk < kCus * per_cu ? nblk : kCus * per_cu;
+  dispatch(K, N, [&](auto k, auto n, auto nw, auto nb) {
+    G = grid_of<C1<decltype(k)::value, decltype(n)::value, decltype(nw)::value, decltype(nb)::value>>(M);
   });
   return G;
 }
@@ -388,7 +431,10 @@ hipError_t conv1x1_bn_stream(const void* X, const void* W, void* Y, int M, int K
   if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(Y)) & 15)
     return hipErrorInvalidValue;
   hipError_t err = hipErrorInvalidValue;
-  dispatch(K, N, [&](auto k, auto n) { err = launch_stream<decltype(k)::value, decltype(n)::value, 4>(X, W, Y, M, e, s); });
+  dispatch(K, N, [&](auto k, auto n, auto nw, auto nb) {
+    err = launch_stream<decltype(k)::value, decltype(n)::value, decltype(nw)::value, decltype(nb)::value>(X, W, Y, M,
+                                                                                                          e, s);
+  });
   return err;
 }
 

@@ -19,7 +19,10 @@ call it). Forward numerics: the statistics are those of the stored bf16 output
 (what the separate pass would read), merged in double.
 
 Anything else -- stride 2, eval mode, fp32, NCHW, odd channel counts, CPU --
-takes the unfused ``bn_act(bn, conv(x))``. ``PTDT_CONVBN=0`` disables the fusion.
+takes the unfused ``bn_act(bn, conv(x))``. Where both apply, ``PTDT_CONVBN=auto`` (default)
+times the two once per shape on the live operands and keeps the faster (MIOpen's 1x1
+forward kernels run close to HBM speed on some shapes, profiles/r3_convbn.md); ``on``
+always fuses, ``off`` never does.
 
 Reference call sites: the Bottleneck convolutions + BatchNorms of torchvision's
 ResNet-50 (NB03:560-570, NB03:807-833).
@@ -35,10 +38,10 @@ from .._ext import native
 from .conv import cast_weight
 from .norm import BatchNorm2d, batch_norm_act
 
-_ENABLED = os.environ.get("PTDT_CONVBN", "1") != "0"
-
-
+_MODE = os.environ.get("PTDT_CONVBN", "auto")  # auto: per-shape timing decides; on / 1: always; off / 0: never
+_ENABLED = _MODE not in ("0", "off")
 _STREAM = os.environ.get("PTDT_CONVBN_STREAM", "1") != "0"
+_CHOICE: dict[tuple, bool] = {}  # (M, K, N, tile) -> fused is faster (PTDT_CONVBN=auto)
 
 
 def _tile(M: int, N: int, K: int) -> int:
@@ -96,6 +99,52 @@ def _fusable(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual) -> bool:
     return True
 
 
+def _time_us(fn, reps: int = 3) -> float:
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    best = float("inf")
+    for _ in range(reps):
+        s.record()
+        fn()
+        e.record()
+        e.synchronize()
+        best = min(best, s.elapsed_time(e) * 1e3)
+    return best
+
+
+def _fused_wins(x: torch.Tensor, w: torch.Tensor, tile: int) -> bool:
+    """PTDT_CONVBN=auto: time, once per (M, K, N), the fused conv + statistics kernel + the BN apply
+    pass against MIOpen's convolution + the BN's statistics and apply passes on the live operands
+    (scratch statistics, no running-stat side effects), and keep the faster. Inside a graph capture an
+    unseen shape keeps the unfused path."""
+    n, cin, h, wd = x.shape
+    cout = w.shape[0]
+    key = (n * h * wd, cin, cout, tile)
+    if key in _CHOICE:
+        return _CHOICE[key]
+    if _MODE in ("1", "on"):
+        return True
+    if torch.cuda.is_current_stream_capturing():
+        return False
+    C = native()
+    x2 = x.detach().permute(0, 2, 3, 1).reshape(-1, cin)
+    w2 = w.detach().reshape(cout, cin)
+    tickets = torch.zeros(C.conv1x1_bn_num_tickets(key[0], cout, tile, cin), dtype=torch.int32, device=x.device)
+
+    def fused():
+        y2, st = C.conv1x1_bn_stats(x2, w2, None, None, None, None, None, 0.1, 1e-5, tickets, tile)
+        C.bn_fwd_apply(y2, st, None, True, False)
+
+    def plain():
+        y = torch.nn.functional.conv2d(x.detach(), w.detach())
+        C.bn_fwd_train(y, None, None, None, None, None, None, True, 0.1, 1e-5, None, False)
+
+    with torch.no_grad():
+        tf, tp = _time_us(fused), _time_us(plain)
+    _CHOICE[key] = tf < tp
+    return _CHOICE[key]
+
+
 def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: torch.Tensor | None = None,
                 relu: bool = False, link: bool = False) -> torch.Tensor:
     """``ReLU?(bn(conv(x)) + residual)``; a stride-1 1x1 ``conv`` feeding an ops.norm.BatchNorm2d in
@@ -104,10 +153,14 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: torch
         from ..models.resnet import bn_act
 
         return bn_act(bn, conv(x), residual, relu, link)
-    w = cast_weight(conv.weight)
-    track = bn.track_running_stats
     M = x.shape[0] * x.shape[2] * x.shape[3]
     tile = _tile(M, conv.out_channels, conv.in_channels)
+    w = cast_weight(conv.weight)
+    if not _fused_wins(x, w, tile):
+        from ..models.resnet import bn_act
+
+        return bn_act(bn, conv._conv_forward(x, w, None), residual, relu, link)
+    track = bn.track_running_stats
     tickets = bn._gemm_tickets
     need = native().conv1x1_bn_num_tickets(M, conv.out_channels, tile, conv.in_channels)
     if tickets.numel() < need or tickets.device != x.device:

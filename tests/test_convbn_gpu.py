@@ -61,9 +61,9 @@ def test_gemm_bn_stats_deterministic_and_offset_robust(native, dev, tile, M, K, 
     partials (tiled) / the running-mean pivot (streaming: here 0.9x the batch mean, as a lagging
     running mean would be) keep the variance; two launches agree bitwise."""
     g = torch.Generator(device=dev).manual_seed(7)
-    x = torch.randn(M, K, device=dev, generator=g) * 0.01
+    x = torch.randn(M, K, device=dev, generator=g)
     x[:, 0] = 1.0
-    w = torch.randn(N, K, device=dev, generator=g) * 0.05
+    w = torch.randn(N, K, device=dev, generator=g) * (1.5 / K ** 0.5)  # std ~1.5 around means of 64-70
     w[:, 0] = 64.0 + torch.arange(N, device=dev) % 7
     x, w = x.to(torch.bfloat16), w.to(torch.bfloat16)
     mean, var = _ref_stats((x.float() @ w.float().t()).to(torch.bfloat16))
@@ -75,6 +75,7 @@ def test_gemm_bn_stats_deterministic_and_offset_robust(native, dev, tile, M, K, 
     assert torch.equal(y1, y2) and torch.equal(s1, s2) and torch.equal(rm1, rm2)
     mean, var = _ref_stats(y1)
     assert float(mean.abs().min()) > 30 * float(var.sqrt().max())  # the regime the centring is for
+    torch.testing.assert_close(s1[0].double(), mean, rtol=1e-6, atol=0)
     torch.testing.assert_close(s1[1].double(), 1.0 / torch.sqrt(var + 1e-5), rtol=1e-4, atol=0)
 
 
@@ -106,6 +107,7 @@ def test_bottleneck_fused_matches_unfused(dev, monkeypatch, inplanes, planes, do
     outs, grads = [], []
     for blk, on in ((fused, True), (plain, False)):
         monkeypatch.setattr(convbn, "_ENABLED", on)
+        monkeypatch.setattr(convbn, "_MODE", "on")  # always fuse (no per-shape timing choice)
         xi = x.clone().requires_grad_()
         with torch.autocast("cuda", torch.bfloat16):
             y = blk(xi)
@@ -126,9 +128,12 @@ def test_bottleneck_fused_matches_unfused(dev, monkeypatch, inplanes, planes, do
 
 
 def test_resnet50_step_uses_fused_kernels(dev, monkeypatch):
-    """ResNet-50 training forward at batch 4 under bf16 autocast: the fused path is taken for
-    every stride-1 1x1 conv (bn1, bn3 and layer1's downsample: 33 of 53 BNs), and the loss and
-    parameter gradients agree with the unfused model."""
+    """ResNet-50 training step under bf16 autocast: the fused path is taken for every stride-1 1x1
+    conv (bn1, bn3 and layer1's downsample: 33 of 53 BNs), and its whole-model gradient error
+    against a float64 CPU reference (same weights and input) is at the level of the unfused bf16
+    model's (MIOpen conv + the BN's own statistics pass): both are bf16 models whose small-batch BNs
+    amplify rounding, so the two bf16 gradients differ from each other about as much as each differs
+    from the reference."""
     import copy
 
     from pytorch_distributed_training_tutorials_amd.models.resnet import resnet50
@@ -137,6 +142,8 @@ def test_resnet50_step_uses_fused_kernels(dev, monkeypatch):
     torch.manual_seed(0)
     m1 = resnet50(num_classes=10).to(dev).to(memory_format=torch.channels_last)
     m2 = copy.deepcopy(m1)
+    ref = resnet50(num_classes=10, norm_layer=nn.BatchNorm2d).double()
+    ref.load_state_dict(m1.state_dict())
     calls = {"n": 0}
     real = convbn._Conv1x1StatsFn.apply
 
@@ -144,21 +151,19 @@ def test_resnet50_step_uses_fused_kernels(dev, monkeypatch):
         calls["n"] += 1
         return real(*a)
 
-    # batch 4 at 96x96: layer4's BNs still normalise over only 36 rows, so bf16 rounding differences
-    # between the two conv implementations move the loss by ~1 %
-    x = torch.randn(4, 3, 96, 96, device=dev).contiguous(memory_format=torch.channels_last)
-    t = torch.randint(0, 10, (4,), device=dev)
-    losses = []
+    x = torch.randn(8, 3, 64, 64, device=dev).contiguous(memory_format=torch.channels_last)
+    t = torch.randint(0, 10, (8,), device=dev)
     for m, on in ((m1, True), (m2, False)):
         monkeypatch.setattr(convbn, "_ENABLED", on)
+        monkeypatch.setattr(convbn, "_MODE", "on")
         monkeypatch.setattr(convbn._Conv1x1StatsFn, "apply", counted)
         with torch.autocast("cuda", torch.bfloat16):
             loss = nn.functional.cross_entropy(m(x).float(), t)
         loss.backward()
-        losses.append(float(loss.detach()))
     assert calls["n"] == 33
-    assert abs(losses[0] - losses[1]) < 5e-2 * max(1.0, abs(losses[1]))
-    g1 = torch.cat([p.grad.flatten().float() for p in m1.parameters()])
-    g2 = torch.cat([p.grad.flatten().float() for p in m2.parameters()])
-    cos = float(torch.nn.functional.cosine_similarity(g1, g2, dim=0))
-    assert cos > 0.99, cos
+    nn.functional.cross_entropy(ref(x.double().cpu()), t.cpu()).backward()
+    g = torch.cat([p.grad.flatten() for p in ref.parameters()])
+    g1 = torch.cat([p.grad.flatten().double().cpu() for p in m1.parameters()])
+    g2 = torch.cat([p.grad.flatten().double().cpu() for p in m2.parameters()])
+    e1, e2 = float((g1 - g).norm() / g.norm()), float((g2 - g).norm() / g.norm())
+    assert e1 <= 1.5 * e2 + 1e-2, f"whole-model gradient error: fused {e1:.3g} vs unfused {e2:.3g}"
