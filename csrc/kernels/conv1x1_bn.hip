@@ -96,49 +96,56 @@ __device__ __forceinline__ float row_bcast(const float (&r)[R]) {
                                                                0x150 + (I & 15), 0xF, 0xF, false));
 }
 
-template <int K, int N, int NW, int NB>
+template <int K, int N, int NW, int NB, int NS>
 struct C1 {
   static constexpr int NT = NW * 64;
   static constexpr int BM = 16 * NW;         // rows per block (16 per wave)
-  static constexpr int WB = N * K * 2;       // resident weights
+  static constexpr int NSL = N / NS;         // channels of one weight slab (one workgroup's share)
+  static constexpr int WB = NSL * K * 2;     // resident weights
   static constexpr int AB = BM * K * 2;      // one X block
   // X blocks in flight + 1: NB, or fewer where the LDS does not hold them
   static constexpr int NBUF = WB + NB * AB <= 160 * 1024 ? NB : (WB + 3 * AB <= 160 * 1024 ? 3 : 2);
   // workgroups per CU: two waves per SIMD (the register budget), and the LDS
   static constexpr int PER_CU = (8 / NW) * (WB + NBUF * AB) <= 160 * 1024 ? 8 / NW : 1;
   static constexpr int DMA = AB / (NT * 16); // LDS-DMAs per thread per block
-  static constexpr int NP = N / 32;          // channel pairs (2 col-frags, 32 channels)
+  static constexpr int NP = NSL / 32;        // channel pairs (2 col-frags, 32 channels)
   static constexpr int KS = K / 32;          // MFMA k-steps
   static constexpr int LDS = WB + NBUF * AB;
-  static constexpr int CH = N < 128 ? N : 128;  // channels per chunk of the MFMA/epilogue loop
+  static constexpr int CH = NSL < 128 ? NSL : 128;  // channels per chunk of the MFMA/epilogue loop
   static constexpr int CP = CH / 32;            // pairs per chunk
   static constexpr int PR = (8 * NP + 15) / 16; // pivot registers per lane (see below)
-  static_assert(AB % (NT * 16) == 0 && N % 32 == 0 && K % 64 == 0, "shape");
+  static_assert(AB % (NT * 16) == 0 && NSL % 32 == 0 && N % NS == 0 && K % 64 == 0, "shape");
   static constexpr bool FITS = LDS <= 160 * 1024;  // dispatch() only launches configurations that fit
+  static_assert(2 * NW * NSL * 4 + 16 <= NBUF * AB, "cross-wave statistics scratch");
 };
 
 // weight row of col-frag j's MFMA row fr (see the header): channel 32p + 8(fr/4) + 4(j%2) + fr%4
 __device__ __forceinline__ int w_channel(int j, int fr) { return 32 * (j >> 1) + 8 * (fr >> 2) + 4 * (j & 1) + (fr & 3); }
 
-template <int K, int N, int NW, int NB>
+template <int K, int N, int NW, int NB, int NS>
 __global__ void __launch_bounds__(NW * 64, 2) conv1x1_bn_stream_kernel(const uint16_t* __restrict__ X,
                                                                        const uint16_t* __restrict__ W,
                                                                        uint16_t* __restrict__ Y, int M,
                                                                        GemmBnEpi e, int nblk) {
-  using S = C1<K, N, NW, NB>;
+  using S = C1<K, N, NW, NB, NS>;
   static_assert(S::FITS, "LDS");
+  constexpr int NSL = S::NSL;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* wl = smem;
   uint8_t* al = smem + S::WB;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
-  const int G = gridDim.x;
+  // workgroup = (row workgroup rwg, weight slab): NS workgroups share each row block, one per slab
+  // of NSL output channels (X is read NS times; the repeats mostly hit the 256 MiB Infinity Cache)
+  const int slab = (int)blockIdx.x % NS, rwg = (int)blockIdx.x / NS;
+  const int G = (int)gridDim.x / NS;  // row workgroups
+  const int n0 = slab * NSL;
 
   // X block t of this workgroup: rows (blockIdx.x + t*G) * BM ..; rows past M clamp to M-1 (computed,
   // never stored, not counted)
   auto stage = [&](int t) {
-    const int blk = blockIdx.x + t * G;
+    const int blk = rwg + t * G;
     const int row0 = blk * S::BM;
     uint8_t* dst0 = al + (t % S::NBUF) * S::AB;
 #pragma unroll
@@ -152,15 +159,15 @@ __global__ void __launch_bounds__(NW * 64, 2) conv1x1_bn_stream_kernel(const uin
       __builtin_amdgcn_global_load_lds((gbl_void*)g, (lds_void*)(dst0 + (i * S::NT + wid * 64) * 16), 16, 0, 0);
     }
   };
-  const int nt = (nblk - (int)blockIdx.x + G - 1) / G;  // blocks of this workgroup (>= 1: grid <= nblk)
+  const int nt = (nblk - rwg + G - 1) / G;  // blocks of this workgroup (>= 1: row workgroups <= nblk)
 
 #pragma unroll
   for (int t = 0; t < S::NBUF - 1; ++t)
     if (t < nt) stage(t);
   // resident weights in MFMA row order (plain loads + LDS stores, once)
-  for (int p = tid; p < N * (K / 8); p += S::NT) {
+  for (int p = tid; p < NSL * (K / 8); p += S::NT) {
     const int r = p / (K / 8), c = p % (K / 8);  // LDS row r = (col-frag j, MFMA row fr)
-    const int ch = w_channel(r >> 4, r & 15);
+    const int ch = n0 + w_channel(r >> 4, r & 15);
     *reinterpret_cast<uint4*>(wl + lds_off<K>(r, c)) = *reinterpret_cast<const uint4*>(W + (int64_t)ch * K + c * 8);
   }
   // pivots (the running mean, or 0) for the lane's channels 32p + 8fq + q, spread over the 16 lanes of
@@ -171,7 +178,7 @@ __global__ void __launch_bounds__(NW * 64, 2) conv1x1_bn_stream_kernel(const uin
 #pragma unroll
   for (int k = 0; k < S::PR; ++k) {
     const int i = 16 * k + fr;
-    pivr[k] = (e.p.running_mean && i < 8 * S::NP) ? e.p.running_mean[32 * (i >> 3) + 8 * fq + (i & 7)] : 0.f;
+    pivr[k] = (e.p.running_mean && i < 8 * S::NP) ? e.p.running_mean[n0 + 32 * (i >> 3) + 8 * fq + (i & 7)] : 0.f;
   }
   // drain the prologue (the first X blocks, weights): from here on the counted waits are exact
   vm_wait<0>();
@@ -197,12 +204,12 @@ __global__ void __launch_bounds__(NW * 64, 2) conv1x1_bn_stream_kernel(const uin
 #pragma unroll
     for (int ks = 0; ks < S::KS; ++ks)
       xb[ks] = *reinterpret_cast<const bf16x8_t*>(at + lds_off<K>(wid * 16 + fr, ks * 4 + fq));
-    const int m = (blockIdx.x + t * G) * S::BM + wid * 16 + fr;
+    const int m = (rwg + t * G) * S::BM + wid * 16 + fr;
     const bool valid = m < M;
     // a row past M multiplied the clamped row M-1: it stores row M-1's identical bytes there, so
     // every wave issues the same store count (the counted waits) and no lane diverges
     const int64_t ms = valid ? m : M - 1;
-    static_for<0, N / S::CH>([&](auto chc) {  // channel chunks: 2*CP accumulator tiles live at a time
+    static_for<0, NSL / S::CH>([&](auto chc) {  // channel chunks: 2*CP accumulator tiles live at a time
       constexpr int ch = decltype(chc)::value;
       f32x4_t acc[2 * S::CP];
 #pragma unroll
@@ -240,7 +247,7 @@ __global__ void __launch_bounds__(NW * 64, 2) conv1x1_bn_stream_kernel(const uin
         u.y = h2[1];
         u.z = h2[2];
         u.w = h2[3];
-        *reinterpret_cast<uint4*>(Y + ms * N + 32 * p + 8 * fq) = u;
+        *reinterpret_cast<uint4*>(Y + ms * N + n0 + 32 * p + 8 * fq) = u;
       });
     });
   }
@@ -266,32 +273,34 @@ __global__ void __launch_bounds__(NW * 64, 2) conv1x1_bn_stream_kernel(const uin
     for (int p = 0; p < S::NP; ++p)
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        red[(wid * 2 + 0) * N + 32 * p + 8 * fq + q] = s1[p][q];
-        red[(wid * 2 + 1) * N + 32 * p + 8 * fq + q] = s2[p][q];
+        red[(wid * 2 + 0) * NSL + 32 * p + 8 * fq + q] = s1[p][q];
+        red[(wid * 2 + 1) * NSL + 32 * p + 8 * fq + q] = s2[p][q];
       }
   }
   __syncthreads();
   float* ws1 = e.ws;
   float* ws2 = e.ws + (int64_t)G * N;
-  for (int c = tid; c < N; c += S::NT) {
+  for (int c = tid; c < NSL; c += S::NT) {
     float a = 0.f, b = 0.f;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
-      a += red[(w * 2 + 0) * N + c];
-      b += red[(w * 2 + 1) * N + c];
+      a += red[(w * 2 + 0) * NSL + c];
+      b += red[(w * 2 + 1) * NSL + c];
     }
-    st_sc1(ws1 + (int64_t)blockIdx.x * N + c, a);
-    st_sc1(ws2 + (int64_t)blockIdx.x * N + c, b);
+    st_sc1(ws1 + (int64_t)rwg * N + n0 + c, a);
+    st_sc1(ws2 + (int64_t)rwg * N + n0 + c, b);
   }
 
   // two-level merge (fixed order: deterministic)
-  int* flag = reinterpret_cast<int*>(red + 2 * NW * N);
+  int* flag = reinterpret_cast<int*>(red + 2 * NW * NSL);
   const int GS = e.group, ng = (G + GS - 1) / GS;
-  const int gi = blockIdx.x / GS, g0 = gi * GS, gc = min(GS, G - g0);
-  if (!last_arrival(e.tickets + gi, gc, flag)) return;
+  const int gi = rwg / GS, g0 = gi * GS, gc = min(GS, G - g0);
+  int* tk = e.tickets + slab * (ng + 1);  // this slab's group tickets, then its final ticket
+  if (!last_arrival(tk + gi, gc, flag)) return;
   float* gs1 = e.ws + (int64_t)2 * G * N;
   float* gs2 = gs1 + (int64_t)ng * N;
-  for (int c = tid; c < N; c += S::NT) {
+  for (int cc = tid; cc < NSL; cc += S::NT) {
+    const int c = n0 + cc;
     double a = 0.0, b = 0.0;
     for (int k = g0; k < g0 + gc; ++k) {
       a += (double)ld_sc1(ws1 + (int64_t)k * N + c);
@@ -300,10 +309,11 @@ __global__ void __launch_bounds__(NW * 64, 2) conv1x1_bn_stream_kernel(const uin
     st_sc1(gs1 + (int64_t)gi * N + c, (float)a);
     st_sc1(gs2 + (int64_t)gi * N + c, (float)b);
   }
-  if (!last_arrival(e.tickets + ng, ng, flag)) return;
+  if (!last_arrival(tk + ng, ng, flag)) return;
   const BnParams& bp = e.p;
   const double Md = (double)M;
-  for (int c = tid; c < N; c += S::NT) {
+  for (int cc = tid; cc < NSL; cc += S::NT) {
+    const int c = n0 + cc;
     double a = 0.0, b = 0.0;
     for (int k = 0; k < ng; ++k) {
       a += (double)ld_sc1(gs1 + (int64_t)k * N + c);
@@ -325,7 +335,7 @@ __global__ void __launch_bounds__(NW * 64, 2) conv1x1_bn_stream_kernel(const uin
       bp.running_var[c] = (float)((1.0 - bp.momentum) * bp.running_var[c] + bp.momentum * unbiased);
     }
   }
-  if (tid == 0 && bp.num_batches_tracked) *bp.num_batches_tracked += 1;
+  if (tid == 0 && slab == 0 && bp.num_batches_tracked) *bp.num_batches_tracked += 1;
 }
 
 constexpr int kCus = 256;
@@ -341,24 +351,27 @@ int stream_group(int G) {
   return g;
 }
 
-template <class S>
-int grid_of(int M) {
+// row workgroups (the grid is that times NS): enough to hold PER_CU workgroups on every CU
+template <class S, int NS>
+int rows_of(int M) {
   const int nblk = (M + S::BM - 1) / S::BM;
-  return nblk < kCus * S::PER_CU ? nblk : kCus * S::PER_CU;
+  int g = kCus * S::PER_CU / NS;
+  if (g < 1) g = 1;
+  return nblk < g ? nblk : g;
 }
 
-template <int K, int N, int NW, int NB>
+template <int K, int N, int NW, int NB, int NS>
 hipError_t launch_stream(const void* X, const void* W, void* Y, int M, GemmBnEpi e, hipStream_t s) {
-  using S = C1<K, N, NW, NB>;
-  const void* fn = reinterpret_cast<const void*>(&conv1x1_bn_stream_kernel<K, N, NW, NB>);
+  using S = C1<K, N, NW, NB, NS>;
+  const void* fn = reinterpret_cast<const void*>(&conv1x1_bn_stream_kernel<K, N, NW, NB, NS>);
   static bool attr_set = false;
   if (!attr_set) {
     PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS));
     attr_set = true;
   }
-  const int G = grid_of<S>(M);
+  const int G = rows_of<S, NS>(M);
   e.group = stream_group(G);
-  hipLaunchKernelGGL((conv1x1_bn_stream_kernel<K, N, NW, NB>), dim3(G), dim3(S::NT), S::LDS, s,
+  hipLaunchKernelGGL((conv1x1_bn_stream_kernel<K, N, NW, NB, NS>), dim3(G * NS), dim3(S::NT), S::LDS, s,
                      static_cast<const uint16_t*>(X), static_cast<const uint16_t*>(W), static_cast<uint16_t*>(Y), M,
                      e, (M + S::BM - 1) / S::BM);
   return hipGetLastError();
@@ -369,21 +382,22 @@ hipError_t launch_stream(const void* X, const void* W, void* Y, int M, GemmBnEpi
 int cfg_for(int K, int N) {
   const int forced = env_int("PTDT_C1_CFG", -1);  // read per call: benchmarks sweep it in one process
   if (forced >= 0 && forced <= 3) return forced;
-  // measured (profiles/r3_convbn.md): 8 waves x 2 buffers for K = 64 (32.3 vs 37.0 us at 64 -> 64,
-  // 69.6 vs 75.7 at 64 -> 256), all equal for K = 256
+  // measured (profiles/r3_convbn_stream_sweep*.jsonl): 8 waves x 2 buffers for K = 64 (31.3 vs 35.1 us
+  // at 64 -> 64, 65.0 vs 69.2 at 64 -> 256) and 128 -> 512 (47.1 vs 48.5); within noise for K = 256
   (void)N;
-  return K == 64 ? 2 : 0;
+  return K <= 128 ? 2 : 0;
 }
 
-// (K, N) instantiations: ResNet-50 layer1's stride-1 1x1 convolutions
+// (K, N, weight slabs) instances: ResNet-50's stride-1 1x1 convolutions whose weights fit the LDS
+// whole (layer1) or in NS slabs of <= 64 KiB
 template <class F>
 bool dispatch(int K, int N, F&& f) {
   const int cfg = cfg_for(K, N);
-  auto go = [&](auto k, auto n) {
+  auto go = [&](auto k, auto n, auto ns) {
     auto run = [&](auto nw, auto nb) {
-      constexpr int kk = decltype(k)::value, nn = decltype(n)::value;
-      if constexpr (C1<kk, nn, decltype(nw)::value, decltype(nb)::value>::FITS) f(k, n, nw, nb);
-      else f(k, n, std::integral_constant<int, 4>{}, std::integral_constant<int, 3>{});
+      constexpr int kk = decltype(k)::value, nn = decltype(n)::value, s_ = decltype(ns)::value;
+      if constexpr (C1<kk, nn, decltype(nw)::value, decltype(nb)::value, s_>::FITS) f(k, n, nw, nb, ns);
+      else f(k, n, std::integral_constant<int, 4>{}, std::integral_constant<int, 3>{}, ns);
     };
     switch (cfg) {
       case 1: run(std::integral_constant<int, 4>{}, std::integral_constant<int, 5>{}); break;
@@ -392,9 +406,13 @@ bool dispatch(int K, int N, F&& f) {
       default: run(std::integral_constant<int, 4>{}, std::integral_constant<int, 3>{}); break;
     }
   };
-#define PTDT_C1(k, n) \
-  if (K == k && N == n) { go(std::integral_constant<int, k>{}, std::integral_constant<int, n>{}); return true; }
-  PTDT_C1(64, 64) PTDT_C1(64, 256) PTDT_C1(256, 64) PTDT_C1(256, 128)
+#define PTDT_C1(k, n, ns)                                                                                  \
+  if (K == k && N == n) {                                                                                \
+    go(std::integral_constant<int, k>{}, std::integral_constant<int, n>{}, std::integral_constant<int, ns>{}); \
+    return true;                                                                                         \
+  }
+  PTDT_C1(64, 64, 1) PTDT_C1(64, 256, 1) PTDT_C1(256, 64, 1) PTDT_C1(256, 128, 1)
+  PTDT_C1(128, 512, 4) PTDT_C1(256, 1024, 8)
 #undef PTDT_C1
   return false;
 }
@@ -402,26 +420,30 @@ bool dispatch(int K, int N, F&& f) {
 }  // namespace
 
 bool conv1x1_bn_stream_supported(int K, int N) {
-  return dispatch(K, N, [](auto, auto, auto, auto) {});
+  return dispatch(K, N, [](auto, auto, auto, auto, auto) {});
 }
 
-int conv1x1_bn_stream_grid(int M, int K, int N) {
-  int G = 0;
-  dispatch(K, N, [&](auto k, auto n, auto nw, auto nb) {
-    G = grid_of<C1<decltype(k)::value, decltype(n)::value, decltype(nw)::value, decltype(nb)::value>>(M);
+// (row workgroups, weight slabs) of the launch for this shape
+static void stream_geometry(int M, int K, int N, int* G, int* NS) {
+  *G = 0, *NS = 1;
+  dispatch(K, N, [&](auto k, auto n, auto nw, auto nb, auto ns) {
+    constexpr int s_ = decltype(ns)::value;
+    *G = rows_of<C1<decltype(k)::value, decltype(n)::value, decltype(nw)::value, decltype(nb)::value, s_>, s_>(M);
+    *NS = s_;
   });
-  return G;
 }
 
 int64_t conv1x1_bn_stream_ws_floats(int M, int K, int N) {
-  const int G = conv1x1_bn_stream_grid(M, K, N);
+  int G, NS;
+  stream_geometry(M, K, N, &G, &NS);
   const int ng = (G + stream_group(G) - 1) / stream_group(G);
   return (int64_t)2 * N * (G + ng);
 }
 
 int conv1x1_bn_stream_num_tickets(int M, int K, int N) {
-  const int G = conv1x1_bn_stream_grid(M, K, N);
-  return (G + stream_group(G) - 1) / stream_group(G) + 1;
+  int G, NS;
+  stream_geometry(M, K, N, &G, &NS);
+  return NS * ((G + stream_group(G) - 1) / stream_group(G) + 1);
 }
 
 hipError_t conv1x1_bn_stream(const void* X, const void* W, void* Y, int M, int K, int N, GemmBnEpi e,
@@ -431,9 +453,9 @@ hipError_t conv1x1_bn_stream(const void* X, const void* W, void* Y, int M, int K
   if ((reinterpret_cast<uintptr_t>(X) | reinterpret_cast<uintptr_t>(W) | reinterpret_cast<uintptr_t>(Y)) & 15)
     return hipErrorInvalidValue;
   hipError_t err = hipErrorInvalidValue;
-  dispatch(K, N, [&](auto k, auto n, auto nw, auto nb) {
-    err = launch_stream<decltype(k)::value, decltype(n)::value, decltype(nw)::value, decltype(nb)::value>(X, W, Y, M,
-                                                                                                          e, s);
+  dispatch(K, N, [&](auto k, auto n, auto nw, auto nb, auto ns) {
+    err = launch_stream<decltype(k)::value, decltype(n)::value, decltype(nw)::value, decltype(nb)::value,
+                        decltype(ns)::value>(X, W, Y, M, e, s);
   });
   return err;
 }

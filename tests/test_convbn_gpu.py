@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 
 # (M, K, N): ResNet-50 shapes at small batch, edge tiles (M % 256 != 0), several column tiles
 KSHAPES = [(6272, 512, 2048), (3136, 64, 256), (1000, 256, 64), (25088, 1024, 256), (300, 128, 520),
-           (777, 64, 8), (777, 64, 64), (12544, 256, 128), (100000, 64, 256)]
+           (777, 64, 8), (777, 64, 64), (12544, 256, 128), (100000, 64, 256), (5000, 128, 512), (3001, 256, 1024)]
 
 
 def _ref_stats(y: torch.Tensor):
@@ -55,7 +55,8 @@ def test_gemm_bn_stats_matches_reference(native, dev, M, K, N, tile):
     assert int(tickets.abs().sum()) == 0  # re-armed for the next launch
 
 
-@pytest.mark.parametrize("tile,M,K,N", [(256, 25088, 256, 512), (0, 25088, 64, 256), (0, 25088, 256, 128)])
+@pytest.mark.parametrize("tile,M,K,N", [(256, 25088, 256, 512), (0, 25088, 64, 256), (0, 25088, 256, 128),
+                                        (0, 25088, 128, 512)])
 def test_gemm_bn_stats_deterministic_and_offset_robust(native, dev, tile, M, K, N):
     """|mean| >> std per channel (a constant input column carrying a large weight): the centred
     partials (tiled) / the running-mean pivot (streaming: here 0.9x the batch mean, as a lagging
