@@ -3,15 +3,21 @@ epilogue: ``ReLU?(BN(conv1x1(x)) + residual?)``.
 
 A stride-1 1x1 convolution over an NHWC (channels_last) activation is a GEMM,
 ``Y[N*H*W, Cout] = X[N*H*W, Cin] . W[Cout, Cin]^T``, with both operands already
-K-contiguous in memory. ``gemm_bn_stats`` (csrc/kernels/gemm_big.hip) runs that
-GEMM on the LDS-DMA MFMA kernel and, while the output tile is still in registers,
-reduces it to per-channel sums and centred sums of squares; row-tile partials are
-merged in fixed order by the last workgroups to finish (two ticket levels), which
-also write the BN coefficients and update the running statistics. The BN then
-runs only its apply pass (``bn_fwd_apply``): the separate statistics pass -- a full
-read of the conv output -- is gone. In torchvision's ResNet-50 that is every bn1
-and bn3 and the layer1 downsample BN (bf16, batch 128: ~0.75 ms of statistics
-passes per step, profiles/r3_bn_kernels.md).
+K-contiguous in memory. Two native kernels run it and, while each output value is
+still in registers, reduce the output to per-channel sums for the BatchNorm:
+
+* ``conv1x1_bn.hip`` (streaming; ResNet-50's layer1 shapes and, with the weights in
+  <= 64 KiB slabs, 128 -> 512 and 256 -> 1024): persistent workgroups, weights
+  resident in LDS, activation row blocks LDS-DMA'd ahead, 16-B output stores,
+  per-lane sums about running-mean pivots;
+* ``gemm_bn_stats`` in ``gemm_big.hip`` (tiled, any K % 64 == 0 shape): the
+  LDS-DMA GEMM with centred per-wave partials in its epilogue.
+
+Partials are merged in fixed order by the last workgroups to finish (two ticket
+levels, sc1 hand-off), which also write the BN coefficients and update the running
+statistics. The BN then runs only its apply pass (``bn_fwd_apply``): the separate
+statistics pass -- a full read of the conv output -- is gone (bf16, batch 128:
+-214 us per ResNet-50 step, profiles/r3_convbn.md).
 
 Backward is unchanged: the BN's native backward, then the convolution's data and
 weight gradients on MIOpen (``aten.convolution_backward``, as autograd would
