@@ -114,7 +114,7 @@ struct VecIO {
     } else {
       uint32_t w[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f32_to_bf16(v[2 * i]) | ((uint32_t)f32_to_bf16(v[2 * i + 1]) << 16);
+      for (int i = 0; i < 4; ++i) w[i] = pack_bf16x2(v[2 * i], v[2 * i + 1]);
       u.x = w[0]; u.y = w[1]; u.z = w[2]; u.w = w[3];
     }
     *reinterpret_cast<uint4*>(p) = u;
