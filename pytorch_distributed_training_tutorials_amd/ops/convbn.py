@@ -145,9 +145,11 @@ def _fused_wins(x: torch.Tensor, w: torch.Tensor, tile: int) -> bool:
         y = torch.nn.functional.conv2d(x.detach(), w.detach())
         C.bn_fwd_train(y, None, None, None, None, None, None, True, 0.1, 1e-5, None, False)
 
-    with torch.no_grad():
-        tf, tp = _time_us(fused), _time_us(plain)
-    _CHOICE[key] = tf < tp
+    with torch.no_grad():  # interleaved, best of 5 each; near-ties (< 3 %) keep MIOpen's path
+        tf, tp = float("inf"), float("inf")
+        for _ in range(5):
+            tf, tp = min(tf, _time_us(fused, 1)), min(tp, _time_us(plain, 1))
+    _CHOICE[key] = tf < 0.97 * tp
     return _CHOICE[key]
 
 
