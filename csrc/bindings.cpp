@@ -943,7 +943,8 @@ const float* opt_f32(const c10::optional<Tensor>& t, int64_t C, const char* name
 std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> weight, c10::optional<Tensor> bias,
                                  c10::optional<Tensor> running_mean, c10::optional<Tensor> running_var,
                                  c10::optional<Tensor> num_batches_tracked, c10::optional<Tensor> residual, bool relu,
-                                 double momentum, double eps, c10::optional<Tensor> tickets, bool want_mask) {
+                                 double momentum, double eps, c10::optional<Tensor> tickets, bool want_mask,
+                                 bool stats_only) {
   int64_t M;
   int C;
   bn_rows(x, &M, &C);
@@ -954,10 +955,10 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> weight, c10::op
     same_rows(*residual, x, "residual");
     a.residual = residual->data_ptr();
   }
-  Tensor y = at::empty_like(x);
+  Tensor y = stats_only ? Tensor() : at::empty_like(x);
   Tensor stats = at::empty({4, C}, x.options().dtype(at::kFloat));
   Tensor ws = at::empty({bn_workspace_floats(M, C, dt_of(x))}, x.options().dtype(at::kFloat));
-  a.y = y.data_ptr();
+  a.y = stats_only ? nullptr : y.data_ptr();
   a.dtype = dt_of(x);
   a.M = M;
   a.C = C;
@@ -982,7 +983,7 @@ std::vector<Tensor> bn_fwd_train(Tensor x, c10::optional<Tensor> weight, c10::op
   a.p.scale = st + 2 * C;
   a.p.shift = st + 3 * C;
   Tensor mask;
-  if (want_mask && relu && a.residual != nullptr) {  // one byte per 16-B vector of x
+  if (want_mask && relu && a.residual != nullptr && !stats_only) {  // one byte per 16-B vector of x
     mask = at::empty({M * C / (x.scalar_type() == at::kFloat ? 4 : 8)}, x.options().dtype(at::kByte));
     a.mask_out = mask.data_ptr<uint8_t>();
   }
@@ -1204,9 +1205,18 @@ PoolArgs pool_args(const Tensor& x, int64_t Ho, int64_t Wo, std::vector<int64_t>
   return a;
 }
 
-std::vector<Tensor> maxpool2d_fwd(Tensor x, std::vector<int64_t> k, std::vector<int64_t> st, std::vector<int64_t> pad) {
+// scale/shift (f32 [C], optional): y = maxpool(ReLU?(x * scale + shift)) -- a training BatchNorm's
+// apply pass folded into the pool (ops/norm.bn_relu_maxpool)
+std::vector<Tensor> maxpool2d_fwd(Tensor x, std::vector<int64_t> k, std::vector<int64_t> st, std::vector<int64_t> pad,
+                                  c10::optional<Tensor> scale, c10::optional<Tensor> shift, bool relu) {
   const int64_t Ho = (x.size(2) + 2 * pad[0] - k[0]) / st[0] + 1, Wo = (x.size(3) + 2 * pad[1] - k[1]) / st[1] + 1;
   PoolArgs a = pool_args(x, Ho, Wo, k, st, pad);
+  if (scale.has_value() && scale->defined()) {
+    TORCH_CHECK(shift.has_value() && shift->defined(), "maxpool: scale and shift together");
+    a.scale = opt_f32(scale, x.size(1), "scale");
+    a.shift = opt_f32(shift, x.size(1), "shift");
+    a.relu = relu ? 1 : 0;
+  }
   c10::hip::HIPGuard guard(x.device().index());
   auto opts = x.options().memory_format(at::MemoryFormat::ChannelsLast);
   Tensor y = at::empty({x.size(0), x.size(1), Ho, Wo}, opts);
@@ -1330,12 +1340,14 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_relu", &bn_relu);
   m.def("bn_fwd_train", &bn_fwd_train, py::arg("x"), py::arg("weight"), py::arg("bias"), py::arg("running_mean"),
         py::arg("running_var"), py::arg("num_batches_tracked"), py::arg("residual"), py::arg("relu"),
-        py::arg("momentum"), py::arg("eps"), py::arg("tickets") = py::none(), py::arg("want_mask") = false);
+        py::arg("momentum"), py::arg("eps"), py::arg("tickets") = py::none(), py::arg("want_mask") = false,
+        py::arg("stats_only") = false);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("x"), py::arg("y"), py::arg("weight"), py::arg("stats"),
         py::arg("relu"), py::arg("want_dres"), py::arg("want_dweight"), py::arg("tickets") = py::none(),
         py::arg("dweight_out") = py::none(), py::arg("dbias_out") = py::none(), py::arg("dy2") = py::none(),
         py::arg("mask") = py::none());
-  m.def("maxpool2d_fwd", &maxpool2d_fwd);
+  m.def("maxpool2d_fwd", &maxpool2d_fwd, py::arg("x"), py::arg("k"), py::arg("s"), py::arg("p"),
+        py::arg("scale") = py::none(), py::arg("shift") = py::none(), py::arg("relu") = false);
   m.def("maxpool2d_bwd", &maxpool2d_bwd);
   m.def("bn_fwd_apply", &bn_fwd_apply, py::arg("x"), py::arg("stats"), py::arg("residual"), py::arg("relu"),
         py::arg("want_mask"));

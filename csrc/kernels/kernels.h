@@ -378,6 +378,11 @@ hipError_t bn_apply(const void* x, const void* residual, void* y, int dtype, con
 struct PoolArgs {
   int N, H, W, C, Ho, Wo;
   int kh, kw, sh, sw, ph, pw;
+  // forward only, optional: every loaded x becomes ReLU?(x * scale[c] + shift[c]) rounded to x's type
+  // before the max -- a training BatchNorm's apply pass folded into the pool that consumes it
+  const float* scale = nullptr;
+  const float* shift = nullptr;
+  int relu = 0;
 };
 hipError_t maxpool2d_nhwc_forward(const void* x, void* y, uint8_t* argmax, int dtype, const PoolArgs& a,
                                   hipStream_t s);

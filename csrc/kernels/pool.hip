@@ -49,7 +49,16 @@ struct V16 {
   }
 };
 
+// AFF: the BatchNorm apply (+ReLU) of the pool's input done on load (PoolArgs.scale/shift/relu), with
+// the same fmaf and rounding as batchnorm.hip's apply pass: output and argmax are bit-identical to
+// BN-then-pool, without writing and re-reading the normalised activation.
 template <typename T>
+__device__ __forceinline__ float round_to(float v) {
+  if constexpr (sizeof(T) == 4) return v;
+  else return __uint_as_float((uint32_t)f32_to_bf16(v) << 16);
+}
+
+template <typename T, bool AFF>
 __global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                                uint8_t* __restrict__ arg, PoolArgs a) {
   constexpr int V = V16<T>::V;
@@ -65,10 +74,15 @@ __global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(const T* __restri
     const int n = (int)(pix / a.Ho);
     float best[V];
     uint32_t bi[V];
+    float sc[AFF ? V : 1], sf[AFF ? V : 1];
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       best[v] = -__builtin_inff();
       bi[v] = 0;
+      if constexpr (AFF) {
+        sc[v] = a.scale[c0 + v];
+        sf[v] = a.shift[c0 + v];
+      }
     }
     const int h0 = ho * a.sh - a.ph, w0 = wo * a.sw - a.pw;
     for (int dy = 0; dy < a.kh; ++dy) {
@@ -79,6 +93,14 @@ __global__ void __launch_bounds__(kThreads) maxpool_fwd_kernel(const T* __restri
         if (w < 0 || w >= a.W) continue;
         float v_[V];
         V16<T>::load(x + (((int64_t)n * a.H + h) * a.W + w) * a.C + c0, v_);
+        if constexpr (AFF) {
+#pragma unroll
+          for (int v = 0; v < V; ++v) {
+            float o = fmaf(v_[v], sc[v], sf[v]);
+            if (a.relu) o = fmaxf(o, 0.f);
+            v_[v] = round_to<T>(o);
+          }
+        }
         const uint32_t k = (uint32_t)(dy * a.kw + dx);
 #pragma unroll
         for (int v = 0; v < V; ++v)
@@ -165,12 +187,23 @@ hipError_t maxpool2d_nhwc_forward(const void* x, void* y, uint8_t* argmax, int d
   if (a.C % V || a.kh * a.kw > 256 || a.kh < 1 || a.kw < 1 || a.sh < 1 || a.sw < 1) return hipErrorInvalidValue;
   const int64_t work = (int64_t)a.N * a.Ho * a.Wo * (a.C / V);
   if (work == 0) return hipSuccess;
-  if (dtype == kF32)
-    hipLaunchKernelGGL(maxpool_fwd_kernel<float>, dim3(grid_for(work)), dim3(kThreads), 0, s,
-                       static_cast<const float*>(x), static_cast<float*>(y), argmax, a);
-  else
-    hipLaunchKernelGGL(maxpool_fwd_kernel<uint16_t>, dim3(grid_for(work)), dim3(kThreads), 0, s,
-                       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), argmax, a);
+  if ((a.scale == nullptr) != (a.shift == nullptr)) return hipErrorInvalidValue;
+  const bool aff = a.scale != nullptr;
+  if (dtype == kF32) {
+    if (aff)
+      hipLaunchKernelGGL((maxpool_fwd_kernel<float, true>), dim3(grid_for(work)), dim3(kThreads), 0, s,
+                         static_cast<const float*>(x), static_cast<float*>(y), argmax, a);
+    else
+      hipLaunchKernelGGL((maxpool_fwd_kernel<float, false>), dim3(grid_for(work)), dim3(kThreads), 0, s,
+                         static_cast<const float*>(x), static_cast<float*>(y), argmax, a);
+  } else {
+    if (aff)
+      hipLaunchKernelGGL((maxpool_fwd_kernel<uint16_t, true>), dim3(grid_for(work)), dim3(kThreads), 0, s,
+                         static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), argmax, a);
+    else
+      hipLaunchKernelGGL((maxpool_fwd_kernel<uint16_t, false>), dim3(grid_for(work)), dim3(kThreads), 0, s,
+                         static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), argmax, a);
+  }
   return hipGetLastError();
 }
 

@@ -23,7 +23,7 @@ import torch.nn as nn
 from ..ops.conv import Conv2d
 from ..ops.convbn import conv_bn_act
 from ..ops.linear import Linear
-from ..ops.norm import BatchNorm2d, MaxPool2d, grad_link
+from ..ops.norm import BatchNorm2d, MaxPool2d, bn_relu_maxpool, grad_link
 
 
 def bn_act(bn: nn.Module, x: torch.Tensor, residual: torch.Tensor | None = None, relu: bool = False,
@@ -128,7 +128,8 @@ class ResNet(nn.Module):
         return nn.Sequential(*layers)
 
     def _forward_impl(self, x):
-        x = self.maxpool(bn_act(self.bn1, self.conv1(x), relu=True))
+        # stem: the BN apply + ReLU run inside the pool's loads (ops.norm.bn_relu_maxpool)
+        x = bn_relu_maxpool(self.conv1(x), self.bn1, self.maxpool)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         x = torch.flatten(self.avgpool(x), 1)
         return self.fc(x)

@@ -242,17 +242,76 @@ def _pair(v):
     return [int(v), int(v)] if isinstance(v, int) else [int(t) for t in v]
 
 
+def _pool_cfg(pool: nn.MaxPool2d, x: torch.Tensor):
+    """(k, s, p) when the native NHWC pool applies to ``x``, else None."""
+    k, s, p = _pair(pool.kernel_size), _pair(pool.stride or pool.kernel_size), _pair(pool.padding)
+    d = _pair(pool.dilation)
+    vec = 4 if x.dtype == torch.float32 else 8
+    if (x.is_cuda and x.dim() == 4 and x.dtype in (torch.float32, torch.bfloat16) and d == [1, 1]
+            and not pool.ceil_mode and not pool.return_indices and x.shape[1] % vec == 0
+            and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0
+            and 2 * p[0] <= k[0] and 2 * p[1] <= k[1]):
+        return k, s, p
+    return None
+
+
+class _BnReluPoolFn(torch.autograd.Function):
+    """maxpool(ReLU(BN(x))) in two launches: the BN statistics, then the pool applying
+    ReLU(x * scale + shift) to every value it loads -- the normalised activation (the ResNet stem's
+    [B, 64, 112, 112]) is never written or re-read. Backward: the pool's gather, then the BN backward
+    with the ReLU mask recomputed from x (bit-exact with the fused apply)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, momentum: float, eps: float, tickets, k, s, p):
+        _, stats, _ = native().bn_fwd_train(x, weight, bias, running_mean, running_var, nbt, None, True, momentum,
+                                            eps, tickets, False, True)
+        y, arg = native().maxpool2d_fwd(x, k, s, p, stats[2], stats[3], True)
+        ctx.save_for_backward(x, arg, weight, stats)
+        ctx.cfg = (k, s, p)
+        ctx.tickets = tickets
+        ctx.params = (weight, bias)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, arg, weight, stats = ctx.saved_tensors
+        k, s, p = ctx.cfg
+        dy = native().maxpool2d_bwd(gy.contiguous(memory_format=torch.channels_last), arg, list(x.shape), k, s, p)
+        want_dw = weight is not None and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        sinks = [None, None]
+        if want_dw:  # DDP grad sinks: dweight/dbias straight into the bucket slots
+            for i, prm in enumerate(ctx.params):
+                if prm is not None and prm.grad is None and getattr(prm, "_ptdt_grad_sink", None) is not None:
+                    sinks[i] = prm._ptdt_grad_sink()
+        dx, dw, db, _ = native().bn_bwd(dy, x, None, weight, stats, True, False, want_dw, ctx.tickets, sinks[0],
+                                        sinks[1], None, None)
+        return (dx if ctx.needs_input_grad[0] else None, dw if want_dw else None, db if want_dw else None,
+                *([None] * 9))
+
+
+def bn_relu_maxpool(x: torch.Tensor, bn: nn.Module, pool: nn.MaxPool2d) -> torch.Tensor:
+    """``pool(ReLU(bn(x)))`` (the ResNet stem): fused for an ops.norm.BatchNorm2d in training over a
+    channels_last GPU activation (PTDT_BN_POOL=0 disables), composed otherwise."""
+    cfg = _pool_cfg(pool, x) if _BN_POOL else None
+    if (cfg is None or not isinstance(bn, BatchNorm2d) or not bn.training or bn.momentum is None
+            or not _rows_layout_ok(x)):
+        y = bn(x, relu=True) if isinstance(bn, BatchNorm2d) else torch.relu(bn(x))
+        return pool(y)
+    track = bn.track_running_stats
+    return _BnReluPoolFn.apply(x, bn.weight, bn.bias, bn.running_mean if track else None,
+                               bn.running_var if track else None, bn.num_batches_tracked if track else None,
+                               float(bn.momentum), float(bn.eps), _tickets_of(bn, x), *cfg)
+
+
+_BN_POOL = __import__("os").environ.get("PTDT_BN_POOL", "1") != "0"
+
+
 class MaxPool2d(nn.MaxPool2d):
     """Drop-in ``nn.MaxPool2d``; channels_last GPU activations run on the native NHWC
     kernels (csrc/kernels/pool.hip: one-byte window argmax, gather backward)."""
 
     def forward(self, x):
-        k, s, p = _pair(self.kernel_size), _pair(self.stride or self.kernel_size), _pair(self.padding)
-        d = _pair(self.dilation)
-        vec = 4 if x.dtype == torch.float32 else 8
-        if (x.is_cuda and x.dim() == 4 and x.dtype in (torch.float32, torch.bfloat16) and d == [1, 1]
-                and not self.ceil_mode and not self.return_indices and x.shape[1] % vec == 0
-                and x.is_contiguous(memory_format=torch.channels_last) and x.data_ptr() % 16 == 0
-                and 2 * p[0] <= k[0] and 2 * p[1] <= k[1]):
-            return _MaxPoolFn.apply(x, k, s, p)
+        cfg = _pool_cfg(self, x)
+        if cfg is not None:
+            return _MaxPoolFn.apply(x, *cfg)
         return super().forward(x)

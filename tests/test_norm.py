@@ -327,3 +327,35 @@ def test_grad_link_downsample_branch_matches_autograd_add(dtype):
         for gt, g0, g1 in zip(truth, grads(dtype, False), grads(dtype, True)):
             e0, e1 = (g0 - gt).norm().item(), (g1 - gt).norm().item()
             assert e1 <= 1.5 * e0 + 1e-3 * gt.norm().item(), (e1, e0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(8, 64, 56, 56), (3, 32, 17, 15)])
+def test_bn_relu_maxpool_matches_composed(shape):
+    """The ResNet stem fusion (BN apply + ReLU inside the pool's loads) vs BN-then-pool on the same
+    native kernels: output bit-identical, gradients and running statistics equal."""
+    import copy
+
+    from pytorch_distributed_training_tutorials_amd.ops.norm import MaxPool2d, bn_relu_maxpool
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    bn1 = BatchNorm2d(shape[1]).to(dev)
+    with torch.no_grad():
+        bn1.weight.uniform_(-1.5, 1.5)  # negative scales too: the max is taken after the affine
+        bn1.bias.uniform_(-0.5, 0.5)
+    bn2 = copy.deepcopy(bn1)
+    pool = MaxPool2d(kernel_size=3, stride=2, padding=1)
+    x = torch.randn(*shape, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x1, x2 = x.clone().requires_grad_(), x.clone().requires_grad_()
+    y1 = bn_relu_maxpool(x1, bn1, pool)
+    y2 = pool(bn2(x2, relu=True))
+    assert torch.equal(y1, y2)
+    g = torch.randn_like(y1)
+    y1.backward(g)
+    y2.backward(g)
+    assert torch.equal(x1.grad, x2.grad)
+    torch.testing.assert_close(bn1.weight.grad, bn2.weight.grad)
+    torch.testing.assert_close(bn1.bias.grad, bn2.bias.grad)
+    for k in ("running_mean", "running_var", "num_batches_tracked"):
+        torch.testing.assert_close(getattr(bn1, k), getattr(bn2, k))
