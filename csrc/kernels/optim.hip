@@ -123,6 +123,44 @@ __global__ void __launch_bounds__(kBlock) sgd_multi_kernel(TensorList tl, int32_
   // f32 params: the bf16 autocast copy of the updated weight, written in the same pass
   uint16_t* shadow = std::is_same<T, float>::value ? reinterpret_cast<uint16_t*>(tl.s2[t]) : nullptr;
   const int64_t end = min(start + (int64_t)kChunk, tl.numel[t]);
+  if constexpr (std::is_same<T, float>::value) {
+    // 4 elements per thread: 16-B loads/stores of p, g, momentum and one 8-B store of the bf16 shadow,
+    // when this tensor's pointers allow it (chunk starts are multiples of kChunk: aligned with them)
+    const uintptr_t al = reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) |
+                         reinterpret_cast<uintptr_t>(mom) | (reinterpret_cast<uintptr_t>(shadow) << 1);
+    if ((al & 15) == 0 && (mom != nullptr || h.mu == 0.f)) {
+      const int64_t vend = start + ((end - start) & ~(int64_t)3);
+      for (int64_t i = start + 4 * threadIdx.x; i < vend; i += 4 * kBlock) {
+        const float4 pv = *reinterpret_cast<const float4*>(p + i);
+        const float4 gv = *reinterpret_cast<const float4*>(g + i);
+        float pa[4] = {pv.x, pv.y, pv.z, pv.w};
+        const float ga[4] = {gv.x, gv.y, gv.z, gv.w};
+        float ma[4] = {0.f, 0.f, 0.f, 0.f};
+        if (mom != nullptr && h.mu != 0.f && !first) {
+          const float4 mv = *reinterpret_cast<const float4*>(mom + i);
+          ma[0] = mv.x, ma[1] = mv.y, ma[2] = mv.z, ma[3] = mv.w;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float d = ga[k] * h.gscale + h.wd * pa[k];
+          if (mom != nullptr && h.mu != 0.f) {
+            ma[k] = first ? d : h.mu * ma[k] + (1.f - h.damp) * d;
+            d = h.nesterov ? d + h.mu * ma[k] : ma[k];
+          }
+          pa[k] = pa[k] - h.lr * d;
+        }
+        *reinterpret_cast<float4*>(p + i) = make_float4(pa[0], pa[1], pa[2], pa[3]);
+        if (mom != nullptr && h.mu != 0.f) *reinterpret_cast<float4*>(mom + i) = make_float4(ma[0], ma[1], ma[2], ma[3]);
+        if (shadow) *reinterpret_cast<uint2*>(shadow + i) = make_uint2(pack_bf16x2(pa[0], pa[1]), pack_bf16x2(pa[2], pa[3]));
+      }
+      for (int64_t i = vend + threadIdx.x; i < end; i += kBlock) {  // tail (< 4 elements)
+        const float nv = sgd_update(p[i], g[i], mom, i, first, h);
+        p[i] = nv;
+        if (shadow) shadow[i] = f32_to_bf16(nv);
+      }
+      return;
+    }
+  }
   for (int64_t i = start + threadIdx.x; i < end; i += kBlock) {
     const float pv = Cvt<T>::load(p, i);
     const float nv = sgd_update(pv, Cvt<T>::load(g, i), mom, i, first, h);
