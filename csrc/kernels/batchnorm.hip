@@ -16,7 +16,7 @@
 // grid (row blocks, channel tiles): threads of a block cover TC channel vectors
 // x RPI rows and walk the block's row range; partial sums are combined in LDS,
 // written per row block, and the LAST row block of each channel tile to finish
-// (atomic ticket, agent-scope fences across the XCD L2s) reduces the partials
+// (atomic ticket; sc1 partial stores/loads, see last_block) reduces the partials
 // in fixed order (deterministic), computes the per-channel coefficients and
 // re-arms its ticket. So a BN forward is 2 launches (stats, apply) and a
 // backward 2 launches (reduce, apply).
@@ -196,12 +196,29 @@ __device__ __forceinline__ void block_rows_sum(float (&acc)[NS][V], float* sh, i
   }
 }
 
+// Partials cross workgroups through sc1 (write-through, L1-bypassing) agent-scope relaxed stores and
+// loads; the ticket's returned value names the last arriver (MI355X_MICROARCH.md, hand-off table row
+// 1). The agent-scope release fence this replaced wrote back the XCD L2's dirty lines once per
+// workgroup -- with the backward's g tensor streaming out through those L2s, a per-block cost at the
+// tail of every reduction (profiles/r3_convbn.md shows the same fence at +110 us on a GEMM).
+typedef __attribute__((address_space(1))) float gfloat_t;
+// PTDT_BN_FENCE=1 (A/B measurements only): plain partial stores/loads behind the agent-scope
+// release (every block) and acquire (last block) fences this hand-off replaced.
+__device__ __forceinline__ void st_sc1(float* p, float v, bool fence = false) {
+  if (fence) *p = v;
+  else __hip_atomic_store((gfloat_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p, bool fence = false) {
+  if (fence) return *p;
+  return __hip_atomic_load((gfloat_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Last block of a channel tile: sum the gx row-block partials (two [gx][C] slabs)
 // of the tile's `width` channels with ALL threads -- thread (part, ch) adds
 // partials part, part + P, ... with 4 loads in flight, then the P part-sums are
 // added in part order through LDS (deterministic). Result in threads t < width.
 __device__ __forceinline__ void combine_partials(const float* ws, int gx, int C, int cbase, int width, float* sh,
-                                                 double& s0, double& s1) {
+                                                 double& s0, double& s1, bool fence) {
   const int P = kRed / width;
   const int t = threadIdx.x, ch = t % width, part = t / width;
   const int c = cbase + ch;
@@ -214,8 +231,8 @@ __device__ __forceinline__ void combine_partials(const float* ws, int gx, int C,
       float u[4], v[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        u[k] = w0[(int64_t)(b + k * P) * C + c];
-        v[k] = w1[(int64_t)(b + k * P) * C + c];
+        u[k] = ld_sc1(w0 + (int64_t)(b + k * P) * C + c, fence);
+        v[k] = ld_sc1(w1 + (int64_t)(b + k * P) * C + c, fence);
       }
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -224,8 +241,8 @@ __device__ __forceinline__ void combine_partials(const float* ws, int gx, int C,
       }
     }
     for (; b < gx; b += P) {
-      a0 += (double)w0[(int64_t)b * C + c];
-      a1 += (double)w1[(int64_t)b * C + c];
+      a0 += (double)ld_sc1(w0 + (int64_t)b * C + c, fence);
+      a1 += (double)ld_sc1(w1 + (int64_t)b * C + c, fence);
     }
   }
   __syncthreads();  // the reduction slots in sh are free again
@@ -244,21 +261,20 @@ __device__ __forceinline__ void combine_partials(const float* ws, int gx, int C,
   }
 }
 
-// Atomic ticket: true in exactly one block per channel tile (the last to arrive),
-// after every block's partials are visible to it. The hand-off recipe of
-// cdna_hip_programming.md §6 G16 (per-XCD L2s are not coherent): plain partial
-// stores drained by every wave, barrier, lane 0 agent-scope release + drain, then
-// the relaxed agent-scope ticket; the last arriver's lane 0 agent-scope acquire
-// + drain, barrier, plain loads. The flag travels through the kernel's one LDS array.
-__device__ __forceinline__ bool last_block(int* ticket, int* sh_flag) {
+// Atomic ticket: true in exactly one block per channel tile (the last to arrive), after every
+// block's sc1 partial stores have landed (each wave drains its own, then the barrier), told by the
+// value the relaxed agent-scope add returns. The flag travels through the kernel's one LDS array.
+__device__ __forceinline__ bool last_block(int* ticket, int* sh_flag, bool fence) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (fence) {  // A/B: the replaced form (write-back of this XCD's L2 before the ticket)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     const int prev = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = prev == (int)gridDim.x - 1;
-    if (last) {
+    if (last && fence) {
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -329,12 +345,12 @@ __global__ void __launch_bounds__(kRed) bn_stats_kernel(const T* __restrict__ x,
   const int width = TC * V;
   const int c = blockIdx.y * width + tid;
   if (tid < width && c < C) {
-    ws[(int64_t)blockIdx.x * C + c] = part[0];
-    ws[((int64_t)gridDim.x + blockIdx.x) * C + c] = part[1];
+    st_sc1(ws + (int64_t)blockIdx.x * C + c, part[0], (p.fence_handoff != 0));
+    st_sc1(ws + ((int64_t)gridDim.x + blockIdx.x) * C + c, part[1], (p.fence_handoff != 0));
   }
-  if (!last_block(tickets + blockIdx.y, flag)) return;
+  if (!last_block(tickets + blockIdx.y, flag, (p.fence_handoff != 0))) return;
   double s, q;
-  combine_partials(ws, (int)gridDim.x, C, blockIdx.y * width, width, sh, s, q);
+  combine_partials(ws, (int)gridDim.x, C, blockIdx.y * width, width, sh, s, q, (p.fence_handoff != 0));
   if (tid < width && c < C) {
     const double Kc = (double)Cvt<T>::load(x, c);
     const double ms = s / (double)M;
@@ -521,12 +537,12 @@ __global__ void __launch_bounds__(kRed) bn_bwd_reduce_kernel(const T* __restrict
   const int width = TC * V;
   const int c = blockIdx.y * width + tid;
   if (tid < width && c < C) {
-    ws[(int64_t)blockIdx.x * C + c] = part[0];
-    ws[((int64_t)gridDim.x + blockIdx.x) * C + c] = part[1];
+    st_sc1(ws + (int64_t)blockIdx.x * C + c, part[0], (p.fence_handoff != 0));
+    st_sc1(ws + ((int64_t)gridDim.x + blockIdx.x) * C + c, part[1], (p.fence_handoff != 0));
   }
-  if (!last_block(tickets + blockIdx.y, flag)) return;
+  if (!last_block(tickets + blockIdx.y, flag, (p.fence_handoff != 0))) return;
   double sdy, sdx;
-  combine_partials(ws, (int)gridDim.x, C, blockIdx.y * width, width, sh, sdy, sdx);
+  combine_partials(ws, (int)gridDim.x, C, blockIdx.y * width, width, sh, sdy, sdx, (p.fence_handoff != 0));
   if (tid < width && c < C) {
     const double invstd = p.invstd[c], mean = p.mean[c];
     const double w = p.weight ? p.weight[c] : 1.0;
@@ -789,8 +805,16 @@ int bn_num_tickets(int C, int dtype) {
   return (cv + TC - 1) / TC;
 }
 
-hipError_t bn_forward_train(const BnFwdArgs& a, hipStream_t s) {
-  if (a.M <= 0 || a.C <= 0) return hipErrorInvalidValue;
+// PTDT_BN_FENCE=1: the fence-based partial hand-off, for same-box A/B measurements only
+int fence_handoff() {
+  static const int v = env_int("PTDT_BN_FENCE", 0) != 0;
+  return v;
+}
+
+hipError_t bn_forward_train(const BnFwdArgs& a0, hipStream_t s) {
+  if (a0.M <= 0 || a0.C <= 0) return hipErrorInvalidValue;
+  BnFwdArgs a = a0;
+  a.p.fence_handoff = fence_handoff();
   return a.dtype == kF32 ? fwd_impl<float>(a, s) : fwd_impl<uint16_t>(a, s);
 }
 
@@ -801,8 +825,10 @@ hipError_t bn_apply(const void* x, const void* residual, void* y, int dtype, con
                        : apply_impl<uint16_t>(x, residual, y, scale, shift, M, C, relu, s);
 }
 
-hipError_t bn_backward(const BnBwdArgs& a, hipStream_t s) {
-  if (a.M <= 0 || a.C <= 0) return hipErrorInvalidValue;
+hipError_t bn_backward(const BnBwdArgs& a0, hipStream_t s) {
+  if (a0.M <= 0 || a0.C <= 0) return hipErrorInvalidValue;
+  BnBwdArgs a = a0;
+  a.p.fence_handoff = fence_handoff();
   return a.dtype == kF32 ? bwd_impl<float>(a, s) : bwd_impl<uint16_t>(a, s);
 }
 

@@ -321,6 +321,7 @@ struct BnParams {
   float momentum, eps;
   float* mean; float* invstd;               // saved for backward
   float* scale; float* shift;               // y = x*scale + shift
+  int fence_handoff = 0;                    // A/B only (PTDT_BN_FENCE=1): the old release/acquire hand-off
 };
 struct BnFwdArgs {
   const void* x; const void* residual; void* y;  // residual may be null
@@ -355,6 +356,7 @@ struct BnBwdParams {
   const float* scale; const float* shift;   // forward scale/shift: ReLU mask from x when y is null
   float* dweight; float* dbias;             // may be null
   float* coef_a; float* coef_b; float* coef_c;  // scratch [C] each
+  int fence_handoff = 0;                    // A/B only (PTDT_BN_FENCE=1), as BnParams
 };
 struct BnBwdArgs {
   const void* dy; const void* x; const void* y;  // y: forward output (ReLU mask) or null: mask from x
