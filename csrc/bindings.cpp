@@ -1552,6 +1552,7 @@ PYBIND11_MODULE(_C, m) {
       .def("buckets", &Reducer::buckets)
       .def("bucket_tensors", &Reducer::bucket_tensors)
       .def("zero_grads", &Reducer::zero_grads)
+      .def("zero_grads_except", &Reducer::zero_grads_except)
       .def("grad_view", &Reducer::grad_view)
       .def_property_readonly("iteration", &Reducer::iteration)
       .def_property_readonly("in_backward", &Reducer::in_backward);

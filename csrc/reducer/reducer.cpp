@@ -150,6 +150,17 @@ void Reducer::zero_grads() {
   for (size_t i = 0; i < params_.size(); ++i) ensure_view((int64_t)i);
 }
 
+void Reducer::zero_grads_except(const std::vector<int64_t>& skip) {
+  std::vector<char> sk(params_.size(), 0);
+  for (int64_t i : skip)
+    if (i >= 0 && i < (int64_t)params_.size()) sk[i] = 1;
+  for (size_t i = 0; i < params_.size(); ++i) {
+    if (sk[i]) continue;
+    ensure_view((int64_t)i);
+    params_[i].mutable_grad().zero_();
+  }
+}
+
 void Reducer::prepare_for_backward(bool sync) {
   sync_ = sync;
   in_backward_ = true;

@@ -70,6 +70,9 @@ class Reducer {
   int64_t iteration() const { return iteration_; }
   bool in_backward() const { return in_backward_; }
   void zero_grads();
+  // Zero only the slots of the parameters NOT in `skip` (their .grad re-bound to the views): the
+  // skipped ones are grad-sink parameters whose producer overwrites the whole slot every backward.
+  void zero_grads_except(const std::vector<int64_t>& skip);
   // A fresh view of parameter i's slot in its bucket (the parameter's own strides):
   // autograd "steals" it as .grad when a cast's backward writes the gradient straight
   // into it (ops/conv.py grad sinks), so no separate accumulate kernel runs.

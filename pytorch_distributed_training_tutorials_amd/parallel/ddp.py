@@ -113,7 +113,8 @@ class DistributedDataParallel(nn.Module):
         self._hooks = [p.register_post_accumulate_grad_hook(self._make_hook(i)) for i, p in enumerate(params)]
         # grad sinks (ops/conv.py): weights cast through SinkCast land their gradient directly in
         # the bucket slot when .grad is None, which zero_grad arranges for exactly these params
-        self._sink_params = []
+        self._sink_params, self._sink_idx = [], []
+        self._params = params
         self._forwards = 0
         self._defer, self._pending, self._remaining = False, {}, {}
         if self.device.type == "cuda":
@@ -135,6 +136,8 @@ class DistributedDataParallel(nn.Module):
                     if self._defer:
                         p._ptdt_grad_defer = self._make_defer(i)
                     self._sink_params.append(p)
+                    self._sink_idx.append(i)
+        self._sink_ids = set(self._sink_idx)
 
     # --------------------------------------------------------------- internals
     def _verify_shapes(self):
@@ -276,7 +279,7 @@ class DistributedDataParallel(nn.Module):
                 del p._ptdt_grad_sink
             if getattr(p, "_ptdt_grad_defer", None) is not None:
                 del p._ptdt_grad_defer
-        self._sink_params = []
+        self._sink_params, self._sink_idx, self._sink_ids = [], [], set()
 
     def __del__(self):
         try:
@@ -288,7 +291,14 @@ class DistributedDataParallel(nn.Module):
 
     def zero_grad(self, set_to_none: bool = False):
         """Zero the gradient buckets in place (keeps .grad as bucket views; grad-sink
-        parameters get ``None``, refilled in place by their cast's backward)."""
-        self.reducer.zero_grads()
+        parameters get ``None``, refilled in place by their cast's backward). When the sinks
+        cover most parameters (ResNet-50: all but fc.bias) only the other slots are zeroed:
+        every sink's producer overwrites its whole slot (a producer that does not -- a second
+        use, an unused parameter -- goes through the reducer's copy / zero-on-demand path), so
+        zeroing the full 102 MB of buckets each step was a wasted pass."""
+        if self._sink_params and len(self._sink_ids) * 2 >= len(self._params):
+            self.reducer.zero_grads_except(self._sink_idx)
+        else:
+            self.reducer.zero_grads()
         for p in self._sink_params:
             p.grad = None
