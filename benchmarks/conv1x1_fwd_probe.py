@@ -55,13 +55,17 @@ def main():
             w2 = (torch.randn(cout, cin, device=dev) * 0.05).to(torch.bfloat16)
             rec = {"H": hw, "Cin": cin, "Cout": cout, "M": M, "per_step": cnt}
             res = {}
+            splits = (0, 1) if (cin, cout) == (64, 256) else (0,)
             for _ in range(a.rounds):
-                for cfg in range(4):
-                    os.environ["PTDT_C1_CFG"] = str(cfg)
-                    res.setdefault(cfg, []).append(timed(conv1x1_stats_probe(x2, w2, 0)))
+                for sp in splits:
+                    os.environ["PTDT_C1_SPLIT"] = str(sp)
+                    for cfg in range(4):
+                        os.environ["PTDT_C1_CFG"] = str(cfg)
+                        res.setdefault(cfg + 10 * sp, []).append(timed(conv1x1_stats_probe(x2, w2, 0)))
             os.environ.pop("PTDT_C1_CFG")
+            os.environ.pop("PTDT_C1_SPLIT")
             for cfg, ts in res.items():
-                rec[f"cfg{cfg}_us"] = round(statistics.median(ts), 1)
+                rec[f"cfg{cfg % 10}{'_split' if cfg >= 10 else ''}_us"] = round(statistics.median(ts), 1)
             rec["GBps_cfg0"] = round(2 * M * (cin + cout) / (rec["cfg0_us"] * 1e-6) / 1e9)
             print(json.dumps(rec), flush=True)
         return

@@ -411,6 +411,13 @@ bool dispatch(int K, int N, F&& f) {
     go(std::integral_constant<int, k>{}, std::integral_constant<int, n>{}, std::integral_constant<int, ns>{}); \
     return true;                                                                                         \
   }
+  // 64 -> 256 as two 128-channel slabs: half the per-lane statistics registers (152 VGPRs, 3 waves per
+  // SIMD instead of 2), X read twice: 60.3 vs 65.8 us (profiles/r3_convbn_stream_sweep_split.jsonl);
+  // PTDT_C1_SPLIT=0 keeps one slab
+  if (K == 64 && N == 256 && env_int("PTDT_C1_SPLIT", 1) == 1) {
+    go(std::integral_constant<int, 64>{}, std::integral_constant<int, 256>{}, std::integral_constant<int, 2>{});
+    return true;
+  }
   PTDT_C1(64, 64, 1) PTDT_C1(64, 256, 1) PTDT_C1(256, 64, 1) PTDT_C1(256, 128, 1)
   PTDT_C1(128, 512, 4) PTDT_C1(256, 1024, 8)
 #undef PTDT_C1
