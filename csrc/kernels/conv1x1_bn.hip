@@ -72,12 +72,20 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// 16-B chunk c of LDS row r (rows of K bf16): the 8 chunks of every 64-wide k block are XOR-swizzled
-// by (r >> 1) & 7, so the 16 lanes of a fragment read (16 consecutive rows, one chunk) hit 16
-// distinct 16-B slots
+// 16-B chunk c of LDS row r (rows of K bf16) is stored in slot swz(r, c) of the row, so the 16 lanes of
+// a fragment read (16 consecutive rows, one chunk) hit 16 distinct 16-B slots
+template <int K>
+__device__ __forceinline__ int swz(int r, int c) {
+  // rows of 128 B (K = 64): XOR the 8 chunks of the row by (r >> 1) & 7 (two rows share a 256-B bank row);
+  // rows of >= 256 B: XOR the chunk index by r & 15, so 16 consecutive rows land on 16 distinct 16-B slots
+  // of the bank row (the (r >> 1) & 7 form left two rows of a fragment read on one bank: PMC
+  // SQ_LDS_BANK_CONFLICT 3.6-7.2M cycles per launch, profiles/r3_pmc_convbn_stream.md). An involution.
+  if constexpr (K >= 128) return c ^ (r & 15);
+  else return (c & ~7) | ((c & 7) ^ ((r >> 1) & 7));
+}
 template <int K>
 __device__ __forceinline__ int lds_off(int r, int c) {
-  return r * (K * 2) + (((c & ~7) | ((c & 7) ^ ((r >> 1) & 7))) * 16);
+  return r * (K * 2) + swz<K>(r, c) * 16;
 }
 
 // compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. n-1
@@ -153,7 +161,7 @@ __global__ void __launch_bounds__(NW * 64, 2) conv1x1_bn_stream_kernel(const uin
       const int p = i * S::NT + tid;  // 16-B chunk of the block image (linear LDS order)
       const int r = p / (K / 8), slot = p % (K / 8);
       // the chunk stored in LDS slot `slot` of row r is logical chunk c (the swizzle is an involution)
-      const int c = (slot & ~7) | ((slot & 7) ^ ((r >> 1) & 7));
+      const int c = swz<K>(r, slot);
       const int gr = min(row0 + r, M - 1);
       const uint16_t* g = X + (int64_t)gr * K + c * 8;
       __builtin_amdgcn_global_load_lds((gbl_void*)g, (lds_void*)(dst0 + (i * S::NT + wid * 64) * 16), 16, 0, 0);
