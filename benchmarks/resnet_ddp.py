@@ -45,6 +45,10 @@ def main(argv=None):
                          "both in this process after warm-up and keep the faster (auto: the eager loop's cost "
                          "depends on the host, the graph's does not)")
     ap.add_argument("--no_graph", action="store_true", help="= --graph off")
+    ap.add_argument("--pre_steps", type=int, default=None,
+                    help="untimed training steps before --warmup (default: torch impl runs as many as the native "
+                         "--graph auto path does before its warm-up, so both report the loss after the same number "
+                         "of steps)")
     ap.add_argument("--no_cudnn_benchmark", action="store_true",
                     help="keep MIOpen's heuristic solver choice (default: exhaustive find per conv shape)")
     a = ap.parse_args(argv)
@@ -98,11 +102,13 @@ def main(argv=None):
         return loss
 
     ab = None
+    executed = 0  # training steps run before the timed loop's warm-up (the comparator runs as many)
     if graphed:  # utils/graphs.py: eager warm-up steps on a side stream, then one hipGraph per step
         from pytorch_distributed_training_tutorials_amd.utils.graphs import GraphedStep
 
         eager = step
         gstep = GraphedStep(eager, dev, comm=comm, warmup=max(3, a.warmup))
+        executed += max(3, a.warmup)
         step = gstep
         if mode == "auto":  # interleaved A/B in this process: 3 rounds of 4 steps each way
             ab = {"eager": [], "graph": []}
@@ -115,6 +121,7 @@ def main(argv=None):
                         fn()
                     torch.cuda.synchronize(dev)
                     ab[name].append((time.perf_counter() - t0) / 4 * 1e3)
+                    executed += 4
             med = {k: sorted(v)[1] for k, v in ab.items()}
             win = "graph" if med["graph"] <= med["eager"] else "eager"
             if world > 1:  # every rank must take the same path (the graph holds collectives)
@@ -124,8 +131,14 @@ def main(argv=None):
             graphed = win == "graph"
             step = gstep if graphed else eager
             ab = {k: round(v, 3) for k, v in med.items()}
+    for _ in range(a.pre_steps if a.pre_steps is not None else (max(3, a.warmup) + 24 if a.impl == "torch" else 0)):
+        # comparator: as many steps before the timed region as the native default mode runs
+        # (GraphedStep warm-up max(3, warmup) + the 3 x (4 eager + 4 replay) A/B)
+        step()
+        executed += 1
     for _ in range(a.warmup):
         step()
+    executed += a.warmup
     comm.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
@@ -137,7 +150,18 @@ def main(argv=None):
     if world > 1:
         comm.all_reduce(el, "max")
     el = float(el.item())
-    if rank == 0:
+    final = float(loss.detach())
+    finite = final == final and abs(final) != float("inf")
+    if world > 1:  # every replica must be finite
+        f = torch.tensor([1.0 if finite else 0.0], device=dev)
+        comm.all_reduce(f, "min")
+        finite = bool(f.item() == 1.0)
+    if rank == 0 and not finite:
+        print(json.dumps({"metric": "ResNet-50 DDP training throughput (whole node)", "value": None,
+                          "error": f"non-finite training loss {final} after {executed + a.steps} steps: no throughput "
+                                   "is reported for a diverged run", "finite": False, "impl": a.impl,
+                          "graph_mode": mode, **({"tag": a.tag} if a.tag else {})}), flush=True)
+    elif rank == 0:
         print(json.dumps({
             "metric": "ResNet-50 DDP training throughput (whole node)", "value": round(a.steps * a.batch_size * world / el, 1),
             "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
@@ -147,7 +171,7 @@ def main(argv=None):
                        "parallelism": f"dp{world}", "channels_last": not a.no_channels_last},
             "impl": a.impl, "hipgraph": graphed, "graph_mode": mode, **({"ab_ms_per_step": ab} if ab else {}), "bn_dir": os.environ.get("PTDT_BN_DIR", "0"), "miopen_find": "exhaustive (cudnn.benchmark)" if torch.backends.cudnn.benchmark else "heuristic",
             "buckets_MB": [round(b / 2 ** 20, 2) for b in ddp.bucket_sizes_bytes()] if a.impl == "native" else None,
-            "final_loss": float(loss.detach()), **({"tag": a.tag} if a.tag else {}),
+            "final_loss": final, "finite": True, "steps_total": executed + a.steps, **({"tag": a.tag} if a.tag else {}),
         }), flush=True)
     env.destroy_process_group()
 

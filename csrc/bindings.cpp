@@ -722,8 +722,12 @@ Tensor sum_all_(Tensor x) {
 void col_sum_(Tensor x, Tensor out, bool accumulate) {
   check_gpu(x, "x");
   TORCH_CHECK(x.dim() == 2 && out.scalar_type() == at::kFloat && out.numel() == x.size(1));
+  TORCH_CHECK(out.is_cuda() && out.is_contiguous() && out.device() == x.device(), "col_sum_: out must be on x's device");
   c10::hip::HIPGuard guard(x.device().index());
-  hip_check(col_sum(x.data_ptr(), dt_of(x), x.size(0), x.size(1), out.data_ptr<float>(), accumulate, cur_stream(x)),
+  const int nsplit = col_sum_splits(x.size(0), x.size(1));
+  Tensor ws = nsplit > 1 ? at::empty({nsplit, x.size(1)}, out.options()) : Tensor();
+  hip_check(col_sum(x.data_ptr(), dt_of(x), x.size(0), x.size(1), out.data_ptr<float>(), accumulate,
+                    nsplit > 1 ? ws.data_ptr<float>() : nullptr, nsplit, cur_stream(x)),
             "col_sum");
 }
 

@@ -21,17 +21,41 @@ __global__ void __launch_bounds__(kBlock) relu_bwd_kernel(const T* dy, const T* 
     Cvt<T>::store(dx, i, Cvt<T>::load(y, i) > 0.f ? Cvt<T>::load(dy, i) : 0.f);
 }
 
-// out[c] (+)= sum_r x[r, c]; one thread per column strip, rows split over blockIdx.y.
+// out[c] (+)= sum_r x[r, c] in a FIXED order (no atomics, no memset: bit-identical
+// across launches, and nothing in it depends on a memset node when it is replayed
+// from a hipGraph -- a captured hipMemsetAsync was seen to zero only part of the
+// buffer once eager memsets had run between replays, profiles/r4_graph_memset.md).
+// A workgroup (4 waves) owns 64 columns (one per lane) and a row range; wave w sums
+// rows w, w+4, ...; the 4 partials meet in LDS in wave order. With nsplit > 1 the
+// row ranges write partials to ws[split][cols] and col_sum_finish adds them in order.
 template <typename T>
-__global__ void __launch_bounds__(kBlock) col_sum_kernel(const T* x, int64_t rows, int64_t cols,
-                                                         float* out, int rows_per) {
-  const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (c >= cols) return;
+__global__ void __launch_bounds__(kBlock) col_sum_kernel(const T* x, int64_t rows, int64_t cols, float* out,
+                                                         float* ws, int64_t rows_per, int accumulate) {
+  __shared__ float red[kBlock / 64][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
   const int64_t r0 = (int64_t)blockIdx.y * rows_per;
   const int64_t r1 = min(rows, r0 + rows_per);
   float s = 0.f;
-  for (int64_t r = r0; r < r1; ++r) s += Cvt<T>::load(x, r * cols + c);
-  atomicAdd(out + c, s);
+  if (c < cols)
+    for (int64_t r = r0 + w; r < r1; r += kBlock / 64) s += Cvt<T>::load(x, r * cols + c);
+  red[w][lane] = s;
+  __syncthreads();
+  if (w != 0 || c >= cols) return;
+  s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (ws != nullptr)
+    ws[(int64_t)blockIdx.y * cols + c] = s;
+  else
+    out[c] = accumulate ? out[c] + s : s;
+}
+
+__global__ void __launch_bounds__(kBlock) col_sum_finish_kernel(const float* ws, int nsplit, int64_t cols, float* out,
+                                                                int accumulate) {
+  const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int k = 0; k < nsplit; ++k) s += ws[(int64_t)k * cols + c];
+  out[c] = accumulate ? out[c] + s : s;
 }
 
 // Sum of all elements into out[0] (fp32 accumulation, fixed order: deterministic).
@@ -120,21 +144,33 @@ hipError_t relu_backward(const void* dy, const void* y, void* dx, int dtype, int
   return hipGetLastError();
 }
 
-hipError_t col_sum(const void* x, int dtype, int64_t rows, int64_t cols, float* out, int accumulate,
-                   hipStream_t s) {
+int col_sum_splits(int64_t rows, int64_t cols) {
+  const int64_t gx = (cols + 63) / 64;
+  int64_t want = (256 + gx - 1) / gx;              // ~256 workgroups in flight
+  const int64_t by_rows = (rows + 1023) / 1024;   // >= 1024 rows per split
+  if (want > by_rows) want = by_rows;
+  if (want > 64) want = 64;
+  return want < 1 ? 1 : (int)want;
+}
+
+hipError_t col_sum(const void* x, int dtype, int64_t rows, int64_t cols, float* out, int accumulate, float* ws,
+                   int nsplit, hipStream_t s) {
   if (cols <= 0) return hipSuccess;
-  if (!accumulate) PTDT_HIP_CHECK(hipMemsetAsync(out, 0, cols * sizeof(float), s));
-  if (rows <= 0) return hipSuccess;
-  const int gx = (int)((cols + kBlock - 1) / kBlock);
-  int gy = (int)((rows + 63) / 64);
-  if (gy > 1024) gy = 1024;
-  const int rows_per = (int)((rows + gy - 1) / gy);
+  if (nsplit < 1 || (nsplit > 1 && ws == nullptr)) return hipErrorInvalidValue;
+  if (rows < 0) rows = 0;
+  const int64_t rows_per = nsplit > 1 ? (rows + nsplit - 1) / nsplit : (rows > 0 ? rows : 1);
+  const dim3 grid((unsigned)((cols + 63) / 64), (unsigned)nsplit);
+  float* part = nsplit > 1 ? ws : nullptr;
   if (dtype == kF32)
-    hipLaunchKernelGGL(col_sum_kernel<float>, dim3(gx, gy), dim3(kBlock), 0, s, (const float*)x, rows,
-                       cols, out, rows_per);
+    hipLaunchKernelGGL(col_sum_kernel<float>, grid, dim3(kBlock), 0, s, (const float*)x, rows, cols, out, part,
+                       rows_per, accumulate);
   else
-    hipLaunchKernelGGL(col_sum_kernel<uint16_t>, dim3(gx, gy), dim3(kBlock), 0, s, (const uint16_t*)x,
-                       rows, cols, out, rows_per);
+    hipLaunchKernelGGL(col_sum_kernel<uint16_t>, grid, dim3(kBlock), 0, s, (const uint16_t*)x, rows, cols, out,
+                       part, rows_per, accumulate);
+  PTDT_HIP_CHECK(hipGetLastError());
+  if (nsplit > 1)
+    hipLaunchKernelGGL(col_sum_finish_kernel, dim3((unsigned)((cols + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, ws,
+                       nsplit, cols, out, accumulate);
   return hipGetLastError();
 }
 

@@ -337,10 +337,17 @@ __global__ void __launch_bounds__(512) i8_mm_t256_kernel(const int8_t* __restric
   i8_epilogue<FI, FJ>(e, acc, m0 + wr * 128, n0 + wc * 64, c, g);
 }
 
+__global__ void __launch_bounds__(kThreads) zero_u32_kernel(unsigned* p, int n) {
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (i < n) p[i] = 0u;
+}
+
 template <typename T>
 hipError_t outliers_t(const void* x, int M, int K, float threshold, uint8_t* mask, unsigned* ws, hipStream_t s) {
-  PTDT_HIP_CHECK(hipMemsetAsync(ws, 0, sizeof(unsigned) * (size_t)K, s));
+  // zeroed by a kernel, not hipMemsetAsync: graph-replayed memset nodes are unreliable once eager
+  // memsets run between replays (profiles/r4_graph_memset.md)
   const int cb = (K + kThreads - 1) / kThreads;
+  hipLaunchKernelGGL(zero_u32_kernel, dim3(cb), dim3(kThreads), 0, s, ws, K);
   if (M > 0) {
     const dim3 grid(cb, (M + kRowsPerChunk - 1) / kRowsPerChunk);
     hipLaunchKernelGGL(col_absmax_kernel<T>, grid, dim3(kThreads), 0, s, static_cast<const T*>(x), M, K, ws);

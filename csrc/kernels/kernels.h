@@ -255,8 +255,11 @@ hipError_t sum_all(const void* x, int dtype, int64_t n, float* out, hipStream_t 
 // One-thread completion mark for a graph-captured collective (csrc/comm/rccl_comm.cpp):
 // ++*ctr (device memory), then the new value is stored to the host-mapped mirror.
 hipError_t comm_done_mark(uint64_t* ctr, uint64_t* host_mirror, hipStream_t s);
-hipError_t col_sum(const void* x, int dtype, int64_t rows, int64_t cols, float* out, int accumulate,
-                   hipStream_t s);
+// Fixed-order column sums (deterministic; no atomics or memsets). nsplit > 1 needs a
+// float workspace of nsplit * cols; col_sum_splits picks nsplit for a shape.
+int col_sum_splits(int64_t rows, int64_t cols);
+hipError_t col_sum(const void* x, int dtype, int64_t rows, int64_t cols, float* out, int accumulate, float* ws,
+                   int nsplit, hipStream_t s);
 hipError_t fill_f32(float* x, float v, int64_t n, hipStream_t s);
 hipError_t cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
 hipError_t cast_bf16_f32(const uint16_t* x, float* y, int64_t n, hipStream_t s);

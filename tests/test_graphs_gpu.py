@@ -64,6 +64,117 @@ def _run(dev, graphed: bool, steps: int, init_state):
     return [float(v) for v in losses], {k: v.detach().float().cpu() for k, v in model.state_dict().items()}
 
 
+def test_col_sum_replay_after_eager_launches(dev, native):
+    """The Linear bias-gradient column sum replayed from a graph after eager launches of the same op
+    (the round-3 ResNet divergence: the captured zero-fill of its accumulator stopped being applied
+    once eager steps had run between replays, so fc.bias's gradient summed onto stale memory)."""
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randn(128, 1000, generator=g).to(dev, torch.bfloat16)
+    out = torch.empty(1000, device=dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        native.col_sum_(x, out, False)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    torch.cuda.synchronize(dev)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        native.col_sum_(x, out, False)
+    torch.cuda.synchronize(dev)
+    want = x.float().sum(0)
+    for rnd in range(3):
+        for _ in range(4):  # eager launches of the op on other buffers
+            x2 = torch.randn(128, 1000, device=dev, dtype=torch.bfloat16)
+            o2 = torch.full((1000,), 123.0, device=dev)
+            native.col_sum_(x2, o2, False)
+            torch.testing.assert_close(o2, x2.float().sum(0), rtol=1e-4, atol=1e-3)
+        out.fill_(7e30)
+        graph.replay()
+        torch.cuda.synchronize(dev)
+        torch.testing.assert_close(out, want, rtol=1e-4, atol=1e-3, msg=lambda m: f"round {rnd}: {m}")
+
+
+def test_col_sum_deterministic(dev, native):
+    """Bias gradients are fixed-order sums: bit-identical across launches (no atomics)."""
+    for rows, cols in ((128, 1000), (32, 1), (20000, 96), (3, 4100)):
+        x = torch.randn(rows, cols, device=dev, dtype=torch.bfloat16)
+        a = torch.empty(cols, device=dev)
+        b = torch.empty(cols, device=dev)
+        native.col_sum_(x, a, False)
+        native.col_sum_(x, b, False)
+        assert torch.equal(a, b)
+        torch.testing.assert_close(a, x.double().sum(0).float(), rtol=1e-4, atol=2e-3)
+        c = torch.ones(cols, device=dev)
+        native.col_sum_(x, c, True)
+        torch.testing.assert_close(c, a + 1, rtol=1e-5, atol=1e-4)
+
+
+def _interleaved(dev, pattern: str, init_state, lr: float = 0.05, warm: int = 2):
+    """One trajectory: ``warm`` eager warm-up steps inside GraphedStep, then ``pattern`` (E = eager
+    step, R = graph replay) -- benchmarks/resnet_ddp.py's --graph auto A/B does exactly this."""
+    from pytorch_distributed_training_tutorials_amd.models.resnet import resnet50
+    from pytorch_distributed_training_tutorials_amd.ops.loss import cross_entropy
+    from pytorch_distributed_training_tutorials_amd.ops.optim import FusedSGD
+    from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
+    from pytorch_distributed_training_tutorials_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_distributed_training_tutorials_amd.utils.graphs import GraphedStep
+
+    comm = comm_mod.get_default(dev)
+    model = resnet50(num_classes=10).to(dev).to(memory_format=torch.channels_last)
+    model.load_state_dict(init_state)
+    ddp = DistributedDataParallel(model, device_ids=[dev.index], comm=comm)
+    opt = FusedSGD(model.parameters(), lr=lr, momentum=0.9, weight_decay=1e-4, bf16_shadow=True)
+    g = torch.Generator(device="cpu").manual_seed(7)
+    x = torch.randn(4, 3, 64, 64, generator=g).to(dev).contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, 10, (4,), generator=g).to(dev)
+    losses = []
+
+    def step():
+        ddp.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            out = ddp(x)
+        loss = cross_entropy(out.float(), y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.detach().clone())
+        return loss
+
+    if "R" in pattern:
+        gs = GraphedStep(step, dev, comm=comm, warmup=warm)
+        losses.pop()  # the capture call's loss (nothing executed)
+    else:
+        gs = None
+        pattern = "E" * warm + pattern
+    for c in pattern:
+        if c == "E":
+            step()
+        else:
+            losses.append(gs().detach().clone())
+    torch.cuda.synchronize(dev)
+    return [float(v) for v in losses], {k: v.detach().float().cpu() for k, v in model.state_dict().items()}
+
+
+def test_interleaved_eager_and_replay_matches_pure_eager(pg, dev):
+    """E E R R E E R R ... (18 steps after warm-up) follows the pure-eager trajectory."""
+    from pytorch_distributed_training_tutorials_amd.models.resnet import resnet50
+
+    torch.manual_seed(0)
+    init = {k: v.clone() for k, v in resnet50(num_classes=10).state_dict().items()}
+    old = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = True, False
+    try:
+        pat = "EERR" * 4 + "ER"
+        la, sa = _interleaved(dev, "E" * len(pat), init)
+        lb, sb = _interleaved(dev, pat, init)
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
+    assert len(la) == len(lb) == len(pat) + 2
+    assert all(torch.isfinite(torch.tensor(lb)))
+    torch.testing.assert_close(torch.tensor(lb), torch.tensor(la), rtol=2e-3, atol=2e-3)
+    for k in sa:
+        torch.testing.assert_close(sb[k], sa[k], rtol=2e-3, atol=2e-3, msg=lambda m, k=k: f"{k}: {m}")
+
+
 def test_graphed_resnet_ddp_step_matches_eager(pg, dev):
     from pytorch_distributed_training_tutorials_amd.models.resnet import resnet50
 
