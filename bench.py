@@ -367,7 +367,7 @@ def _mlp_side(args, rank, world, dev, comm, xg):
     plan = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses)
     plan.launch_at(n_w, 0)
     torch.cuda.synchronize(dev)
-    t = _timed(comm, dev, lambda: plan.launch_at(n_t, n_w))
+    t = _timed(comm, dev, lambda: plan.launch_at(n_t, n_w), label="mlp_side")
     failed = xg is not None and _xgmi_failed(comm, dev, xg, "MLP side measurement")
     return {"mlp_us_per_step": None if failed else round(1e6 * t / n_t, 3),
             "mlp_samples_per_s": None if failed else round(n_t * args.batch_size * world / t, 1),
@@ -435,7 +435,7 @@ def run_autograd(args, rank, world, dev, comm):
 
 
 # --------------------------------------------------------------------------- reference
-def run_reference(args, rank, world, dev, comm, steps=None, warmup=None):
+def run_reference(args, rank, world, dev, comm, steps=None, warmup=None, label: str = "headline"):
     """Stock PyTorch-ROCm loop with the reference's structure (comparator):
     reference ddp_gpus_torchrun.py:16-88 with synthetic data of the same shape."""
     import torch.nn.functional as F
@@ -483,7 +483,7 @@ def run_reference(args, rank, world, dev, comm, steps=None, warmup=None):
             opt.step()
 
     run(max(warmup, 1))
-    t = _timed(comm, dev, lambda: run(steps))
+    t = _timed(comm, dev, lambda: run(steps), label=label)
     return t, {"kernels": "stock torch: DataLoader+DistributedSampler, nn.Linear, F.cross_entropy, torch DDP, SGD"}
 
 
@@ -493,18 +493,49 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
-def _timed(comm, dev, fn):
+_TIMINGS: dict = {}  # label -> start skew / whole-node window of each timed region (reported in the JSON line)
+_SPIN: dict = {}
+
+
+def _spin(comm):
+    """The node-local spin barrier for ``comm`` (utils/spin_barrier.py), created once."""
+    key = id(comm)
+    if key not in _SPIN:
+        from pytorch_distributed_training_tutorials_amd.utils import spin_barrier
+
+        _SPIN[key] = spin_barrier.create(comm) if os.environ.get("PTDT_BENCH_SPIN", "1") != "0" else None
+    return _SPIN[key]
+
+
+def _timed(comm, dev, fn, label: str = "headline"):
+    """Elapsed seconds of ``fn`` (MAX over ranks): collective barrier + device sync, then the
+    node-local spin barrier (ranks released within ~1-2 us instead of the collective's tens of
+    us), then every rank reads CLOCK_MONOTONIC (one clock per node), runs ``fn``, syncs and reads
+    it again. The per-rank stamps are gathered afterwards: ``start_skew_us`` = max - min of the
+    start stamps, ``window_us`` = last end - first start (the whole-node wall window)."""
     comm.barrier()
     _sync(dev)
-    t0 = time.perf_counter()
+    spin = _spin(comm)
+    if spin is not None:
+        spin.wait()
+    m0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)
     fn()
     _sync(dev)
-    t1 = time.perf_counter()  # this rank's work is done; the barrier below only re-aligns the ranks
+    m1 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)  # this rank's work is done
     comm.barrier()
-    el = torch.tensor([t1 - t0], device=dev, dtype=torch.float64)
+    mine = (m1 - m0) * 1e-9
     if comm.world > 1:
-        comm.all_reduce(el, "max")
-    return float(el.item())
+        stamps = comm.all_gather_object((m0, m1))
+        t0s, t1s = [a for a, _ in stamps], [b for _, b in stamps]
+        el = max((b - a) * 1e-9 for a, b in stamps)
+        _TIMINGS[label] = {"start_skew_us": round((max(t0s) - min(t0s)) * 1e-3, 2),
+                           "end_skew_us": round((max(t1s) - min(t1s)) * 1e-3, 2),
+                           "window_us": round((max(t1s) - min(t0s)) * 1e-3, 2),
+                           "per_rank_elapsed_us": [round((b - a) * 1e-3, 2) for a, b in stamps],
+                           "release": "spin barrier (/dev/shm)" if spin is not None else "collective barrier"}
+        return el
+    _TIMINGS[label] = {"start_skew_us": 0.0, "window_us": round(mine * 1e6, 2)}
+    return mine
 
 
 def _record(args, world, value, elapsed, extra):
@@ -548,7 +579,7 @@ def _comparator(args, rank, world, dev, comm):
     """The stock PyTorch-ROCm loop at the same N, in this process, after the headline."""
     steps = args.ref_steps or max(args.steps, 256)
     warm = max(args.warmup, 32)
-    t, _ = run_reference(args, rank, world, dev, comm, steps=steps, warmup=warm)
+    t, _ = run_reference(args, rank, world, dev, comm, steps=steps, warmup=warm, label="comparator")
     sps = steps * args.batch_size * world / t
     return {"ref_samples_per_s": round(sps, 1), "ref_ms_per_step": round(1e3 * t / steps, 4), "ref_steps": steps,
             "ref_warmup": warm, "ref_engine": "stock torch DDP (RCCL) + DataLoader/DistributedSampler + nn.Linear + "
@@ -599,6 +630,7 @@ def main(argv=None):
         extra.update(_comparator(args, rank, world, dev, comm))
         extra["speedup_vs_torch"] = round(value / extra["ref_samples_per_s"], 3)
     dl.set_phase("report")
+    extra["timing"] = dict(_TIMINGS)
     rec = _record(args, world, value, elapsed, extra)
     if args.share_gpu:
         rec["rehearsal"] = f"{world} ranks sharing cuda:0 (no xGMI hop): protocol/correctness check, not a scaling number"

@@ -27,9 +27,10 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--top", type=int, default=12)
+    ap.add_argument("--nondet", action="store_true", help="cudnn.benchmark instead of deterministic MIOpen")
     a = ap.parse_args(argv)
-    torch.backends.cudnn.benchmark = False
-    torch.backends.cudnn.deterministic = True
+    torch.backends.cudnn.benchmark = a.nondet
+    torch.backends.cudnn.deterministic = not a.nondet
     from pytorch_distributed_training_tutorials_amd import native
     from pytorch_distributed_training_tutorials_amd.models.resnet import resnet50
     from pytorch_distributed_training_tutorials_amd.ops.loss import cross_entropy
@@ -116,10 +117,14 @@ def main(argv=None):
 
     dr = diffs(after_e, after_r)
     de = diffs(after_e, after_e2)
+    nan_r = [k for k, v in after_r.items() if v.is_floating_point() and not bool(torch.isfinite(v).all())]
+    nan_e = [k for k, v in after_e.items() if v.is_floating_point() and not bool(torch.isfinite(v).all())]
+    dr = [t for t in dr if t[0] == t[0]]
     print(json.dumps({"eager_steps_before": a.eager, "loss_eager": le, "loss_replay": lr_, "loss_eager_again": le2,
                       "replay_vs_eager_top": [(k, m, r) for m, r, k in dr[:a.top]],
                       "eager_vs_eager_top": [(k, m, r) for m, r, k in de[:4]],
-                      "n_tensors_differing": sum(1 for m, _, _ in dr if m > 0)}), flush=True)
+                      "n_tensors_differing": sum(1 for m, _, _ in dr if m > 0),
+                      "nonfinite_after_replay": nan_r, "nonfinite_after_eager": nan_e}), flush=True)
     env.destroy_process_group()
 
 

@@ -26,6 +26,12 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def _choices():
+    from pytorch_distributed_training_tutorials_amd.utils import tuning
+
+    return tuning.choices()
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--batch_size", type=int, default=128, help="per-GPU batch")
@@ -171,7 +177,7 @@ def main(argv=None):
                        "parallelism": f"dp{world}", "channels_last": not a.no_channels_last},
             "impl": a.impl, "hipgraph": graphed, "graph_mode": mode, **({"ab_ms_per_step": ab} if ab else {}), "bn_dir": os.environ.get("PTDT_BN_DIR", "0"), "miopen_find": "exhaustive (cudnn.benchmark)" if torch.backends.cudnn.benchmark else "heuristic",
             "buckets_MB": [round(b / 2 ** 20, 2) for b in ddp.bucket_sizes_bytes()] if a.impl == "native" else None,
-            "final_loss": final, "finite": True, "steps_total": executed + a.steps, **({"tag": a.tag} if a.tag else {}),
+            "final_loss": final, "finite": True, "kernel_choices": _choices(), "steps_total": executed + a.steps, **({"tag": a.tag} if a.tag else {}),
         }), flush=True)
     env.destroy_process_group()
 

@@ -264,6 +264,16 @@ __device__ __forceinline__ void combine_partials(const float* ws, int gx, int C,
 // Atomic ticket: true in exactly one block per channel tile (the last to arrive), after every
 // block's sc1 partial stores have landed (each wave drains its own, then the barrier), told by the
 // value the relaxed agent-scope add returns. The flag travels through the kernel's one LDS array.
+//
+// Memory-model note (ISA-level, gfx950): the HIP/LLVM model gives relaxed atomics no
+// happens-before, so correctness rests on the hardware, not the language: (1) the partials are
+// written with sc1 stores (write-through to the coherent level) and each wave waits vmcnt(0)
+// before the barrier, so they are globally visible before the ticket add issues; (2) the last
+// block reads them with sc1 loads, which miss the non-coherent caches. The compiler cannot move
+// those loads above the ticket: __syncthreads() after the flag write is a workgroup-scope
+// release/acquire fence pair, and the explicit signal fence below pins the order in the IR too.
+// tests/test_norm.py compares this hand-off with the fence-based one (PTDT_BN_FENCE=1) bit for bit
+// on many-block shapes.
 __device__ __forceinline__ bool last_block(int* ticket, int* sh_flag, bool fence) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -281,6 +291,7 @@ __device__ __forceinline__ bool last_block(int* ticket, int* sh_flag, bool fence
     *sh_flag = last;
   }
   __syncthreads();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // no load of the partials is hoisted above this point
   return *sh_flag != 0;
 }
 

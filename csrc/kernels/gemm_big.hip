@@ -437,6 +437,9 @@ __device__ __forceinline__ bool last_arrival(int* ticket, int count, int* sh_fla
     *sh_flag = last;
   }
   __syncthreads();
+  // relaxed atomics carry no happens-before in the HIP model: visibility rests on the sc1 stores /
+  // loads (see batchnorm.hip last_block); this fence keeps the partial loads below the ticket in the IR
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
   return *sh_flag != 0;
 }
 

@@ -130,6 +130,12 @@ def _fused_wins(x: torch.Tensor, w: torch.Tensor, tile: int) -> bool:
         return _CHOICE[key]
     if _MODE in ("1", "on"):
         return True
+    from ..utils import tuning
+
+    pin = tuning.pinned("convbn", key)
+    if pin is not None:
+        _CHOICE[key] = pin == "fused"
+        return _CHOICE[key]
     if torch.cuda.is_current_stream_capturing():
         return False
     C = native()
@@ -149,7 +155,9 @@ def _fused_wins(x: torch.Tensor, w: torch.Tensor, tile: int) -> bool:
         tf, tp = float("inf"), float("inf")
         for _ in range(5):
             tf, tp = min(tf, _time_us(fused, 1)), min(tp, _time_us(plain, 1))
-    _CHOICE[key] = tf < 0.97 * tp
+    local = "fused" if tf < 0.97 * tp else "unfused"
+    # rank 0's choice on every rank: DDP replicas must run the same BN statistics path (utils/tuning.py)
+    _CHOICE[key] = tuning.agree("convbn", key, local, ("unfused", "fused"), x.device) == "fused"
     return _CHOICE[key]
 
 

@@ -101,9 +101,17 @@ def _library(relu: bool = False, key=None, native_fn=None, library_fn=None) -> b
     hit = _TUNED.get(key)
     if hit is not None:
         return hit
+    from ..utils import tuning
+
+    pin = tuning.pinned("linear", key)
+    if pin is not None:
+        _TUNED[key] = pin == "library"
+        return _TUNED[key]
     if torch.cuda.is_current_stream_capturing():
         return True  # no timing inside a capture; the shape stays untuned
-    _TUNED[key] = _time(library_fn) <= _time(native_fn)
+    local = "library" if _time(library_fn) <= _time(native_fn) else "native"
+    # every DDP rank takes rank 0's engine (replicas must stay bit-identical; utils/tuning.py)
+    _TUNED[key] = tuning.agree("linear", key, local, ("native", "library"), torch.cuda.current_device()) == "library"
     return _TUNED[key]
 
 

@@ -106,8 +106,13 @@ class _BatchNormActFn(torch.autograd.Function):
                     sinks[k] = p._ptdt_grad_sink()
         dx, dw, db, dres = native().bn_bwd(dy, x, None, weight, stats, ctx.relu, want_dres, want_dw,
                                            ctx.tickets, sinks[0], sinks[1], dy2, mask)
-        if link_in is not None:  # delivered to the residual's producer instead of autograd
-            link_in.dres, dres = dres, None
+        if link_in is not None and dres is not None:  # delivered to the residual's producer instead of autograd
+            if link_in.dres is None:
+                link_in.dres, dres = dres, None
+            elif not ctx.needs_input_grad[3]:  # the link is taken (another consumer delivered): sum into it
+                link_in.dres = link_in.dres + dres
+                dres = None
+            # else: autograd adds this one (returned below), as _GradLinkFn does
         return (dx if ctx.needs_input_grad[0] else None, dw if want_dw else None, db if want_dw else None,
                 dres if (dres is not None and ctx.needs_input_grad[3]) else None, *([None] * 10))
 

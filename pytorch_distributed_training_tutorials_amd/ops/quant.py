@@ -92,11 +92,10 @@ class Int8Linear(nn.Module):
 
     def _llm_int8(self, x2: torch.Tensor) -> torch.Tensor:
         b = self.bias
-        if not use_native(x2):  # CPU tensors: the plain-PyTorch reference
+        if not use_native(x2) or x2.dtype not in _NATIVE_DTYPES or self.in_features % 16 != 0:
+            # CPU tensors, and GPU shapes / dtypes the int8 MFMA kernel has no instance for (its K step
+            # is 16: e.g. in_features = 40): the plain-PyTorch LLM.int8 product, same numerics
             return llm_int8_reference(x2, self.weight_q, self.weight_scale, b, self.threshold)
-        if x2.dtype not in _NATIVE_DTYPES or self.in_features % 16 != 0:
-            raise NotImplementedError(f"LLM.int8 on GPU: dtype {x2.dtype} (float32/bfloat16/float16) and "
-                                      f"in_features % 16 == 0 (got {self.in_features})")
         C = native()
         x2 = x2.contiguous()
         mask = C.int8_col_outliers(x2, self.threshold)

@@ -117,6 +117,8 @@ class DistributedDataParallel(nn.Module):
         self._params = params
         self._forwards = 0
         self._defer, self._pending, self._remaining = False, {}, {}
+        self._fwd_stream = None
+        self._multi_use = set()  # weights seen with a second, non-SinkCast use: never deferred again
         if self.device.type == "cuda":
             from ..ops.conv import Conv2d
             from ..ops.linear import Linear
@@ -135,6 +137,7 @@ class DistributedDataParallel(nn.Module):
                     p._ptdt_grad_sink = self._make_sink(i, p)
                     if self._defer:
                         p._ptdt_grad_defer = self._make_defer(i)
+                        self._hooks.append(p.register_hook(self._make_tied_check(i)))
                     self._sink_params.append(p)
                     self._sink_idx.append(i)
         self._sink_ids = set(self._sink_idx)
@@ -190,21 +193,52 @@ class DistributedDataParallel(nn.Module):
                         ddp.reducer.grad_view(j).copy_(g)
                         break
                 return True
-            if src.dtype != torch.bfloat16 or dst.dtype != torch.float32 or not _same_dense_layout(src, dst):
+            if (i in ddp._multi_use or src.dtype != torch.bfloat16 or dst.dtype != torch.float32
+                    or not _same_dense_layout(src, dst)):
                 return False
             ddp._pending.setdefault(b, []).append((i, src))
             return True
         return defer
 
+    def _make_tied_check(self, i: int):
+        """Leaf gradient pre-hook (runs on the SUM of every contribution, before AccumulateGrad) for a
+        deferred-cast weight. With one contribution the incoming gradient IS the slot view the sink
+        handed out, whose cast is still pending: nothing to do. A different tensor means autograd summed
+        another, non-SinkCast use of the weight (e.g. a Linear weight tied to an fp32 F.embedding) onto
+        the slot's STALE contents (zero_grad skips sink slots): the pending cast would then overwrite
+        that sum. Return ``g - stale + cast`` instead (the other use's gradient plus this one's), drop
+        the pending entry, and never defer this weight again."""
+        ref = weakref.ref(self)
+
+        def check(g):
+            ddp = ref()
+            if ddp is None or not ddp._defer:
+                return None
+            pend = ddp._pending.get(ddp._bucket_of.get(i))
+            if not pend:
+                return None
+            k = next((k for k, (j, _) in enumerate(pend) if j == i), None)
+            if k is None or g.data_ptr() == ddp._slot_ptr[i]:
+                return None
+            _, src = pend.pop(k)
+            ddp._multi_use.add(i)
+            return g - ddp.reducer.grad_view(i) + src.to(g.dtype)
+        return check
+
     def _index_buckets(self):
         self._buckets = [list(b) for b in self.reducer.buckets()]
         self._bucket_of = {int(i): b for b, ps in enumerate(self._buckets) for i in ps}
+        self._slot_ptr = {i: self.reducer.grad_view(i).data_ptr() for i in range(len(self._params))}
 
     def _flush_casts(self, b=None):
         keys = [b] if b is not None else list(self._pending)
         for k in keys:
             pend = self._pending.pop(k, None)
             if pend:
+                cur = torch.cuda.current_stream(self.device)
+                if cur != self._fwd_stream:  # hooks on another stream than the producers (an AccumulateGrad
+                    for _, g in pend:        # node kept from another stream): keep the sources alive for it
+                        g.record_stream(cur)
                 native().cast_multi_([self.reducer.grad_view(j) for j, _ in pend], [g for _, g in pend])
 
     def _make_hook(self, i: int):
@@ -253,6 +287,7 @@ class DistributedDataParallel(nn.Module):
             self._forwards += 1  # a new forward: every grad sink may be claimed once again
             if self._defer:
                 self._flush_casts()
+                self._fwd_stream = torch.cuda.current_stream(self.device)
                 self._remaining = {b: len(ps) for b, ps in enumerate(self._buckets)}
         return self.module(*args, **kwargs)
 

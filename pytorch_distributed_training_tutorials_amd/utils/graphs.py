@@ -34,6 +34,16 @@ import torch
 from ..ops.fused_step import WatchedGraph
 
 
+def _detach(out):
+    if isinstance(out, torch.Tensor):
+        return out.detach()
+    if isinstance(out, (tuple, list)):
+        return type(out)(_detach(o) for o in out)
+    if isinstance(out, dict):
+        return {k: _detach(v) for k, v in out.items()}
+    return out
+
+
 class GraphedStep:
     """``step = GraphedStep(fn, device, comm=comm)``; ``out = step()`` replays.
 
@@ -58,7 +68,12 @@ class GraphedStep:
         before = rc.captured if rc is not None else 0
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):
-            self.outputs = fn()
+            # detached: a captured loss that keeps its autograd graph alive also keeps every
+            # parameter's AccumulateGrad node alive -- nodes created on the capture stream, which
+            # later EAGER steps on another stream would then reuse: gradient accumulation and the
+            # DDP hooks run on the capture stream while their inputs come from the eager one
+            # (cross-stream frees of gradient buffers; the round-3 --graph auto divergence)
+            self.outputs = _detach(fn())
         torch.cuda.synchronize(device)
         self.graph = WatchedGraph(g, rc, (rc.captured - before) if rc is not None else 0)
         self.replays = 0

@@ -388,3 +388,41 @@ def ddp_wrapper_collectable(rank, world, port, out_dir):
     torch.save({"collected": ref() is None, "grads": all(p.grad is not None for p in model.parameters())},
                os.path.join(out_dir, f"r{rank}.pt"))
     destroy_process_group()
+
+
+def spin_barrier_check(rank, world, port, out_dir):
+    import time
+
+    _init(rank, world, port)
+    from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+    from pytorch_distributed_training_tutorials_amd.utils import spin_barrier
+
+    os.environ["LOCAL_WORLD_SIZE"] = str(world)
+    c = comm_mod.get_default(None)
+    bar = spin_barrier.create(c)
+    assert bar is not None
+    arrive, leave = [], []
+    for rnd in range(3):
+        if rank == rnd % world:
+            time.sleep(0.05)  # the late rank of this round
+        arrive.append(time.clock_gettime(time.CLOCK_MONOTONIC))
+        bar.wait()
+        leave.append(time.clock_gettime(time.CLOCK_MONOTONIC))
+    bar.close()
+    torch.save({"arrive": arrive, "leave": leave}, os.path.join(out_dir, f"r{rank}.pt"))
+    destroy_process_group()
+
+
+def tuning_agree(rank, world, port, out_dir):
+    """Each rank 'times' a different winner; utils.tuning.agree hands every rank rank 0's."""
+    _init(rank, world, port)
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+    from pytorch_distributed_training_tutorials_amd.utils import tuning
+
+    got = []
+    for k in range(3):
+        local = ("native", "library")[(rank + k) % 2]
+        got.append(tuning.agree("linear", ("nt", 128, 1000 + k, 2048), local, ("native", "library")))
+    torch.save({"got": got, "choices": tuning.choices()}, os.path.join(out_dir, f"r{rank}.pt"))
+    destroy_process_group()

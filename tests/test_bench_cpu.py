@@ -52,3 +52,36 @@ def test_bench_deadline_on_injected_hang():
     assert rec["phase"].startswith("headline")
     assert deadline <= rec["elapsed_s"] < deadline + 15
     assert wall < deadline + 90
+
+
+def test_bench_cpu_8_ranks_reports_start_skew():
+    """8 ranks (the driver's N = 8 shape) on gloo: the record carries the timed region's start skew
+    and whole-node window, and the spin barrier released every rank (skew well under a millisecond)."""
+    p, lines, _ = _run(8, ["--steps", "20", "--warmup", "5"], timeout=400)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert len(lines) == 1
+    tm = lines[0]["timing"]["headline"]
+    assert tm["release"].startswith("spin barrier")
+    assert len(tm["per_rank_elapsed_us"]) == 8
+    # (8 spinning processes on this 8-CPU container: allow scheduler noise; on the GPU node it is ~us)
+    assert 0.0 <= tm["start_skew_us"] < 20000.0, tm
+    assert tm["window_us"] >= max(tm["per_rank_elapsed_us"]) - 1.0
+
+
+def test_spin_barrier_releases_together(tmp_path):
+    """utils/spin_barrier.py over 4 gloo ranks: no wait() returns before every rank arrived (a rank
+    arriving 50 ms late holds the others), repeatedly."""
+    from torch.multiprocessing import spawn
+
+    from tests import _workers
+
+    world = 4
+    spawn(_workers.spin_barrier_check, args=(world, free_port(), str(tmp_path)), nprocs=world)
+    import torch
+
+    res = [torch.load(os.path.join(tmp_path, f"r{r}.pt")) for r in range(world)]
+    for rnd in range(3):
+        arrive = max(r["arrive"][rnd] for r in res)
+        for r in res:
+            assert r["leave"][rnd] >= arrive  # released only after the last arrival
+        assert max(r["leave"][rnd] for r in res) - arrive < 0.05  # and promptly

@@ -104,3 +104,30 @@ def test_ddp_wrapper_is_collectable(tmp_path):
     spawn(_workers.ddp_wrapper_collectable, args=(2, free_port(), str(tmp_path)), nprocs=2)
     for r in _load(tmp_path, 2):
         assert r["collected"] and r["grads"]
+
+
+def test_kernel_choices_agree_across_ranks(tmp_path):
+    """Per-shape engine selection (ops/linear.py, ops/convbn.py) is rank 0's on every rank, even when
+    the ranks' own timings disagree (ADVICE r3 / VERDICT r3 #7)."""
+    world = 2
+    spawn(_workers.tuning_agree, args=(world, free_port(), str(tmp_path)), nprocs=world)
+    res = _load(tmp_path, world)
+    assert res[0]["got"] == res[1]["got"] == ["native", "library", "native"]
+    assert res[0]["choices"] == res[1]["choices"]
+
+
+def test_tuning_table_pins_choice(tmp_path, monkeypatch):
+    import json
+
+    from pytorch_distributed_training_tutorials_amd.utils import tuning
+
+    path = tmp_path / "t.json"
+    path.write_text(json.dumps({"linear": {"nt,128,1000,2048": "library"}, "convbn": {"401408,64,256,0": "fused"}}))
+    monkeypatch.setenv("PTDT_TUNING_TABLE", str(path))
+    monkeypatch.setattr(tuning, "_TABLE", None)
+    assert tuning.pinned("linear", ("nt", 128, 1000, 2048)) == "library"
+    assert tuning.pinned("convbn", (401408, 64, 256, 0)) == "fused"
+    assert tuning.pinned("linear", ("nt", 1, 2, 3)) is None
+    out = tmp_path / "dump.json"
+    tuning.dump(str(out))
+    assert json.loads(out.read_text())["linear"]["nt,128,1000,2048"] == "library"

@@ -231,6 +231,52 @@ def test_ddp_autocast_tied_weight_grads_are_summed():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("defer", ["1", "0"])
+def test_ddp_tied_weight_with_fp32_embedding_use(defer, monkeypatch):
+    """A Linear head whose weight is also read by an fp32 F.embedding (tied embedding / lm_head):
+    one use goes through SinkCast (deferred cast into a slot zero_grad did not clear), the other
+    does not. Both gradients must survive every step (the pending cast overwrote the
+    sum from the second step on, when the slot holds the previous step's gradient)."""
+    import torch.nn.functional as F
+
+    from pytorch_distributed_training_tutorials_amd.ops.linear import Linear
+    from pytorch_distributed_training_tutorials_amd.parallel import env
+    from pytorch_distributed_training_tutorials_amd.parallel.ddp import DistributedDataParallel
+
+    monkeypatch.setenv("PTDT_DEFER_GRAD_CAST", defer)
+
+    class Tied(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.head = Linear(16, 40)  # weight [40, 16] doubles as a 40-token embedding table
+
+        def forward(self, idx):
+            return self.head(F.embedding(idx, self.head.weight))
+
+    env.init_process_group("nccl")
+    try:
+        dev = torch.device("cuda", 0)
+        torch.manual_seed(0)
+        m = Tied().to(dev)
+        ref = Tied().to(dev)
+        ref.load_state_dict(m.state_dict())
+        ddp = DistributedDataParallel(m, device_ids=[0])
+        for step in range(4):
+            idx = torch.randint(0, 40, (8,), device=dev)
+            ddp.zero_grad()
+            ref.zero_grad()
+            with torch.autocast("cuda", torch.bfloat16):
+                (ddp(idx).float() ** 2).sum().backward()
+                (ref(idx).float() ** 2).sum().backward()
+            torch.testing.assert_close(m.head.weight.grad, ref.head.weight.grad, rtol=2e-2, atol=2e-2,
+                                       msg=lambda s, step=step: f"step {step}: {s}")
+            torch.testing.assert_close(m.head.bias.grad, ref.head.bias.grad, rtol=2e-2, atol=2e-2)
+        ddp.remove_grad_sinks()
+    finally:
+        env.destroy_process_group()
+
+
+@pytest.mark.gpu
 def test_fused_sgd_bf16_shadow_replaces_autocast_cast():
     """FusedSGD(bf16_shadow=True) writes bf16(p) in the update kernel; conv under bf16
     autocast then uses it (no per-forward cast) and the training trajectory is the

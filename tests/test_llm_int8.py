@@ -81,6 +81,25 @@ def test_llm_int8_linear_matches_reference(dev, dtype, outliers):
 
 
 @pytest.mark.gpu
+def test_llm_int8_unsupported_k_falls_back(dev):
+    """in_features = 40 (no 16-deep K instance) converts and runs on the reference path (ADVICE r3:
+    quantize_int8_ converts every Linear, so such a layer must not fail in forward)."""
+    from pytorch_distributed_training_tutorials_amd.ops.quant import Int8Linear, llm_int8_reference, quantize_int8_
+
+    model = torch.nn.Sequential(torch.nn.Linear(40, 24), torch.nn.ReLU(), torch.nn.Linear(24, 8)).to(dev)
+    x = torch.randn(5, 40, device=dev)
+    full = model(x)
+    quantize_int8_(model, llm_int8=True)
+    assert isinstance(model[0], Int8Linear) and isinstance(model[2], Int8Linear)
+    y = model(x)
+    assert y.shape == (5, 8) and torch.isfinite(y).all()
+    m = model[0]
+    ref = llm_int8_reference(x, m.weight_q, m.weight_scale, m.bias, m.threshold)
+    torch.testing.assert_close(m(x), ref)
+    assert (y - full).abs().max() <= 0.05 * full.abs().max() + 1e-3
+
+
+@pytest.mark.gpu
 def test_int8_weight_only_fp16(dev):
     """Weight-only int8 on fp16 activations (run in fp32, output fp16) tracks the fp16 Linear."""
     from pytorch_distributed_training_tutorials_amd.ops.quant import Int8Linear
