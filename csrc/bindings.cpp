@@ -869,6 +869,35 @@ Tensor int8_mm_(Tensor A, Tensor sa, Tensor B, Tensor sb, c10::optional<Tensor> 
   return y;
 }
 
+// LLM.int8 decode (M <= 32): y = int8 product with outlier columns, two launches, no host sync
+Tensor int8_decode_(Tensor x, Tensor q, Tensor sw, c10::optional<Tensor> bias, double threshold,
+                    const std::string& out_dtype) {
+  check_gpu(x, "x");
+  check_gpu(q, "weight_q");
+  TORCH_CHECK(x.dim() == 2 && q.dim() == 2 && q.scalar_type() == at::kChar && x.size(1) == q.size(1),
+              "int8_decode: x [M, K], weight_q int8 [N, K]");
+  const int64_t M = x.size(0), N = q.size(0), K = x.size(1);
+  TORCH_CHECK(int8_decode_supported((int)M, (int)N, (int)K), "int8_decode: M <= 32, K % 64 == 0, K <= ",
+              kInt8DecodeMaxK, " (got M=", M, ", K=", K, ")");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(q.data_ptr()) % 16 == 0, "int8_decode: 16-B aligned weight");
+  TORCH_CHECK(sw.scalar_type() == at::kFloat && sw.numel() == N && sw.is_contiguous(), "int8_decode: scale [N]");
+  const void* bp = nullptr;
+  int bias_dt = kF32;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous() && bias->is_cuda(), "int8_decode: bias [N]");
+    bp = bias->data_ptr();
+    bias_dt = dt_of16(*bias);
+  }
+  c10::hip::HIPGuard guard(x.device().index());
+  Tensor ws = at::empty({(int64_t)int8_decode_ws_bytes((int)M, (int)K)}, x.options().dtype(at::kByte));
+  Tensor y = at::empty({M, N}, x.options().dtype(scalar_of(out_dtype)));
+  hip_check(int8_decode(x.data_ptr(), dt_of16(x), (int)M, (int)K, (float)threshold, q.data_ptr<int8_t>(),
+                        sw.data_ptr<float>(), bp, bias_dt, (int)N, y.data_ptr(), dt_of16(y), ws.data_ptr(),
+                        cur_stream(x)),
+            "int8_decode");
+  return y;
+}
+
 Tensor bn_relu(Tensor x, Tensor scale, Tensor shift, bool relu) {
   check_gpu(x, "x");
   TORCH_CHECK(x.dim() >= 2);
@@ -1330,6 +1359,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("tile") = 256, py::arg("split_k") = 1);
   m.def("relu_bwd", &relu_bwd);
   m.def("col_sum_", &col_sum_);
+  m.def("int8_decode", &int8_decode_, "LLM.int8 decode path (M <= 32): outliers + quantise + int8 GEMV, no host sync");
+  m.def("int8_decode_supported", &int8_decode_supported);
   m.def("sum_all", &sum_all_);
   m.def("philox_", &philox_);
   m.def("one_hot", &one_hot_);

@@ -308,6 +308,14 @@ hipError_t int8_quant_rows(const void* x, int dtype, int M, int K, const uint8_t
 hipError_t int8_mm(const int8_t* A, const float* sa, const int8_t* B, const float* sb, const float* addend,
                    const void* bias, int bias_dtype, int M, int N, int K, void* y, int y_dtype, hipStream_t s);
 bool int8_mm_tiled_supported(int M, int N, int K);
+// LLM.int8 decode path (csrc/kernels/int8_decode.hip): M <= 32 rows, K % 64 == 0, K <= kInt8DecodeMaxK.
+// Outlier detection, activation quantisation and the int8 GEMV with the outlier columns fused, in two
+// launches and no host read. ws: int8_decode_ws_bytes(M, K) bytes, 16-B aligned.
+constexpr int kInt8DecodeMaxK = 16384;
+size_t int8_decode_ws_bytes(int M, int K);
+bool int8_decode_supported(int M, int N, int K);
+hipError_t int8_decode(const void* x, int x_dtype, int M, int K, float threshold, const int8_t* W, const float* sw,
+                       const void* bias, int bias_dtype, int N, void* y, int y_dtype, void* ws, hipStream_t s);
 
 // BatchNorm(train stats applied) + ReLU fused epilogue over NCHW (csrc/kernels/elementwise.hip)
 hipError_t bn_relu_apply(const void* x, int dtype, const float* scale, const float* shift, int64_t N,

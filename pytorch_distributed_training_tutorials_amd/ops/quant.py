@@ -16,7 +16,9 @@ columns; every other feature is quantised row-wise (absmax per token) to int8
 and multiplied int8 x int8 -> int32 on MFMA (``v_mfma_i32_16x16x64_i8``,
 csrc/kernels/int8_mm.hip), dequantised in the epilogue where the outlier product
 and the bias are added. (Gathering the outlier columns reads their indices on
-the host, as bitsandbytes does.) fp32, bf16 and fp16 activations run natively
+the host, as bitsandbytes does -- except at decode shapes, <= 32 tokens, where
+csrc/kernels/int8_decode.hip fuses the outlier columns into an int8 GEMV: two
+launches, no host read.) fp32, bf16 and fp16 activations run natively
 (the reference's load_in_8bit Llama is fp16); the plain-PyTorch
 ``llm_int8_reference`` is the CPU path and the numerics reference only.
 """
@@ -28,6 +30,7 @@ import torch.nn as nn
 from .._ext import native, use_native
 
 _NATIVE_DTYPES = (torch.float32, torch.bfloat16, torch.float16)
+_DECODE = __import__("os").environ.get("PTDT_INT8_DECODE", "1") != "0"  # 0: decode shapes take the GEMM path
 _DTYPE_NAME = {torch.float32: "float32", torch.bfloat16: "bfloat16", torch.float16: "float16"}
 
 
@@ -98,6 +101,10 @@ class Int8Linear(nn.Module):
             return llm_int8_reference(x2, self.weight_q, self.weight_scale, b, self.threshold)
         C = native()
         x2 = x2.contiguous()
+        if _DECODE and C.int8_decode_supported(x2.shape[0], self.out_features, self.in_features):
+            # decode shapes (<= 32 tokens): outliers, quantisation and the int8 GEMV with the outlier
+            # columns fused, two launches, no host read (csrc/kernels/int8_decode.hip)
+            return C.int8_decode(x2, self.weight_q, self.weight_scale, b, self.threshold, _DTYPE_NAME[x2.dtype])
         mask = C.int8_col_outliers(x2, self.threshold)
         cols = mask.nonzero().flatten()  # host read: usually a handful of features
         xq, sx = C.int8_quant_rows(x2, mask if cols.numel() else None)

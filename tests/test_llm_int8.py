@@ -128,3 +128,47 @@ def test_tiny_llama_llm_int8_logits_track_bf16(dev):
     with torch.no_grad():
         a, b = ref(ids).logits, q(ids).logits
     assert (a - b).norm() <= 0.05 * a.norm()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [1, 7, 16, 17, 32])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("outliers", [0, 3])
+def test_llm_int8_decode_path_matches_reference(dev, M, dtype, outliers):
+    """Decode shapes (<= 32 tokens): csrc/kernels/int8_decode.hip (outliers + quantisation + int8 GEMV
+    with the outlier columns fused, no host read) against the plain-PyTorch LLM.int8 product; N not a
+    multiple of 16, K = 320 (5 K-steps: uneven split over the 4 waves)."""
+    from pytorch_distributed_training_tutorials_amd import native
+    from pytorch_distributed_training_tutorials_amd.ops.quant import Int8Linear, llm_int8_reference
+
+    lin = _lin(K=320, N=101, seed=M + outliers).to(dev).to(dtype)
+    m = Int8Linear.from_linear(lin, llm_int8=True)
+    x = torch.randn(M, 320, device=dev, dtype=dtype)
+    for j in range(outliers):
+        x[min(j, M - 1), 7 + 100 * j] = 40.0
+    assert native().int8_decode_supported(M, 101, 320)
+    y = m(x)
+    ref = llm_int8_reference(x, m.weight_q, m.weight_scale, m.bias, m.threshold)
+    tol = dict(rtol=1e-5, atol=1e-5) if dtype == torch.float32 else dict(rtol=1e-2, atol=1e-2)
+    assert y.dtype == dtype and y.shape == (M, 101)
+    torch.testing.assert_close(y, ref, **tol)
+    if outliers:  # the outlier columns are decomposed, not quantised: close to the unquantised product
+        full = lin(x).float()
+        assert (y.float() - full).abs().max() <= 0.03 * full.abs().max()
+
+
+@pytest.mark.gpu
+def test_llm_int8_decode_llama_shape(dev):
+    """The reference's Llama-7B MLP up-projection at one decode token batch (M = 16, 4096 -> 11008,
+    fp16, two outlier features)."""
+    from pytorch_distributed_training_tutorials_amd.ops.quant import Int8Linear, llm_int8_reference
+
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(4096, 11008, bias=False, device=dev, dtype=torch.float16)
+    m = Int8Linear.from_linear(lin, llm_int8=True)
+    x = torch.randn(16, 4096, device=dev, dtype=torch.float16)
+    x[:, 1234] *= 20.0
+    x[3, 77] = -30.0
+    y = m(x)
+    ref = llm_int8_reference(x, m.weight_q, m.weight_scale, None, m.threshold)
+    torch.testing.assert_close(y, ref, rtol=1e-2, atol=1e-2)
