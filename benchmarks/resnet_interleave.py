@@ -64,7 +64,7 @@ def main(argv=None):
     y = torch.randint(0, 1000, (a.batch,), device=dev, generator=torch.Generator(device=dev).manual_seed(5))
     seq = a.pattern * a.repeat + "R" * a.tail
     n_exec = a.warmup + len(seq)
-    results = {}
+    results, captures = {}, {}
     for variant in a.variants.split(","):
         model = copy.deepcopy(base)
         ddp = DistributedDataParallel(model, device_ids=[dev.index], comm=comm)
@@ -83,6 +83,8 @@ def main(argv=None):
 
         def rec(fn, variant=variant):
             v = fn()
+            if torch.cuda.is_current_stream_capturing():  # a (re-)capture executes nothing
+                return v
             losses.append(v.detach().clone())
             if a.sync and not torch.cuda.is_current_stream_capturing():
                 torch.cuda.synchronize(dev)
@@ -94,13 +96,19 @@ def main(argv=None):
                 rec(step)
         else:
             gs = GraphedStep(lambda: rec(step), dev, comm=comm, warmup=a.warmup)
-            losses.pop()  # the capture call's loss tensor (nothing executed)
-            for c in seq:  # interleave: the pattern; graph: replays only; eager_after_capture: eager only
-                if variant == "eager_after_capture" or (variant == "interleave" and c == "E"):
+            # interleave: the pattern with GraphedStep.eager (re-captures before the next replay);
+            # interleave_raw: eager steps by calling the step function directly (the round-3 bench's
+            # hazard); graph: replays only; eager_after_capture: eager only
+            for c in seq:
+                if variant == "eager_after_capture" or (variant == "interleave_raw" and c == "E"):
                     rec(step)
+                elif variant == "interleave" and c == "E":
+                    gs.eager()  # runs rec(step) (GraphedStep's fn): recorded there
                 else:
                     rec(gs)
         torch.cuda.synchronize(dev)
+        if variant != "eager":
+            captures[variant] = gs.captures
         results[variant] = ([float(v) for v in losses],
                             {k: v.detach().float().clone() for k, v in model.state_dict().items()})
         del ddp, opt, model
@@ -118,7 +126,7 @@ def main(argv=None):
                           "final_loss": round(ls[-1], 4), "first_loss_divergence_step": first_diff,
                           "max_param_diff_vs_first_variant": dmax, "worst_param": dkey,
                           "env": {k: v for k, v in os.environ.items() if k.startswith("PTDT_")},
-                          "losses": [round(v, 4) for v in ls]}), flush=True)
+                          "captures": captures.get(variant), "losses": [round(v, 4) for v in ls]}), flush=True)
     env.destroy_process_group()
 
 

@@ -57,32 +57,54 @@ class GraphedStep:
             raise ValueError("GraphedStep needs a GPU device")
         self.fn = fn
         self.device = device
-        stream = torch.cuda.Stream(device)
-        stream.wait_stream(torch.cuda.current_stream(device))
-        with torch.cuda.stream(stream):
+        self.comm = comm
+        self._stream = torch.cuda.Stream(device)
+        self._stream.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(self._stream):
             for _ in range(max(1, warmup)):
                 fn()
-        torch.cuda.current_stream(device).wait_stream(stream)
+        torch.cuda.current_stream(device).wait_stream(self._stream)
         torch.cuda.synchronize(device)
-        rc = getattr(comm, "handle", None) if comm is not None else None
+        self.graph = None
+        self.captures = 0
+        self._capture()
+        self.replays = 0
+        self._dirty = False
+
+    def _capture(self):
+        rc = getattr(self.comm, "handle", None) if self.comm is not None else None
         before = rc.captured if rc is not None else 0
+        self.graph = None  # the old graph (and its memory pool) goes first
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=stream, capture_error_mode="thread_local"):
+        with torch.cuda.graph(g, stream=self._stream, capture_error_mode="thread_local"):
             # detached: a captured loss that keeps its autograd graph alive also keeps every
             # parameter's AccumulateGrad node alive -- nodes created on the capture stream, which
             # later EAGER steps on another stream would then reuse: gradient accumulation and the
             # DDP hooks run on the capture stream while their inputs come from the eager one
-            # (cross-stream frees of gradient buffers; the round-3 --graph auto divergence)
-            self.outputs = _detach(fn())
-        torch.cuda.synchronize(device)
+            # (cross-stream frees of gradient buffers)
+            self.outputs = _detach(self.fn())
+        torch.cuda.synchronize(self.device)
         self.graph = WatchedGraph(g, rc, (rc.captured - before) if rc is not None else 0)
-        self.replays = 0
+        self.captures += 1
 
     @property
     def n_collectives(self) -> int:
         return self.graph.n_collectives
 
+    def eager(self):
+        """Run the step eagerly. The next replay re-captures first: on ROCm 7 a memset node of an
+        instantiated graph (MIOpen's atomic weight-gradient solvers zero their outputs with
+        hipMemsetAsync) stops zeroing its whole buffer once eager hipMemsetAsync calls have run after
+        the instantiation (tools/graph_memset_repro.hip, profiles/r4_graph_memset.md) -- replaying the
+        old graph after eager steps summed weight gradients onto stale memory (the round-3 ResNet-50
+        ``--graph auto`` divergence)."""
+        self._dirty = True
+        return self.fn()
+
     def __call__(self):
+        if self._dirty:
+            self._capture()
+            self._dirty = False
         self.graph.replay()
         self.replays += 1
         return self.outputs

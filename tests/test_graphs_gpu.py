@@ -136,18 +136,18 @@ def _interleaved(dev, pattern: str, init_state, lr: float = 0.05, warm: int = 2)
         loss = cross_entropy(out.float(), y)
         loss.backward()
         opt.step()
-        losses.append(loss.detach().clone())
+        if not torch.cuda.is_current_stream_capturing():  # a capture executes nothing
+            losses.append(loss.detach().clone())
         return loss
 
     if "R" in pattern:
         gs = GraphedStep(step, dev, comm=comm, warmup=warm)
-        losses.pop()  # the capture call's loss (nothing executed)
     else:
         gs = None
         pattern = "E" * warm + pattern
     for c in pattern:
         if c == "E":
-            step()
+            step() if gs is None else gs.eager()
         else:
             losses.append(gs().detach().clone())
     torch.cuda.synchronize(dev)
@@ -155,7 +155,8 @@ def _interleaved(dev, pattern: str, init_state, lr: float = 0.05, warm: int = 2)
 
 
 def test_interleaved_eager_and_replay_matches_pure_eager(pg, dev):
-    """E E R R E E R R ... (18 steps after warm-up) follows the pure-eager trajectory."""
+    """E E R R E E R R ... (18 steps after warm-up; eager steps through GraphedStep.eager, which
+    re-captures before the next replay) follows the pure-eager trajectory."""
     from pytorch_distributed_training_tutorials_amd.models.resnet import resnet50
 
     torch.manual_seed(0)
