@@ -1199,6 +1199,105 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor x, c10::optional<Tensor> y, c10::op
   return {dx, dw, db, dres};
 }
 
+// BN backward reduce pass only (for conv1x1_bwd_): returns (g, dweight, dbias, coef[3, C]) where g is the
+// masked incoming gradient (ReLU mask, + dy2) and dx = coef[0] g + coef[1] x + coef[2] per channel.
+std::vector<Tensor> bn_bwd_reduce(Tensor dy, Tensor x, c10::optional<Tensor> weight, Tensor stats, bool relu,
+                                  bool want_dweight, c10::optional<Tensor> tickets, c10::optional<Tensor> dweight_out,
+                                  c10::optional<Tensor> dbias_out, c10::optional<Tensor> dy2,
+                                  c10::optional<Tensor> mask) {
+  int64_t M;
+  int C;
+  bn_rows(x, &M, &C);
+  same_rows(dy, x, "dy");
+  c10::hip::HIPGuard guard(x.device().index());
+  TORCH_CHECK(stats.is_cuda() && stats.scalar_type() == at::kFloat && stats.is_contiguous() && stats.numel() == 4 * C,
+              "batchnorm: stats must be the [4, C] forward statistics");
+  BnBwdArgs a{};
+  a.dy = dy.data_ptr();
+  if (dy2.has_value() && dy2->defined()) {
+    same_rows(*dy2, x, "dy2");
+    a.dy2 = dy2->data_ptr();
+  }
+  a.x = x.data_ptr();
+  if (relu && mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte &&
+                    mask->numel() == M * C / (x.scalar_type() == at::kFloat ? 4 : 8),
+                "batchnorm: mask must be the forward's [M*C/V] byte mask");
+    a.mask = mask->data_ptr<uint8_t>();
+  }
+  Tensor g = at::empty_like(x);
+  Tensor dwb = at::empty({5, C}, x.options().dtype(at::kFloat));
+  Tensor ws = at::empty({bn_workspace_floats(M, C, dt_of(x))}, x.options().dtype(at::kFloat));
+  a.dx = nullptr;
+  a.dres = g.data_ptr();
+  a.reduce_only = 1;
+  a.dtype = dt_of(x);
+  a.M = M;
+  a.C = C;
+  a.relu = relu ? 1 : 0;
+  a.workspace = ws.data_ptr<float>();
+  a.tickets = bn_tickets(x, tickets, bn_num_tickets(C, a.dtype));
+  const float* st = stats.data_ptr<float>();
+  a.p.weight = opt_f32(weight, C, "weight");
+  a.p.mean = st;
+  a.p.invstd = st + C;
+  a.p.scale = st + 2 * C;
+  a.p.shift = st + 3 * C;
+  float* d = dwb.data_ptr<float>();
+  a.p.dweight = want_dweight ? d : nullptr;
+  a.p.dbias = want_dweight ? d + C : nullptr;
+  Tensor dw_out, db_out;
+  if (want_dweight && dweight_out.has_value() && dweight_out->defined()) {
+    a.p.dweight = const_cast<float*>(opt_f32(dweight_out, C, "dweight_out"));
+    dw_out = *dweight_out;
+  }
+  if (want_dweight && dbias_out.has_value() && dbias_out->defined()) {
+    a.p.dbias = const_cast<float*>(opt_f32(dbias_out, C, "dbias_out"));
+    db_out = *dbias_out;
+  }
+  a.p.coef_a = d + 2 * C;
+  a.p.coef_b = d + 3 * C;
+  a.p.coef_c = d + 4 * C;
+  hip_check(bn_backward(a, cur_stream(x)), "bn_backward(reduce)");
+  Tensor dw = want_dweight ? (dw_out.defined() ? dw_out : dwb[0]) : Tensor();
+  Tensor db = want_dweight ? (db_out.defined() ? db_out : dwb[1]) : Tensor();
+  return {g, dw, db, dwb.narrow(0, 2, 3)};
+}
+
+bool conv1x1_bwd_supported_(int64_t K, int64_t N) { return conv1x1_bwd_supported((int)K, (int)N); }
+
+int64_t conv1x1_bwd_num_tickets_(int64_t M, int64_t K, int64_t N) {
+  return conv1x1_bwd_num_tickets((int)M, (int)K, (int)N);
+}
+
+// Backward of BN(conv1x1(x)) from bn_bwd_reduce's (g, coef): returns (dx [M, K], dw [N, K]) in bf16.
+std::vector<Tensor> conv1x1_bwd_(Tensor g, Tensor y, Tensor x, Tensor w, Tensor coef, Tensor tickets) {
+  TORCH_CHECK(g.is_cuda() && y.is_cuda() && x.is_cuda() && w.is_cuda() && coef.is_cuda(), "conv1x1_bwd: GPU operands");
+  TORCH_CHECK(g.dim() == 2 && y.sizes() == g.sizes() && x.dim() == 2 && w.dim() == 2 && x.size(0) == g.size(0) &&
+                  w.size(0) == g.size(1) && w.size(1) == x.size(1),
+              "conv1x1_bwd: g, y [M, N], x [M, K], w [N, K]");
+  for (const Tensor* t : {&g, &y, &x, &w})
+    TORCH_CHECK(t->scalar_type() == at::kBFloat16 && t->is_contiguous(), "conv1x1_bwd: contiguous bf16 operands");
+  const int64_t M = g.size(0), N = g.size(1), K = x.size(1);
+  TORCH_CHECK(conv1x1_bwd_supported((int)K, (int)N), "conv1x1_bwd: no (K, N) = (", K, ", ", N, ") instance");
+  TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() == 3 * N,
+              "conv1x1_bwd: coef [3, N] float");
+  TORCH_CHECK(M < (1LL << 31), "conv1x1_bwd: M < 2^31");
+  TORCH_CHECK(tickets.is_cuda() && tickets.scalar_type() == at::kInt && tickets.is_contiguous() &&
+                  tickets.numel() >= conv1x1_bwd_num_tickets((int)M, (int)K, (int)N),
+              "conv1x1_bwd: tickets must be a zeroed int32 tensor of >= ",
+              conv1x1_bwd_num_tickets((int)M, (int)K, (int)N), " elements");
+  c10::hip::HIPGuard guard(g.device().index());
+  Tensor dx = at::empty({M, K}, x.options());
+  Tensor dw = at::empty({N, K}, w.options());
+  Tensor ws = at::empty({conv1x1_bwd_ws_floats((int)M, (int)K, (int)N)}, g.options().dtype(at::kFloat));
+  hip_check(conv1x1_bwd(g.data_ptr(), y.data_ptr(), x.data_ptr(), w.data_ptr(), coef.data_ptr<float>(), dx.data_ptr(),
+                        dw.data_ptr(), ws.data_ptr<float>(), tickets.data_ptr<int>(), (int)M, (int)K, (int)N,
+                        cur_stream(g)),
+            "conv1x1_bwd");
+  return {dx, dw};
+}
+
 // y = ReLU?(x*scale + shift (+ residual)), per channel (eval-mode BN).
 Tensor bn_apply_(Tensor x, c10::optional<Tensor> residual, Tensor scale, Tensor shift, bool relu) {
   int64_t M;
@@ -1359,6 +1458,10 @@ PYBIND11_MODULE(_C, m) {
         py::arg("tile") = 256, py::arg("split_k") = 1);
   m.def("relu_bwd", &relu_bwd);
   m.def("col_sum_", &col_sum_);
+  m.def("bn_bwd_reduce", &bn_bwd_reduce, "BN backward reduce pass only: (g, dweight, dbias, coef[3, C])");
+  m.def("conv1x1_bwd", &conv1x1_bwd_, "fused BN-apply + 1x1 conv data and weight gradients (bf16)");
+  m.def("conv1x1_bwd_supported", &conv1x1_bwd_supported_);
+  m.def("conv1x1_bwd_num_tickets", &conv1x1_bwd_num_tickets_);
   m.def("int8_decode", &int8_decode_, "LLM.int8 decode path (M <= 32): outliers + quantise + int8 GEMV, no host sync");
   m.def("int8_decode_supported", &int8_decode_supported);
   m.def("sum_all", &sum_all_);

@@ -758,6 +758,13 @@ hipError_t bwd_launch(const BnBwdArgs& a, const Geom& g, hipStream_t s) {
   T* dx = static_cast<T*>(a.dx);
   T* dr = static_cast<T*>(a.dres);
   const dim3 grid(apply_grid(nvec)), blk(kThreads);
+  if (a.reduce_only) {  // g materialised for a consumer that applies the coefficients itself
+    if (!dr) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK, ADD2, true>), dim3(g.gx, g.gy), dim3(kRed), sh_red, s, dy, dy2,
+                       x, y, a.mask, dr, a.M, a.C, g.TC, g.RPI, g.rows_per_block, interleave_rows() | (dir(4) << 1),
+                       a.workspace, a.tickets, a.p);
+    return hipGetLastError();
+  }
   if (dr) {  // the residual gradient is wanted: the reduce pass writes g there, the apply reads g and x
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, MASK, ADD2, true>), dim3(g.gx, g.gy), dim3(kRed), sh_red, s, dy, dy2,
                        x, y, a.mask, dr, a.M, a.C, g.TC, g.RPI, g.rows_per_block, interleave_rows() | (dir(4) << 1), a.workspace,

@@ -377,11 +377,21 @@ struct BnBwdArgs {
   float* workspace; int* tickets;
   BnBwdParams p;
   const uint8_t* mask;  // the forward's mask_out (instead of y; needs dres), or null
+  int reduce_only = 0;  // 1: the reduce pass only, writing the masked gradient g to dres (no dx): the
+                        // consumer applies dx = A g + B x + C itself (conv1x1_bwd, coef_a/b/c)
 };
 int64_t bn_workspace_floats(int64_t M, int C, int dtype);
 int bn_num_tickets(int C, int dtype);
 hipError_t bn_forward_train(const BnFwdArgs& a, hipStream_t s);
 hipError_t bn_backward(const BnBwdArgs& a, hipStream_t s);
+// Backward of BN(conv1x1(x)) for the streaming shapes (csrc/kernels/conv1x1_bwd.hip): dY = A g + B y + C
+// (coef = [A; B; C], 3 x N floats, from a reduce_only bn_backward) feeds dX = dY W and dW = dY^T X
+// without storing dY. g, y: [M, N] bf16; x: [M, K]; w: [N, K]; dx: [M, K]; dw: [N, K] bf16.
+bool conv1x1_bwd_supported(int K, int N);
+int64_t conv1x1_bwd_ws_floats(int M, int K, int N);
+int conv1x1_bwd_num_tickets(int M, int K, int N);
+hipError_t conv1x1_bwd(const void* g, const void* y, const void* x, const void* w, const float* coef, void* dx,
+                       void* dw, float* ws, int* tickets, int M, int K, int N, hipStream_t s);
 // y = ReLU?(x*scale + shift (+ residual)) per channel (eval-mode BN, or any affine epilogue)
 hipError_t bn_apply(const void* x, const void* residual, void* y, int dtype, const float* scale, const float* shift,
                     int64_t M, int C, int relu, hipStream_t s);

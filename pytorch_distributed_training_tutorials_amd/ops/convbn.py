@@ -47,6 +47,9 @@ from .norm import BatchNorm2d, batch_norm_act
 _MODE = os.environ.get("PTDT_CONVBN", "auto")  # auto: per-shape timing decides; on / 1: always; off / 0: never
 _ENABLED = _MODE not in ("0", "off")
 _STREAM = os.environ.get("PTDT_CONVBN_STREAM", "1") != "0"
+# fused backward (BN apply + 1x1 data and weight gradients, csrc/kernels/conv1x1_bwd.hip) where an
+# instance exists; 0: the BN's full backward, then MIOpen's convolution_backward
+_BWD = os.environ.get("PTDT_CONVBN_BWD", "1") != "0"
 _CHOICE: dict[tuple, bool] = {}  # (M, K, N, tile) -> fused is faster (PTDT_CONVBN=auto)
 
 
@@ -58,29 +61,57 @@ def _tile(M: int, N: int, K: int) -> int:
     return 256 if (-(-M // 256)) * (-(-N // 256)) >= 192 else 128
 
 
+class ConvBwdLink:
+    """Hand-over from a fused BN's backward to its producing 1x1 conv's backward (the fused backward,
+    csrc/kernels/conv1x1_bwd.hip): the BN runs only its reduce pass and passes the masked gradient g
+    down as "the gradient of y", leaving here the coefficients of its apply (dY = A g + B y + C); the
+    conv's backward then computes dY on the fly inside its data- and weight-gradient GEMMs. None:
+    the BN ran its full backward (the conv receives dY itself)."""
+
+    __slots__ = ("coef", "tickets")
+
+    def __init__(self, tickets):
+        self.coef = None
+        self.tickets = tickets
+
+
 class _Conv1x1StatsFn(torch.autograd.Function):
     """y = conv1x1(x, w) (NHWC bf16) and the [4, Cout] BN statistics of y (non-differentiable)."""
 
     @staticmethod
     def forward(ctx, x, w, bn_weight, bn_bias, running_mean, running_var, nbt, momentum: float, eps: float,
-                tickets, tile: int):
+                tickets, tile: int, link=None):
         n, cin, h, wd = x.shape
         cout = w.shape[0]
         x2 = x.permute(0, 2, 3, 1).reshape(n * h * wd, cin)  # channels_last storage: a view
         y2, stats = native().conv1x1_bn_stats(x2, w.reshape(cout, cin), bn_weight, bn_bias, running_mean,
                                               running_var, nbt, momentum, eps, tickets, tile)
-        ctx.save_for_backward(x, w)
+        ctx.link = link
+        ctx.save_for_backward(x, w, y2 if link is not None else None)
         ctx.mark_non_differentiable(stats)
         return y2.view(n, h, wd, cout).permute(0, 3, 1, 2), stats
 
     @staticmethod
     def backward(ctx, gy, _gstats):
-        x, w = ctx.saved_tensors
+        x, w, y2 = ctx.saved_tensors
+        link = ctx.link
+        if link is not None and link.coef is not None:  # gy is the BN's masked gradient g (ConvBwdLink)
+            coef, link.coef = link.coef, None
+            n, cin, h, wd = x.shape
+            cout = w.shape[0]
+            g2 = gy.permute(0, 2, 3, 1).reshape(-1, cout)
+            if not g2.is_contiguous():
+                g2 = g2.contiguous()
+            x2 = x.permute(0, 2, 3, 1).reshape(-1, cin)
+            dx2, dw2 = native().conv1x1_bwd(g2, y2, x2, w.reshape(cout, cin), coef, link.tickets)
+            dx = dx2.view(n, h, wd, cin).permute(0, 3, 1, 2) if ctx.needs_input_grad[0] else None
+            dw = dw2.view(cout, cin, 1, 1) if ctx.needs_input_grad[1] else None
+            return dx, dw, *([None] * 10)
         gy = gy.contiguous(memory_format=torch.channels_last)
         mask = [ctx.needs_input_grad[0], ctx.needs_input_grad[1], False]
         dx, dw, _ = torch.ops.aten.convolution_backward(gy, x, w, None, [1, 1], [0, 0], [1, 1], False, [0, 0], 1,
                                                         mask)
-        return dx, dw, *([None] * 9)
+        return dx, dw, *([None] * 10)
 
 
 def _fusable(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual) -> bool:
@@ -181,10 +212,17 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: torch
     need = native().conv1x1_bn_num_tickets(M, conv.out_channels, tile, conv.in_channels)
     if tickets.numel() < need or tickets.device != x.device:
         raise RuntimeError(f"conv_bn_act: BN ticket buffer too small ({tickets.numel()} < {need}) or off-device")
+    cin, cout = conv.in_channels, conv.out_channels
+    clink = None
+    if _BWD and torch.is_grad_enabled() and native().conv1x1_bwd_supported(cin, cout):
+        bt = bn._bwd_tickets
+        if bt.numel() < native().conv1x1_bwd_num_tickets(M, cin, cout) or bt.device != x.device:
+            raise RuntimeError("conv_bn_act: BN backward ticket buffer too small or off-device")
+        clink = ConvBwdLink(bt)
     y, stats = _Conv1x1StatsFn.apply(x, w, bn.weight, bn.bias, bn.running_mean if track else None,
                                      bn.running_var if track else None, bn.num_batches_tracked if track else None,
-                                     float(bn.momentum), float(bn.eps), tickets, tile)
-    return batch_norm_act(y, bn, residual, relu, link, stats=stats)
+                                     float(bn.momentum), float(bn.eps), tickets, tile, clink)
+    return batch_norm_act(y, bn, residual, relu, link, stats=stats, conv_link=clink)
 
 
 def conv1x1_stats_probe(x2: torch.Tensor, w2: torch.Tensor, tile: int | None = None):

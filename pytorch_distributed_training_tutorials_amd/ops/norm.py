@@ -66,7 +66,7 @@ class ResidualLink:
 class _BatchNormActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, relu: bool, momentum: float,
-                eps: float, tickets, link_in, link_out, stats_in=None):
+                eps: float, tickets, link_in, link_out, stats_in=None, conv_link=None):
         # with a residual the ReLU mask travels as bits (one byte per 16-B vector, 1/16 of y in
         # bf16); without one it is recomputed from x and the saved scale/shift (bit-exact)
         want_mask = relu and residual is not None
@@ -81,6 +81,7 @@ class _BatchNormActFn(torch.autograd.Function):
         ctx.relu = relu
         ctx.has_res = residual is not None
         ctx.link_in, ctx.link_out = link_in, link_out
+        ctx.conv_link = conv_link
         ctx.save_for_backward(x, mask if want_mask else None, weight, stats)
         return y
 
@@ -104,8 +105,16 @@ class _BatchNormActFn(torch.autograd.Function):
             for k, p in enumerate(ctx.params):
                 if p is not None and p.grad is None and getattr(p, "_ptdt_grad_sink", None) is not None:
                     sinks[k] = p._ptdt_grad_sink()
-        dx, dw, db, dres = native().bn_bwd(dy, x, None, weight, stats, ctx.relu, want_dres, want_dw,
-                                           ctx.tickets, sinks[0], sinks[1], dy2, mask)
+        clink = ctx.conv_link
+        if clink is not None and ctx.needs_input_grad[0]:
+            # reduce pass only: the producing 1x1 conv applies dY = A g + B x + C inside its fused
+            # backward (ops/convbn.py ConvBwdLink); g doubles as the residual gradient
+            g, dw, db, clink.coef = native().bn_bwd_reduce(dy, x, weight, stats, ctx.relu, want_dw, ctx.tickets,
+                                                           sinks[0], sinks[1], dy2, mask)
+            dx, dres = g, (g.view_as(g) if want_dres else None)
+        else:
+            dx, dw, db, dres = native().bn_bwd(dy, x, None, weight, stats, ctx.relu, want_dres, want_dw,
+                                               ctx.tickets, sinks[0], sinks[1], dy2, mask)
         if link_in is not None and dres is not None:  # delivered to the residual's producer instead of autograd
             if link_in.dres is None:
                 link_in.dres, dres = dres, None
@@ -114,7 +123,7 @@ class _BatchNormActFn(torch.autograd.Function):
                 dres = None
             # else: autograd adds this one (returned below), as _GradLinkFn does
         return (dx if ctx.needs_input_grad[0] else None, dw if want_dw else None, db if want_dw else None,
-                dres if (dres is not None and ctx.needs_input_grad[3]) else None, *([None] * 10))
+                dres if (dres is not None and ctx.needs_input_grad[3]) else None, *([None] * 11))
 
 
 class _GradLinkFn(torch.autograd.Function):
@@ -156,7 +165,8 @@ def _tickets_of(bn, x):
 
 
 def batch_norm_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residual: torch.Tensor | None = None,
-                   relu: bool = False, link: bool = False, stats: torch.Tensor | None = None) -> torch.Tensor:
+                   relu: bool = False, link: bool = False, stats: torch.Tensor | None = None,
+                   conv_link=None) -> torch.Tensor:
     """``ReLU?(bn(x) + residual)`` with ``bn``'s parameters, buffers and train/eval mode.
 
     ``link=True``: when ``residual`` is the output of another fused BN, its gradient
@@ -178,7 +188,7 @@ def batch_norm_act(x: torch.Tensor, bn: nn.modules.batchnorm._BatchNorm, residua
         y = _BatchNormActFn.apply(x, bn.weight, bn.bias, residual, bn.running_mean if track else None,
                                   bn.running_var if track else None, bn.num_batches_tracked if track else None,
                                   relu, float(bn.momentum), float(bn.eps), _tickets_of(bn, x), link_in, link_out,
-                                  stats)
+                                  stats, conv_link)
         if link_out is not None:
             y._ptdt_res_link = link_out
         return y
@@ -220,6 +230,8 @@ class BatchNorm2d(nn.BatchNorm2d):
         # tickets of the statistics merge when a 1x1 conv's epilogue computes this BN's statistics
         # (ops/convbn.py; (merge groups + 1) x column tiles, re-armed in-kernel)
         self.register_buffer("_gemm_tickets", torch.zeros(1024, dtype=torch.int32), persistent=False)
+        # tickets of the fused conv1x1 backward's weight-gradient merge (ops/convbn.py ConvBwdLink)
+        self.register_buffer("_bwd_tickets", torch.zeros(64, dtype=torch.int32), persistent=False)
 
     def forward(self, x, residual=None, relu: bool = False, link: bool = False):
         self._check_input_dim(x)

@@ -1,7 +1,7 @@
 cd $GRAFT_REPO_ROOT
 timeout -k 10 120 ./tools/bin/graph_memset_repro > gpurun_out/memset_repro.txt 2>&1 || exit 1
 timeout -k 10 300 python -u benchmarks/resnet_interleave.py --variants eager,interleave,interleave_raw,graph --tail 10 > gpurun_out/il_nondet3.jsonl 2> gpurun_out/il_nondet3.err || exit 2
-timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_graphs_gpu.py tests/test_llm_int8.py tests/test_grad_sink.py -p no:cacheprovider --no-header --tb=short > gpurun_out/t_g3.log 2>&1 || exit 3
-for i in 1 2 3 4 5; do timeout -k 10 200 python -u benchmarks/resnet_ddp.py --tag fix$i >> gpurun_out/r4_resnet_fix2.jsonl 2>> gpurun_out/r4_resnet_fix2.err || exit 4; done
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_convbn_gpu.py tests/test_graphs_gpu.py tests/test_llm_int8.py tests/test_grad_sink.py tests/test_norm.py -p no:cacheprovider --no-header --tb=short > gpurun_out/t_g3.log 2>&1 || exit 3
+for i in 1 2 3; do timeout -k 10 200 python -u benchmarks/resnet_ddp.py --tag fix$i >> gpurun_out/r4_resnet_fix2.jsonl 2>> gpurun_out/r4_resnet_fix2.err || exit 4; done
 timeout -k 10 200 python -u benchmarks/int8_bench.py --shapes 16x11008x4096,1x11008x4096,32x4096x4096,16x4096x11008 > gpurun_out/int8_decode_bench.jsonl 2> gpurun_out/int8_decode_bench.err || exit 5
 timeout -k 10 300 python -u benchmarks/capture_free_audit.py > gpurun_out/cfa.json 2> gpurun_out/cfa.err || exit 6

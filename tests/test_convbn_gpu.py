@@ -168,3 +168,55 @@ def test_resnet50_step_uses_fused_kernels(dev, monkeypatch):
     g2 = torch.cat([p.grad.flatten().double().cpu() for p in m2.parameters()])
     e1, e2 = float((g1 - g).norm() / g.norm()), float((g2 - g).norm() / g.norm())
     assert e1 <= 1.5 * e2 + 1e-2, f"whole-model gradient error: fused {e1:.3g} vs unfused {e2:.3g}"
+
+
+@pytest.mark.parametrize("M,K,N", [(6272, 64, 256), (6272, 256, 64), (4000, 64, 64), (100003, 64, 256), (131, 256, 64)])
+def test_conv1x1_bwd_matches_reference(native, dev, M, K, N):
+    """csrc/kernels/conv1x1_bwd.hip against fp32 PyTorch: dY = A g + B y + C (rounded to bf16, as the
+    unfused BN apply stores it), dX = dY W, dW = dY^T X; M not a multiple of the 64-row block; two
+    launches bit-identical (fixed-order weight-gradient merge); tickets re-armed."""
+    assert native.conv1x1_bwd_supported(K, N)
+    g = torch.Generator(device=dev).manual_seed(M + K + N)
+    gy = torch.randn(M, N, device=dev, generator=g).to(torch.bfloat16)
+    y = torch.randn(M, N, device=dev, generator=g).to(torch.bfloat16)
+    x = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    w = (torch.randn(N, K, device=dev, generator=g) * K ** -0.5).to(torch.bfloat16)
+    coef = torch.randn(3, N, device=dev, generator=g) * torch.tensor([[1.0], [0.3], [0.1]], device=dev)
+    tickets = torch.zeros(native.conv1x1_bwd_num_tickets(M, K, N), dtype=torch.int32, device=dev)
+    dx, dw = native.conv1x1_bwd(gy, y, x, w, coef.contiguous(), tickets)
+    dy = (coef[0] * gy.float() + coef[1] * y.float() + coef[2]).to(torch.bfloat16).float()
+    dx_ref = dy @ w.float()
+    dw_ref = dy.t().double() @ x.double()
+    assert dx.shape == (M, K) and dw.shape == (N, K) and dx.dtype == dw.dtype == torch.bfloat16
+    torch.testing.assert_close(dx.float(), dx_ref, rtol=2e-2, atol=2e-2)
+    scale = float(dw_ref.abs().max())
+    assert float((dw.double() - dw_ref).abs().max()) <= 1e-2 * scale
+    dx2, dw2 = native.conv1x1_bwd(gy, y, x, w, coef.contiguous(), tickets)
+    assert torch.equal(dx, dx2) and torch.equal(dw, dw2)
+    assert int(tickets.abs().sum()) == 0
+
+
+@pytest.mark.parametrize("inplanes,planes,downsample", [(256, 64, False), (64, 64, True)])
+def test_bottleneck_fused_backward_matches_unfused_backward(dev, monkeypatch, inplanes, planes, downsample):
+    """conv+BN fused forward in both runs; the backward fused (BN reduce pass, then BN-apply + data and
+    weight gradients in one kernel) vs the BN's full backward + MIOpen's convolution_backward."""
+    from pytorch_distributed_training_tutorials_amd.ops import convbn
+
+    a, b = _block_pair(dev, inplanes, planes, downsample)
+    x = torch.randn(8, inplanes, 28, 28, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    monkeypatch.setattr(convbn, "_ENABLED", True)
+    monkeypatch.setattr(convbn, "_MODE", "on")
+    grads = []
+    for blk, bwd in ((a, True), (b, False)):
+        monkeypatch.setattr(convbn, "_BWD", bwd)
+        xi = x.clone().requires_grad_()
+        with torch.autocast("cuda", torch.bfloat16):
+            yv = blk(xi)
+        (yv.float() ** 2).mean().backward()
+        grads.append([xi.grad.float()] + [p.grad.float() for p in blk.parameters()])
+    for ga, gb in zip(*grads):
+        scale = max(float(gb.abs().max()), 1e-6)
+        assert float((ga - gb).abs().max()) / scale < 3e-2
+    for n, t in a.named_buffers():
+        if "tickets" in n:
+            assert int(t.abs().sum()) == 0, n
