@@ -766,6 +766,172 @@ hipError_t launch_piece(const BigGemmArgs& g, int split, hipStream_t s) {
   return hipGetLastError();
 }
 
+// SCHED 3 (256x256, BK = 64, 8 waves 2 (M) x 4 (N), 128 KiB LDS): the 8-phase schedule of
+// cdna_hip_programming.md ("The 256^2 8-phase template"). Each K-tile is staged as four 16-KiB
+// quarters (LDS-DMA, 2 per thread each), and each of its 4 phases computes one 64x32 quadrant of the
+// wave's 128x64 output (16 MFMAs) between two barriers, after reading only that quadrant's new
+// fragments -- the reads of the next quadrant, the DMA of one future quarter and the MFMAs of the
+// current one interleave at phase granularity. The wr = 1 waves run one barrier behind the wr = 0
+// waves (the SIMD's two waves alternate between LDS reads and MFMAs).
+//   quarters (LDS slot: content; phase of its last read): 0: QA0 = A rows 64 s.. of each 128-row band
+//   with s = 0 (phase 0), 1: QB1 = B rows 32..63 of each 64-row band (phase 1), 2: QA1 (phase 2),
+//   3: QB0 (phase 0). Phases: 0 reads QA0 + QB0 -> quadrant (0, 0); 1 reads QB1 -> (0, 1); 2 reads QA1
+//   -> (1, 1); 3 reads nothing -> (1, 0).
+//   staging: global phase P = 4 t + r issues quarter (P + 7) & 3 of K-tile (P + 7) >> 2, i.e. 3
+//   quarters ahead; a quarter is restaged one phase after its last read, which every wave retired
+//   (lgkmcnt(0)) before that phase's first barrier; phase 3 waits (counted vmcnt, before its first
+//   barrier) for the next K-tile, whose first reader starts a barrier later for both wave groups.
+constexpr int QBYTES = 128 * BK * 2;  // 16 KiB quarter
+constexpr int P8OPS = 8 * QBYTES;     // 2 K-tiles x 4 quarters: 128 KiB
+constexpr int P8LDS = P8OPS > 8 * epi_floats<4>() * 4 ? P8OPS : 8 * epi_floats<4>() * 4;  // + epilogue: 136 KiB
+
+__device__ __forceinline__ void vm_wait_n(int n) {
+  if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if (n >= 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n >= 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int OUT>
+__global__ void __launch_bounds__(512) gemm_bf16_p8_kernel(BigGemmArgs g, int tm, int tn, int kt_per) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  constexpr int FI = 8, FJ = 4;
+  const int tile = xcd_remap(blockIdx.x, tm * tn);
+  const int m0 = (tile / tn) * 256, n0 = (tile % tn) * 256;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wid >> 2, wc = wid & 3;
+  const uint16_t* A = static_cast<const uint16_t*>(g.A);
+  const uint16_t* Bt = static_cast<const uint16_t*>(g.Bt);
+  const int nk_all = g.K / BK;
+  const int kt_begin = blockIdx.y * kt_per;
+  const int nk = min(nk_all, kt_begin + kt_per) - kt_begin;
+  const int kbase = kt_begin * BK;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int H = 4 * nk;  // quarters to stage
+
+  f32x4_t acc[FI][FJ];
+#pragma unroll
+  for (int i = 0; i < FI; ++i)
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // quarter h = 4 k + q of K-tile k into slot (k & 1, q): rows of the quarter map to operand rows
+  auto stage_q = [&](int h) {
+    if (h >= H) return;
+    const int k = h >> 2, q = h & 3;
+    const bool isA = (q & 1) == 0;     // slots 0, 2: A quarters (s = q >> 1); 1, 3: B (s = 1 for q = 1)
+    const int sub = isA ? (q >> 1) : (q == 1 ? 1 : 0);
+    uint8_t* dst0 = smem + ((k & 1) * 4 + q) * QBYTES;
+    const uint16_t* src = isA ? A : Bt;
+    const int64_t ld = isA ? g.lda : g.ldb;
+    const int nrows = isA ? g.M : g.N;
+    const int k0 = kbase + k * BK;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int p = i * 512 + wid * 64 + lane;  // 16-B chunk of the quarter image
+      const int r = p >> 3, slot = p & 7;
+      const int c = slot ^ ((r >> 1) & 7);
+      const int grow = isA ? m0 + 128 * (r >> 6) + 64 * sub + (r & 63) : n0 + 64 * (r >> 5) + 32 * sub + (r & 31);
+      const uint16_t* gp = src + (int64_t)min(grow, nrows - 1) * ld + k0 + c * 8;
+      __builtin_amdgcn_global_load_lds((gbl_void*)gp, (lds_void*)(dst0 + (i * 512 + wid * 64) * 16), 16, 0, 0);
+    }
+  };
+  auto bar = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  bf16x8_t af[2][4], b0[2][2], b1[2][2];
+  auto read_a = [&](const uint8_t* qa) {  // this wave's 64 rows of the quarter: band wr
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[kb][i] = read_frag(qa, 64 * wr + 16 * i + fr, kb * 4 + fq);
+  };
+  auto read_b = [&](bf16x8_t (&b)[2][2], const uint8_t* qb) {  // this wave's 32 columns: band wc
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[kb][j] = read_frag(qb, 32 * wc + 16 * j + fr, kb * 4 + fq);
+  };
+  auto mma = [&](int ia, const bf16x8_t (&b)[2][2], int jb) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[ia + i][jb + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kb][i], b[kb][j], acc[ia + i][jb + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // prologue: quarters 0..6 (K-tile 0 whole, K-tile 1's first three), K-tile 0 retired
+  for (int h = 0; h < 7; ++h) stage_q(h);
+  vm_wait_n(2 * (min(H, 7) - min(H, 4)));
+  bar();
+  if (wr == 1) bar();  // the wr = 1 waves run one barrier behind
+  for (int t = 0; t < nk; ++t) {
+    const uint8_t* bufb = smem + (t & 1) * 4 * QBYTES;
+    // phase 0: QA0 + QB0 -> quadrant (0, 0)
+    read_b(b0, bufb + 3 * QBYTES);
+    read_a(bufb);
+    stage_q(4 * t + 7);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    mma(0, b0, 0);
+    bar();
+    // phase 1: QB1 -> (0, 1)
+    read_b(b1, bufb + 1 * QBYTES);
+    stage_q(4 * t + 8);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    mma(0, b1, 2);
+    bar();
+    // phase 2: QA1 -> (1, 1)
+    read_a(bufb + 2 * QBYTES);
+    stage_q(4 * t + 9);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    mma(4, b1, 2);
+    bar();
+    // phase 3: no reads -> (1, 0); K-tile t+1 retired before the first barrier
+    stage_q(4 * t + 10);
+    {
+      const int issued = min(H, 4 * t + 11), need = min(H, 4 * t + 8);
+      vm_wait_n(2 * (issued - need));
+    }
+    bar();
+    mma(4, b0, 0);
+    bar();
+  }
+  if (wr == 0) bar();  // balance the wr = 1 waves' extra barrier
+  if constexpr (OUT == 2) {
+    store_tile<FI, FJ, OUT>(g, acc, m0, n0, wr, wc, fr, fq);
+  } else {
+    __builtin_amdgcn_s_barrier();  // every wave's fragment reads done: the LDS is scratch now
+    store_tile_lds<FI, FJ, OUT>(g, acc, m0, n0, wr, wc, fr, fq,
+                                reinterpret_cast<float*>(smem) + wid * epi_floats<FJ>());
+  }
+}
+
+template <int OUT>
+hipError_t launch_p8(const BigGemmArgs& g, int split, hipStream_t s) {
+  const void* fn = reinterpret_cast<const void*>(&gemm_bf16_p8_kernel<OUT>);
+  static bool attr_set = false;
+  if (!attr_set) {
+    PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, P8LDS));
+    attr_set = true;
+  }
+  const int tm = (g.M + 255) / 256, tn = (g.N + 255) / 256;
+  const int nk = g.K / BK;
+  const int kt_per = (nk + split - 1) / split;
+  split = (nk + kt_per - 1) / kt_per;
+  hipLaunchKernelGGL((gemm_bf16_p8_kernel<OUT>), dim3(tm * tn, split), dim3(512), P8LDS, s, g, tm, tn, kt_per);
+  return hipGetLastError();
+}
+
 // operand double buffer, or the coalesced epilogue's scratch if that is larger
 template <class T>
 constexpr int lds_bytes() {
@@ -872,6 +1038,10 @@ hipError_t gemm_bf16_big(const BigGemmArgs& g, hipStream_t s) {
   if (g.sched == 2) {
     if (split > 1) return launch_piece<2>(g, split, s);
     return g.out_dtype == kF32 ? launch_piece<1>(g, 1, s) : launch_piece<0>(g, 1, s);
+  }
+  if (g.sched == 3) {
+    if (split > 1) return launch_p8<2>(g, split, s);
+    return g.out_dtype == kF32 ? launch_p8<1>(g, 1, s) : launch_p8<0>(g, 1, s);
   }
   return hipErrorInvalidValue;
 }

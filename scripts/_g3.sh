@@ -5,3 +5,5 @@ timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method threa
 for i in 1 2 3; do timeout -k 10 200 python -u benchmarks/resnet_ddp.py --tag fix$i >> gpurun_out/r4_resnet_fix2.jsonl 2>> gpurun_out/r4_resnet_fix2.err || exit 4; done
 timeout -k 10 200 python -u benchmarks/int8_bench.py --shapes 16x11008x4096,1x11008x4096,32x4096x4096,16x4096x11008 > gpurun_out/int8_decode_bench.jsonl 2> gpurun_out/int8_decode_bench.err || exit 5
 timeout -k 10 300 python -u benchmarks/capture_free_audit.py > gpurun_out/cfa.json 2> gpurun_out/cfa.err || exit 6
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k "gemm_big" -p no:cacheprovider --no-header --tb=short > gpurun_out/t_gemm3.log 2>&1 || exit 7
+timeout -k 10 200 python -u benchmarks/gemm_bench.py --shapes 4096x4096x4096,8192x8192x8192,4096x11008x4096 --extra_sched 2 3 --splits 2 > gpurun_out/gemm_p8.jsonl 2> gpurun_out/gemm_p8.err || exit 8
