@@ -16,13 +16,18 @@ from collections import defaultdict
 
 FAMILIES = [
     ("conv1x1+BN stats (native)", r"conv1x1_bn_stream|gemm_bn_stats"),
+    ("conv1x1 dgrad+wgrad with BN apply (native)", r"conv1x1_bwd"),
     ("BN fwd (native)", r"bn_stats_kernel|bn_apply_kernel"),
     ("BN bwd (native)", r"bn_bwd"),
     ("MIOpen conv (CK / ASM igemm)", r"igemm|ck::|_ZN2ck|conv|Conv|gridwise|xdlops|miopenSp3AsmConv|naive_conv"),
     ("MIOpen helpers (fill/SubTensorOp/transpose)", r"SubTensorOp|Op2d|fill|Fill|transpose|Transpose|Set|Copy"),
     ("pool (native)", r"maxpool"),
     ("SGD / casts / reducer (native)", r"sgd|cast|bucket|optim"),
-    ("GEMM (fc)", r"gemm|Cijk"),
+    # Cijk_* are rocBLAS / hipBLASLt (Tensile) GEMMs: in a ResNet step these are mostly MIOpen's
+    # GEMM-based convolutions (1x1 / strided), plus the fc when the Linear selector picked the
+    # library; the native Linear kernels are named gemm_* / linear_*
+    ("rocBLAS/hipBLASLt GEMM (MIOpen GEMM-convs; fc if library)", r"Cijk"),
+    ("GEMM (native Linear / fc)", r"gemm|linear_"),
     ("loss", r"ce_|cross"),
 ]
 
