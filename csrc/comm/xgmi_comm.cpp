@@ -39,6 +39,10 @@ XgmiComm::XgmiComm(int rank, int world, int max_elems, int device) : device_(dev
     if (n > 0) args_.max_polls = (uint32_t)std::min<long>(n, (long)kXgmiMaxPolls);
   }
   args_.drop_push = 0u;
+  args_.flags = kXgmiPair;
+  if (const char* v = std::getenv("PTDT_XGMI_PAIR")) {
+    if (std::strtol(v, nullptr, 10) == 0) args_.flags &= ~kXgmiPair;
+  }
   if (const char* v = std::getenv("PTDT_FAULT_XGMI_DROP_RANK")) {
     if (std::strtol(v, nullptr, 10) == rank) {
       const char* sq = std::getenv("PTDT_FAULT_XGMI_DROP_SEQ");

@@ -16,6 +16,7 @@ constexpr int kThreads = 256;  // wave 0 trains, waves 1-3 build index lists
 size_t lds_bytes(const PersistArgs& p) {  // two epoch index lists + 8 phase-timer slots
   return (size_t)2 * al4(p.num_samples) * sizeof(int) + 8 * sizeof(unsigned long long);
 }
+constexpr size_t kStaticLds = 512;  // layout F's static pair-exchange scratch (linear_wave_impl.h)
 // loss ring of layout F: (2 epochs + prefetch depth) steps x 64 lane shares
 size_t ring_bytes(const FusedMlpArgs& a, const PersistArgs& p) {
   const int S = (p.num_samples + a.B - 1) / a.B;
@@ -66,7 +67,7 @@ Choice choose(const FusedMlpArgs& a, const PersistArgs& p) {
   Choice best;
   if (a.H != 0 || a.B <= 0 || a.B > 64 || a.Dout <= 0) return best;
   if (a.ar.world > kXgmiMaxRanks) return best;
-  if (lds_bytes(p) > 160 * 1024) return best;
+  if (lds_bytes(p) + kStaticLds > 160 * 1024) return best;
   const bool ar = a.ar.world > 1;
   static const int kLR[][2] = {{1, 1}, {2, 1}, {4, 1}, {8, 1}, {2, 2}, {4, 2}, {0, 1}, {0, 2}, {0, 4}};
   double best_cost = 1e30;
@@ -120,7 +121,7 @@ hipError_t linear_wave_prepare(const FusedMlpArgs& a, const PersistArgs& p, Pers
   out->p = p;
   out->p.loss_ring = 0;
   out->lds = lds_bytes(p);
-  if (c.L == 0 && out->lds + ring_bytes(a, p) <= 160 * 1024) {
+  if (c.L == 0 && out->lds + ring_bytes(a, p) + kStaticLds <= 160 * 1024) {
     out->p.loss_ring = 1;
     out->lds += ring_bytes(a, p);
   }

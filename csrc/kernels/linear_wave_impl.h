@@ -382,6 +382,64 @@ __device__ __forceinline__ bool ll_exchange_packed(const PackPlan<NT>& pp, const
   return ok;
 }
 
+// Pair exchange of layout F at world 2 (tools/exchange_bench.hip variant 4): the rank's npw <= 64
+// values (DOUT*Din weights, then the biases) are staged in LDS and travel as npw consecutive LL
+// words in ONE store instruction to the peer, and come back with ONE poll instruction -- against
+// the chunked exchange's per-row-slot stores and polls (W = 2 rehearsal: 1,799 vs 2,369 cycles,
+// profiles/r3_allreduce.md). The two-term sum x0 + x1 is the chunked path's row sum over
+// {x0, x1, 0, ...} (adding zeros is exact), so both ranks -- and both paths -- get the same values
+// (up to the sign of an exact zero). xs: LDS [128] (staging, then the averages).
+template <int KP, int DOUT>
+__device__ __forceinline__ bool ll_exchange_pair(const XgmiArgs& x, uint32_t seq, int q, int i, int lane, int Din,
+                                                 float (&gW)[DOUT][KP], float (&gb)[DOUT], float* xs, float inv_w,
+                                                 bool drop) {
+  const int k0 = q * KP, nW = DOUT * Din, npw = nW + DOUT;
+  if (i == 0) {
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k)
+        if (k0 + k < Din) xs[c * Din + k0 + k] = gW[c][k];
+      if (q == 0) xs[nW + c] = gb[c];
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops complete in order
+  const bool on = lane < npw;
+  const float mine = on ? xs[lane] : 0.f;
+  const int parity = (int)(seq & 1u), peer = 1 - x.rank;
+  const uint64_t hi = (uint64_t)seq << 32;
+  if (!drop && on) {
+    uint64_t PTDT_GLOBAL* base = nullptr;  // uniform selects, no scratch copy of peers[]
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+      if (peer == r) base = (uint64_t PTDT_GLOBAL*)x.peers[r];
+    __hip_atomic_store(base + (int64_t)(parity * 2 + x.rank) * x.max_elems + lane, hi | __float_as_uint(mine),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const uint64_t PTDT_GLOBAL* const src =
+      (const uint64_t PTDT_GLOBAL*)x.local + (int64_t)(parity * 2 + peer) * x.max_elems + (on ? lane : 0);
+  uint64_t w = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  bool ok = true;
+  for (uint32_t polls = 0; __builtin_amdgcn_ballot_w64(on && (uint32_t)(w >> 32) != seq) != 0; ++polls) {
+    if (polls >= x.max_polls) {  // the peer is gone: fail loudly, never hang
+      __hip_atomic_store((int PTDT_GLOBAL*)x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      ok = false;
+      break;
+    }
+    w = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  const float other = __uint_as_float((uint32_t)w);
+  xs[64 + lane] = (x.rank == 0 ? mine + other : other + mine) * inv_w;  // rank order
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k) gW[c][k] = k0 + k < Din ? xs[64 + c * Din + k0 + k] : 0.f;
+    gb[c] = xs[64 + nW + c];
+  }
+  return ok;
+}
+
 template <int R, int KP, int DOUT, int RY>
 struct Batch {
   float x[R][KP];
@@ -993,6 +1051,9 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   uint32_t seq = AR ? *ar.seq : 0u;
   bool failed = AR && *ar.err != 0;
   const float inv_w = 1.f / (float)world;
+  // world 2: one packed store + one poll per step (ll_exchange_pair), staged through 128 LDS floats
+  __shared__ float xpair[AR ? 128 : 1];
+  const bool pair = AR && world == 2 && (ar.flags & kXgmiPair) != 0u && DOUT * (Din + 1) <= 64;
 
   int ie = e0, ij = j0, barriers = 0;
   int sel_next[R], sel_y_next = 0, nb_next = 0;
@@ -1206,7 +1267,12 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     }
     tk.tick(3);
     // ---- all-reduce over ranks: row slot r <-> rank r, summed with the same DPP tree
-    if (AR && !failed) {
+    if (AR && !failed && pair) {
+      seq += 1u;
+      failed = !ll_exchange_pair<KP, DOUT>(ar, seq, q, i, lane, Din, gW, gb, xpair, inv_w,
+                                           ar.drop_push != 0u && seq >= ar.drop_push);
+      failed = __any(failed);
+    } else if (AR && !failed) {
       seq += 1u;
       float v[DOUT][KP], vb[DOUT];
 #pragma unroll
@@ -1216,7 +1282,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
         for (int k = 0; k < KP; ++k) v[c][k] = i == my_rank ? gW[c][k] : 0.f;
       }
       // (ll_exchange_u / ll_exchange_packed / a separate pusher or poller wave measured no faster at
-      //  W = 8: tools/exchange_bench.hip, profiles/r3_exchange_bench*.jsonl)
+      //  W = 8: tools/exchange_bench.hip, profiles/r3_exchange_bench*.jsonl; W = 2 takes the pair path)
       const bool ok = ll_exchange<KP, DOUT>(i < world && i != my_rank, push_dst, poll_src, my_rank, i, world,
                                             max_elems, seq, k0, Din, hb, q == 0, 4 * KP != Din, gW, gb, v, vb,
                                             ar.err, ar.max_polls, ar.drop_push != 0u && seq >= ar.drop_push);

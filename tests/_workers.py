@@ -234,6 +234,8 @@ def _per_step_reference(eng, X, Y, sampler, n_steps, B, dev):
 
 
 def persistent_two_procs_one_gpu(rank, world, port, out_dir, kind="mlp"):
+    if kind == "linear_nopair":  # the chunked exchange instead of the world-2 pair exchange
+        os.environ["PTDT_XGMI_PAIR"] = "0"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
@@ -258,7 +260,7 @@ def persistent_two_procs_one_gpu(rank, world, port, out_dir, kind="mlp"):
         # instantiated, so use Linear(20, 2))
         model = ToyMLP(20, 16, 4) if kind == "mlp" else torch.nn.Linear(20, 2)
         eng = FusedMLPStep(model.to(dev), loss="ce_index", lr=0.05, momentum=0.9, xgmi=xg)
-        variant = "wave_rows" if kind == "linear_rows" else None
+        variant = "wave_rows" if kind == "linear_rows" else None  # linear / linear_nopair: layout F
         if mode == "persistent":
             out["engine"] = eng.persistent_engine(16, DeviceDistributedSampler(300, world, rank, seed=3, device=dev),
                                                   variant)

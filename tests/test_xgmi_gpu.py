@@ -186,7 +186,7 @@ def test_persistent_plan_launch_at_equals_device_cursor(dev, kind):
     assert torch.equal(res[0], res[1])
 
 
-@pytest.mark.parametrize("kind", ["mlp", "linear", "linear_rows"])
+@pytest.mark.parametrize("kind", ["mlp", "linear", "linear_nopair", "linear_rows"])
 def test_persistent_engine_two_ranks_one_gpu(tmp_path, kind):
     world = 2
     spawn(_workers.persistent_two_procs_one_gpu, args=(world, free_port(), str(tmp_path), kind), nprocs=world)
@@ -296,3 +296,16 @@ def test_mfma_mlp_engine_matches_workgroup_engine(dev, B, Din, H, Dout, loss):
         out[variant] = (eng.P.clone(), losses[:40].clone())
     torch.testing.assert_close(out["mfma"][1], out["workgroup"][1], rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(out["mfma"][0], out["workgroup"][0], rtol=1e-4, atol=1e-5)
+
+
+def test_wave_engine_pair_exchange_equals_chunked(tmp_path):
+    """World 2: the single-wave engine's packed pair exchange (one store + one poll per step) and the
+    chunked per-row-slot exchange (PTDT_XGMI_PAIR=0) train to the same parameters (x0 + x1 either way)."""
+    world = 2
+    got = {}
+    for kind in ("linear", "linear_nopair"):
+        d = tmp_path / kind
+        d.mkdir()
+        spawn(_workers.persistent_two_procs_one_gpu, args=(world, free_port(), str(d), kind), nprocs=world)
+        got[kind] = torch.load(os.path.join(d, "r0.pt"), weights_only=True)["persistent"]
+    assert torch.equal(got["linear"], got["linear_nopair"])
