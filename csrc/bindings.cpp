@@ -693,7 +693,7 @@ void gemm_big_(Tensor A, Tensor Bt, Tensor C, c10::optional<Tensor> bias, bool r
   g.alpha = (float)alpha;
   g.beta = (float)beta;
   g.tile = tile == 128 ? 128 : 256;
-  g.sched = sched < 0 ? (g.tile == 256 ? 1 : 0) : (int)sched;
+  g.sched = sched < 0 ? (g.tile == 256 ? 3 : 0) : (int)sched;  // 256 tile: the 8-phase schedule
   g.split_k = split_k > 1 ? (int)split_k : 1;
   TORCH_CHECK(g.split_k == 1 || (C.scalar_type() == at::kFloat && !relu && beta == 0.0),
               "gemm_big: split-K accumulates fp32 atomics: C must be f32 (pre-zeroed), no relu/beta");
@@ -889,6 +889,8 @@ Tensor int8_decode_(Tensor x, Tensor q, Tensor sw, c10::optional<Tensor> bias, d
     bias_dt = dt_of16(*bias);
   }
   c10::hip::HIPGuard guard(x.device().index());
+  if (!x.is_contiguous() || reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 != 0)
+    x = x.contiguous().clone();  // the prep kernel reads 16-B chunks
   Tensor ws = at::empty({(int64_t)int8_decode_ws_bytes((int)M, (int)K)}, x.options().dtype(at::kByte));
   Tensor y = at::empty({M, N}, x.options().dtype(scalar_of(out_dtype)));
   hip_check(int8_decode(x.data_ptr(), dt_of16(x), (int)M, (int)K, (float)threshold, q.data_ptr<int8_t>(),
