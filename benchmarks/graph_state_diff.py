@@ -28,6 +28,9 @@ def main(argv=None):
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--top", type=int, default=12)
     ap.add_argument("--nondet", action="store_true", help="cudnn.benchmark instead of deterministic MIOpen")
+    ap.add_argument("--replays", type=int, default=0,
+                    help="replay-first mode: right after the capture, K replays from a snapshot, then (restored) "
+                         "K eager steps; per-step losses and the state diff after K (no eager step precedes a replay)")
     a = ap.parse_args(argv)
     torch.backends.cudnn.benchmark = a.nondet
     torch.backends.cudnn.deterministic = not a.nondet
@@ -62,8 +65,9 @@ def main(argv=None):
         return loss
 
     gs = GraphedStep(step, dev, comm=comm, warmup=a.warmup)
-    for _ in range(a.eager):
-        step()
+    if a.replays == 0:
+        for _ in range(a.eager):
+            step()
     torch.cuda.synchronize(dev)
 
     def state():
@@ -93,6 +97,27 @@ def main(argv=None):
                 v.copy_(snap[k])
         torch.cuda.synchronize(dev)
 
+    if a.replays > 0:
+        lr_list = [float(gs()) for _ in range(a.replays)]
+        torch.cuda.synchronize(dev)
+        after_r = {k: v.detach().clone() for k, v in live.items()}
+        restore()
+        le_list = [float(step()) for _ in range(a.replays)]
+        torch.cuda.synchronize(dev)
+        after_e = {k: v.detach().clone() for k, v in live.items()}
+        out = []
+        for k in after_e:
+            d = (after_e[k].double() - after_r[k].double()).abs()
+            m = float(d.max()) if d.numel() else 0.0
+            out.append((m if m == m else float("inf"), k))
+        out.sort(reverse=True)
+        nan_r = [k for k, v in after_r.items() if v.is_floating_point() and not bool(torch.isfinite(v).all())]
+        print(json.dumps({"mode": "replay_first", "replays": a.replays, "losses_replay": lr_list,
+                          "losses_eager": le_list, "replay_vs_eager_top": out[:a.top],
+                          "n_tensors_differing": sum(1 for m, _ in out if m > 0), "nonfinite_after_replay": nan_r[:40]}),
+              flush=True)
+        env.destroy_process_group()
+        return
     le = float(step())
     torch.cuda.synchronize(dev)
     after_e = {k: v.detach().clone() for k, v in live.items()}

@@ -46,6 +46,10 @@ def main(argv=None):
     ap.add_argument("--no_shadow", action="store_true",
                     help="cast the fp32 weights in every forward instead of using FusedSGD's bf16 shadows")
     ap.add_argument("--tag", default=None, help="free-form label copied into the JSON line")
+    ap.add_argument("--deterministic", action="store_true",
+                    help="diagnostic: deterministic MIOpen solvers (cudnn.deterministic, no exhaustive find)")
+    ap.add_argument("--loss_curve", action="store_true",
+                    help="diagnostic: record every executed step's loss (one clone per step) into the JSON line")
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="native impl: replay one captured hipGraph per step (on), launch eagerly (off), or time "
                          "both in this process after warm-up and keep the faster (auto: the eager loop's cost "
@@ -58,7 +62,8 @@ def main(argv=None):
     ap.add_argument("--no_cudnn_benchmark", action="store_true",
                     help="keep MIOpen's heuristic solver choice (default: exhaustive find per conv shape)")
     a = ap.parse_args(argv)
-    torch.backends.cudnn.benchmark = not a.no_cudnn_benchmark
+    torch.backends.cudnn.benchmark = not a.no_cudnn_benchmark and not a.deterministic
+    torch.backends.cudnn.deterministic = a.deterministic
 
     from pytorch_distributed_training_tutorials_amd import native
     from pytorch_distributed_training_tutorials_amd.models.resnet import resnet50
@@ -93,6 +98,7 @@ def main(argv=None):
     amp = a.dtype == "bf16"
     mode = "off" if (a.no_graph or a.impl != "native") else a.graph
     graphed = mode != "off"
+    from pytorch_distributed_training_tutorials_amd.utils.graphs import GraphedStep
 
     def step():
         if a.impl == "native":
@@ -105,13 +111,24 @@ def main(argv=None):
         loss = cross_entropy(out.float(), y)
         loss.backward()
         opt.step()
+        if a.loss_curve and not torch.cuda.is_current_stream_capturing():
+            curve.append(loss.detach().clone())
         return loss
 
+    curve = []
+
+    def replayed(fn):  # loss of a graph replay (the captured step's Python body does not run)
+        def run():
+            loss = fn()
+            if a.loss_curve and isinstance(fn, GraphedStep):
+                curve.append(loss.detach().clone())
+            return loss
+        return run
+
     ab = None
+    graph_info = None
     executed = 0  # training steps run before the timed loop's warm-up (the comparator runs as many)
     if graphed:  # utils/graphs.py: eager warm-up steps on a side stream, then one hipGraph per step
-        from pytorch_distributed_training_tutorials_amd.utils.graphs import GraphedStep
-
         eager = step
         if mode == "auto":
             # eager rounds FIRST, then capture and replay rounds: never a replay after eager steps
@@ -129,13 +146,15 @@ def main(argv=None):
                     torch.cuda.synchronize(dev)
                     t0 = time.perf_counter()
                     for _ in range(4):
-                        fn()
+                        replayed(fn)()
                     torch.cuda.synchronize(dev)
                     ab[name].append((time.perf_counter() - t0) / 4 * 1e3)
                     executed += 4
 
             rounds("eager", eager)
         gstep = GraphedStep(eager, dev, comm=comm, warmup=max(3, a.warmup))
+        graph_info = {"nodes": gstep.node_count, "memset_nodes": gstep.memset_nodes,
+                      "memsets_replaced": gstep.memsets_replaced}
         executed += max(3, a.warmup)
         step = gstep
         if mode == "auto":
@@ -149,6 +168,7 @@ def main(argv=None):
             graphed = win == "graph"
             step = gstep if graphed else gstep.eager
             ab = {k: round(v, 3) for k, v in med.items()}
+    step = replayed(step)
     for _ in range(a.pre_steps if a.pre_steps is not None else (2 * max(3, a.warmup) + 24 if a.impl == "torch" else 0)):
         # comparator: as many steps before the timed region as the native default mode runs
         # (eager warm-up + 3 x 4 eager steps, GraphedStep warm-up + 3 x 4 replays: 2 max(3, warmup) + 24)
@@ -189,6 +209,8 @@ def main(argv=None):
                        "parallelism": f"dp{world}", "channels_last": not a.no_channels_last},
             "impl": a.impl, "hipgraph": graphed, "graph_mode": mode, **({"ab_ms_per_step": ab} if ab else {}), "bn_dir": os.environ.get("PTDT_BN_DIR", "0"), "miopen_find": "exhaustive (cudnn.benchmark)" if torch.backends.cudnn.benchmark else "heuristic",
             "buckets_MB": [round(b / 2 ** 20, 2) for b in ddp.bucket_sizes_bytes()] if a.impl == "native" else None,
+            **({"loss_curve": [round(float(v), 4) for v in curve]} if a.loss_curve else {}),
+            **({"graph": graph_info} if graph_info else {}),
             "final_loss": final, "finite": True, "kernel_choices": _choices(), "steps_total": executed + a.steps, **({"tag": a.tag} if a.tag else {}),
         }), flush=True)
     env.destroy_process_group()

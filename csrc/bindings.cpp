@@ -869,6 +869,21 @@ Tensor int8_mm_(Tensor A, Tensor sa, Tensor B, Tensor sb, c10::optional<Tensor> 
   return y;
 }
 
+std::vector<int64_t> graph_node_census_(int64_t graph) {
+  std::vector<int> c(16, 0);
+  const int n = graph_node_census(reinterpret_cast<void*>(graph), c.data(), (int)c.size());
+  TORCH_CHECK(n >= 0, "graph_node_census: hipGraph query failed");
+  std::vector<int64_t> out(c.begin(), c.end());
+  out.insert(out.begin(), n);
+  return out;  // [total, count of hipGraphNodeType 0, 1, ...]
+}
+
+int64_t graph_replace_memsets_(int64_t graph) {
+  const int r = graph_replace_memsets(reinterpret_cast<void*>(graph));
+  TORCH_CHECK(r >= 0, "graph_replace_memsets: hipGraph edit failed");
+  return r;
+}
+
 // LLM.int8 decode (M <= 32): y = int8 product with outlier columns, two launches, no host sync
 Tensor int8_decode_(Tensor x, Tensor q, Tensor sw, c10::optional<Tensor> bias, double threshold,
                     const std::string& out_dtype) {
@@ -1268,12 +1283,8 @@ std::vector<Tensor> bn_bwd_reduce(Tensor dy, Tensor x, c10::optional<Tensor> wei
 
 bool conv1x1_bwd_supported_(int64_t K, int64_t N) { return conv1x1_bwd_supported((int)K, (int)N); }
 
-int64_t conv1x1_bwd_num_tickets_(int64_t M, int64_t K, int64_t N) {
-  return conv1x1_bwd_num_tickets((int)M, (int)K, (int)N);
-}
-
 // Backward of BN(conv1x1(x)) from bn_bwd_reduce's (g, coef): returns (dx [M, K], dw [N, K]) in bf16.
-std::vector<Tensor> conv1x1_bwd_(Tensor g, Tensor y, Tensor x, Tensor w, Tensor coef, Tensor tickets) {
+std::vector<Tensor> conv1x1_bwd_(Tensor g, Tensor y, Tensor x, Tensor w, Tensor coef) {
   TORCH_CHECK(g.is_cuda() && y.is_cuda() && x.is_cuda() && w.is_cuda() && coef.is_cuda(), "conv1x1_bwd: GPU operands");
   TORCH_CHECK(g.dim() == 2 && y.sizes() == g.sizes() && x.dim() == 2 && w.dim() == 2 && x.size(0) == g.size(0) &&
                   w.size(0) == g.size(1) && w.size(1) == x.size(1),
@@ -1285,16 +1296,12 @@ std::vector<Tensor> conv1x1_bwd_(Tensor g, Tensor y, Tensor x, Tensor w, Tensor 
   TORCH_CHECK(coef.scalar_type() == at::kFloat && coef.is_contiguous() && coef.numel() == 3 * N,
               "conv1x1_bwd: coef [3, N] float");
   TORCH_CHECK(M < (1LL << 31), "conv1x1_bwd: M < 2^31");
-  TORCH_CHECK(tickets.is_cuda() && tickets.scalar_type() == at::kInt && tickets.is_contiguous() &&
-                  tickets.numel() >= conv1x1_bwd_num_tickets((int)M, (int)K, (int)N),
-              "conv1x1_bwd: tickets must be a zeroed int32 tensor of >= ",
-              conv1x1_bwd_num_tickets((int)M, (int)K, (int)N), " elements");
   c10::hip::HIPGuard guard(g.device().index());
   Tensor dx = at::empty({M, K}, x.options());
   Tensor dw = at::empty({N, K}, w.options());
   Tensor ws = at::empty({conv1x1_bwd_ws_floats((int)M, (int)K, (int)N)}, g.options().dtype(at::kFloat));
   hip_check(conv1x1_bwd(g.data_ptr(), y.data_ptr(), x.data_ptr(), w.data_ptr(), coef.data_ptr<float>(), dx.data_ptr(),
-                        dw.data_ptr(), ws.data_ptr<float>(), tickets.data_ptr<int>(), (int)M, (int)K, (int)N,
+                        dw.data_ptr(), ws.data_ptr<float>(), (int)M, (int)K, (int)N,
                         cur_stream(g)),
             "conv1x1_bwd");
   return {dx, dw};
@@ -1463,7 +1470,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_reduce", &bn_bwd_reduce, "BN backward reduce pass only: (g, dweight, dbias, coef[3, C])");
   m.def("conv1x1_bwd", &conv1x1_bwd_, "fused BN-apply + 1x1 conv data and weight gradients (bf16)");
   m.def("conv1x1_bwd_supported", &conv1x1_bwd_supported_);
-  m.def("conv1x1_bwd_num_tickets", &conv1x1_bwd_num_tickets_);
+  m.def("graph_node_census", &graph_node_census_, "node count and per-hipGraphNodeType counts of a raw hipGraph_t");
+  m.def("graph_replace_memsets", &graph_replace_memsets_, "replace a raw hipGraph_t's memset nodes by fill-kernel nodes");
   m.def("int8_decode", &int8_decode_, "LLM.int8 decode path (M <= 32): outliers + quantise + int8 GEMV, no host sync");
   m.def("int8_decode_supported", &int8_decode_supported);
   m.def("sum_all", &sum_all_);

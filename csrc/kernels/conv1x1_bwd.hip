@@ -19,8 +19,10 @@
 //   * weight gradient: both operands are column slices of those row-major images, read with
 //     ds_read_b64_tr_b16 (gfx950's transposing LDS read); fp32 accumulators per wave for the whole
 //     launch (N*K/256 values per lane);
-//   * partials [workgroup][N][K] merged by the last workgroup of each group / the last group (sc1
-//     stores and loads + ticket, as conv1x1_bn.hip): deterministic.
+//   * partials [workgroup][N][K] (plain stores) summed by a second kernel in a fixed order:
+//     deterministic. (The first version merged in-kernel -- last arrival of each group, sc1 loads one
+//     partial at a time: ~800 us per call at layer1's 512 partials of 64 KB; ResNet-50 step 20.2 vs
+//     16.3 ms unfused, profiles/r4_resnet_step.md.)
 #include "common.h"
 #include "kernels.h"
 
@@ -32,33 +34,13 @@ typedef __attribute__((ext_vector_type(4))) float f32x4_t;
 typedef __attribute__((ext_vector_type(2))) float f32x2_t;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;  // native vector: register arrays of it stay in VGPRs
 typedef __attribute__((address_space(3))) s16x4_t lds_s16x4;
 typedef __attribute__((address_space(1))) float gfloat;
 
 constexpr int kBwdWaves = 4;
 constexpr int kBwdThreads = 64 * kBwdWaves;
 constexpr int kBwdBM = 64;  // rows per block (16 per wave for the data gradient)
-
-__device__ __forceinline__ void st_sc1(float* p, float v) {
-  __hip_atomic_store((gfloat*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __hip_atomic_load((gfloat*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ bool last_arrival(int* ticket, int count, int* sh_flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's sc1 partial stores have landed
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int prev = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = prev == count - 1;
-    if (last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *sh_flag = last;
-  }
-  __syncthreads();
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // partial loads stay below the ticket (batchnorm.hip last_block)
-  return *sh_flag != 0;
-}
 
 // input channel of row i of data-gradient A tile j (a pair of tiles covers 32 channels; lane group q
 // of the pair holds channels 32p + 8q .. +7)
@@ -73,7 +55,7 @@ struct Cb {
   static constexpr int DY_B = kBwdBM * SDY;
   static constexpr int X_B = kBwdBM * SX;
   static constexpr int CO_B = 3 * N * 4;  // A, B, C coefficients
-  static constexpr int LDS = WT_B + DY_B + X_B + CO_B + 16;
+  static constexpr int LDS = WT_B + DY_B + X_B + CO_B;
   static constexpr int PER_CU = 2 * LDS <= 160 * 1024 ? 2 : 1;
   static constexpr int NS = N / 32;        // k-steps of the data gradient (over N)
   static constexpr int KP = K / 32;        // output channel pairs of the data gradient
@@ -89,14 +71,13 @@ template <int K, int N>
 __global__ void __launch_bounds__(kBwdThreads, 2) conv1x1_bwd_kernel(
     const uint16_t* __restrict__ G, const uint16_t* __restrict__ Y, const uint16_t* __restrict__ X,
     const uint16_t* __restrict__ W, const float* __restrict__ coef, uint16_t* __restrict__ dX,
-    uint16_t* __restrict__ dW, float* __restrict__ ws, int* __restrict__ tickets, int M, int nblk, int group) {
+    float* __restrict__ ws, int M, int nblk) {
   using S = Cb<K, N>;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* const wt = smem;
   uint8_t* const dyi = wt + S::WT_B;
   uint8_t* const xi = dyi + S::DY_B;
   float* const co = reinterpret_cast<float*>(xi + S::X_B);
-  int* const flag = reinterpret_cast<int*>(co + 3 * N);
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
@@ -105,14 +86,13 @@ __global__ void __launch_bounds__(kBwdThreads, 2) conv1x1_bwd_kernel(
   // ---- prologue: W^T (permuted rows) and the coefficients into LDS
   for (int e = tid; e < N * (K / 8); e += kBwdThreads) {
     const int n = e / (K / 8), kc = e % (K / 8);
-    const uint4 v = *reinterpret_cast<const uint4*>(W + (int64_t)n * K + kc * 8);
-    const uint16_t* h = reinterpret_cast<const uint16_t*>(&v);
+    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(W + (int64_t)n * K + kc * 8);
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int k = kc * 8 + u;
       // LDS row r of tile j holds channel k_of(j, i): r = 16 j + i with k_of(j, i) = k
       const int j = 2 * (k >> 5) + ((k >> 2) & 1), i = 4 * ((k >> 3) & 3) + (k & 3);
-      *reinterpret_cast<uint16_t*>(wt + (16 * j + i) * S::SWT + n * 2) = h[u];
+      *reinterpret_cast<uint16_t*>(wt + (16 * j + i) * S::SWT + n * 2) = (uint16_t)(v[u >> 1] >> (16 * (u & 1)));
     }
   }
   for (int e = tid; e < 3 * N; e += kBwdThreads) co[e] = coef[e];
@@ -130,31 +110,29 @@ __global__ void __launch_bounds__(kBwdThreads, 2) conv1x1_bwd_kernel(
     const int mr = m0 + 16 * w + fr;
     const bool valid = mr < M;
     const int64_t mc = valid ? mr : M - 1;
-    uint4 gv[S::NS], yv[S::NS], xv[S::XPL];
+    u32x4_t gv[S::NS], yv[S::NS], xv[S::XPL];
 #pragma unroll
     for (int s = 0; s < S::NS; ++s) {
-      gv[s] = *reinterpret_cast<const uint4*>(G + mc * N + 32 * s + 8 * fq);
-      yv[s] = *reinterpret_cast<const uint4*>(Y + mc * N + 32 * s + 8 * fq);
+      gv[s] = *reinterpret_cast<const u32x4_t*>(G + mc * N + 32 * s + 8 * fq);
+      yv[s] = *reinterpret_cast<const u32x4_t*>(Y + mc * N + 32 * s + 8 * fq);
     }
 #pragma unroll
     for (int u = 0; u < S::XPL; ++u) {
       const int e = lane + 64 * u, r = e / S::XCH, c = e % S::XCH;
       const int xr = m0 + 16 * w + r;
-      xv[u] = *reinterpret_cast<const uint4*>(X + (int64_t)(xr < M ? xr : M - 1) * K + c * 8);
+      xv[u] = *reinterpret_cast<const u32x4_t*>(X + (int64_t)(xr < M ? xr : M - 1) * K + c * 8);
     }
     __syncthreads();  // the previous block's weight-gradient reads of the images are done
 #pragma unroll
     for (int u = 0; u < S::XPL; ++u) {
       const int e = lane + 64 * u, r = e / S::XCH, c = e % S::XCH;
-      *reinterpret_cast<uint4*>(xi + (16 * w + r) * S::SX + c * 16) = xv[u];
+      *reinterpret_cast<u32x4_t*>(xi + (16 * w + r) * S::SX + c * 16) = xv[u];
     }
     // ---- dY (bf16) for the data gradient's B operand and the image
     bf16x8_t dyb[S::NS];
 #pragma unroll
     for (int s = 0; s < S::NS; ++s) {
       const int n0 = 32 * s + 8 * fq;
-      const uint16_t* gh = reinterpret_cast<const uint16_t*>(&gv[s]);
-      const uint16_t* yh = reinterpret_cast<const uint16_t*>(&yv[s]);
       const f32x4_t* ca = reinterpret_cast<const f32x4_t*>(co + n0);
       const f32x4_t* cb = reinterpret_cast<const f32x4_t*>(co + N + n0);
       const f32x4_t* cc = reinterpret_cast<const f32x4_t*>(co + 2 * N + n0);
@@ -164,19 +142,20 @@ __global__ void __launch_bounds__(kBwdThreads, 2) conv1x1_bwd_kernel(
         const f32x4_t A4 = ca[h], B4 = cb[h], C4 = cc[h];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const float gg = bf16_to_f32(gh[4 * h + u]), yy = bf16_to_f32(yh[4 * h + u]);
+          const int e = 4 * h + u;
+          const float gg = bf16_to_f32((uint16_t)(gv[s][e >> 1] >> (16 * (e & 1))));
+          const float yy = bf16_to_f32((uint16_t)(yv[s][e >> 1] >> (16 * (e & 1))));
           d[4 * h + u] = valid ? fmaf(A4[u], gg, fmaf(B4[u], yy, C4[u])) : 0.f;
         }
       }
-      uint4 pk;
-      uint32_t* pw = reinterpret_cast<uint32_t*>(&pk);
+      u32x4_t pk;
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
         const f32x2_t f = {d[2 * h], d[2 * h + 1]};
-        pw[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2_t));
+        pk[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2_t));
       }
       dyb[s] = __builtin_bit_cast(bf16x8_t, pk);
-      *reinterpret_cast<uint4*>(dyi + (16 * w + fr) * S::SDY + n0 * 2) = pk;
+      *reinterpret_cast<u32x4_t*>(dyi + (16 * w + fr) * S::SDY + n0 * 2) = pk;
     }
     // ---- data gradient: dX[m][k] = sum_n W^T[k][n] dY[m][n], two tiles (32 channels) at a time
 #pragma unroll
@@ -191,15 +170,14 @@ __global__ void __launch_bounds__(kBwdThreads, 2) conv1x1_bwd_kernel(
           acc[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, dyb[s], acc[h], 0, 0, 0);
         }
       if (valid) {
-        uint4 pk;
-        uint32_t* pw = reinterpret_cast<uint32_t*>(&pk);
+        u32x4_t pk;
 #pragma unroll
         for (int h = 0; h < 4; ++h) {
           const f32x4_t& a = acc[h >> 1];
           const f32x2_t f = {a[(2 * h) & 3], a[(2 * h + 1) & 3]};
-          pw[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2_t));
+          pk[h] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f, bf16x2_t));
         }
-        *reinterpret_cast<uint4*>(dX + (int64_t)mr * K + 32 * p + 8 * fq) = pk;
+        *reinterpret_cast<u32x4_t*>(dX + (int64_t)mr * K + 32 * p + 8 * fq) = pk;
       }
     }
     __syncthreads();  // both images complete
@@ -233,39 +211,49 @@ __global__ void __launch_bounds__(kBwdThreads, 2) conv1x1_bwd_kernel(
     }
   }
 
-  // ---- weight-gradient partials (lane (fr, fq) of tile (a, t): dW[n = 16 nt + 4 fq + r][k = 16 t + fr])
+  // ---- weight-gradient partial of this workgroup (lane (fr, fq) of tile (a, t): dW[n = 16 nt + 4 fq + r][k = 16 t + fr])
   float* const wp = ws + (int64_t)rwg * N * K;
 #pragma unroll
   for (int a = 0; a < S::NTW; ++a)
 #pragma unroll
     for (int t = 0; t < S::KT; ++t)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = (w * S::NTW + a) * 16 + 4 * fq + r, k = 16 * t + fr;
-        st_sc1(wp + (int64_t)n * K + k, wacc[a][t][r]);
-      }
-  // ---- two-level fixed-order merge
-  const int GS = group, ng = (Gn + GS - 1) / GS;
-  const int gi = rwg / GS, g0 = gi * GS, gc = min(GS, Gn - g0);
-  if (!last_arrival(tickets + gi, gc, flag)) return;
-  float* const gsum = ws + (int64_t)Gn * N * K;
-  for (int e = tid; e < N * K; e += kBwdThreads) {
-    float acc = 0.f;
-    for (int q = g0; q < g0 + gc; ++q) acc += ld_sc1(ws + (int64_t)q * N * K + e);
-    st_sc1(gsum + (int64_t)gi * N * K + e, acc);
-  }
-  if (!last_arrival(tickets + ng, ng, flag)) return;
-  for (int e = tid; e < N * K; e += kBwdThreads) {
-    float acc = 0.f;
-    for (int q = 0; q < ng; ++q) acc += ld_sc1(gsum + (int64_t)q * N * K + e);
-    dW[e] = f32_to_bf16(acc);
-  }
+      for (int r = 0; r < 4; ++r) wp[(int64_t)((w * S::NTW + a) * 16 + 4 * fq + r) * K + 16 * t + fr] = wacc[a][t][r];
 }
 
-int bwd_group(int G) {
-  int g = 1;
-  while (g * g < G) ++g;
-  return g;
+// dW = sum of the G partials [G][NK] in a fixed order: 16 waves per workgroup, each 64 float4
+// columns; wave v sums partials v, v + 16, ... (4 loads in flight per lane), the 16 wave sums meet
+// in LDS and wave 0 adds them in wave order. The kernel boundary makes the partials visible.
+constexpr int kMergeWaves = 16;
+__global__ void __launch_bounds__(64 * kMergeWaves) conv1x1_bwd_merge_kernel(const float* __restrict__ ws, int G,
+                                                                             int nk4, uint16_t* __restrict__ dW) {
+  __shared__ f32x4_t part[kMergeWaves][64];
+  const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;  // float4 column
+  const f32x4_t* const src = reinterpret_cast<const f32x4_t*>(ws);
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  if (c < nk4) {
+    int q = v;
+    for (; q + 3 * kMergeWaves < G; q += 4 * kMergeWaves) {
+      const f32x4_t a0 = src[(int64_t)q * nk4 + c], a1 = src[(int64_t)(q + kMergeWaves) * nk4 + c];
+      const f32x4_t a2 = src[(int64_t)(q + 2 * kMergeWaves) * nk4 + c], a3 = src[(int64_t)(q + 3 * kMergeWaves) * nk4 + c];
+      acc += a0;
+      acc += a1;
+      acc += a2;
+      acc += a3;
+    }
+    for (; q < G; q += kMergeWaves) acc += src[(int64_t)q * nk4 + c];
+  }
+  part[v][lane] = acc;
+  __syncthreads();
+  if (v != 0 || c >= nk4) return;
+  f32x4_t sum = part[0][lane];
+#pragma unroll
+  for (int u = 1; u < kMergeWaves; ++u) sum += part[u][lane];
+  uint2 pk;
+  pk.x = (uint32_t)f32_to_bf16(sum[0]) | ((uint32_t)f32_to_bf16(sum[1]) << 16);
+  pk.y = (uint32_t)f32_to_bf16(sum[2]) | ((uint32_t)f32_to_bf16(sum[3]) << 16);
+  reinterpret_cast<uint2*>(dW)[c] = pk;
 }
 
 template <int K, int N>
@@ -301,23 +289,18 @@ static void bwd_geometry(int M, int K, int N, int* G) {
 int64_t conv1x1_bwd_ws_floats(int M, int K, int N) {
   int G;
   bwd_geometry(M, K, N, &G);
-  const int ng = (G + bwd_group(G) - 1) / bwd_group(G);
-  return (int64_t)(G + ng) * N * K;
-}
-
-int conv1x1_bwd_num_tickets(int M, int K, int N) {
-  int G;
-  bwd_geometry(M, K, N, &G);
-  return (G + bwd_group(G) - 1) / bwd_group(G) + 1;
+  return (int64_t)G * N * K;
 }
 
 hipError_t conv1x1_bwd(const void* g, const void* y, const void* x, const void* w, const float* coef, void* dx,
-                       void* dw, float* ws, int* tickets, int M, int K, int N, hipStream_t s) {
-  if (M <= 0 || ws == nullptr || tickets == nullptr) return hipErrorInvalidValue;
+                       void* dw, float* ws, int M, int K, int N, hipStream_t s) {
+  if (M <= 0 || ws == nullptr) return hipErrorInvalidValue;
   if ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(y) | reinterpret_cast<uintptr_t>(x) |
-       reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(coef)) & 15)
+       reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(dx) | reinterpret_cast<uintptr_t>(dw) |
+       reinterpret_cast<uintptr_t>(ws) | reinterpret_cast<uintptr_t>(coef)) & 15)
     return hipErrorInvalidValue;
   hipError_t err = hipErrorInvalidValue;
+  int G = 0;
   bwd_dispatch(K, N, [&](auto k, auto n) {
     constexpr int kk = decltype(k)::value, nn = decltype(n)::value;
     using S = Cb<kk, nn>;
@@ -327,15 +310,18 @@ hipError_t conv1x1_bwd(const void* g, const void* y, const void* x, const void* 
       if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, S::LDS) != hipSuccess) return;
       attr = true;
     }
-    const int G = bwd_rows<kk, nn>(M);
+    G = bwd_rows<kk, nn>(M);
     hipLaunchKernelGGL((conv1x1_bwd_kernel<kk, nn>), dim3(G), dim3(kBwdThreads), S::LDS, s,
                        static_cast<const uint16_t*>(g), static_cast<const uint16_t*>(y),
                        static_cast<const uint16_t*>(x), static_cast<const uint16_t*>(w), coef,
-                       static_cast<uint16_t*>(dx), static_cast<uint16_t*>(dw), ws, tickets, M,
-                       (M + kBwdBM - 1) / kBwdBM, bwd_group(G));
+                       static_cast<uint16_t*>(dx), ws, M, (M + kBwdBM - 1) / kBwdBM);
     err = hipGetLastError();
   });
-  return err;
+  if (err != hipSuccess) return err;
+  const int nk4 = N * K / 4;
+  hipLaunchKernelGGL(conv1x1_bwd_merge_kernel, dim3((nk4 + 63) / 64), dim3(64 * kMergeWaves), 0, s, ws, G, nk4,
+                     static_cast<uint16_t*>(dw));
+  return hipGetLastError();
 }
 
 }  // namespace ptdt

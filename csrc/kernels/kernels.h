@@ -308,6 +308,12 @@ hipError_t int8_quant_rows(const void* x, int dtype, int M, int K, const uint8_t
 hipError_t int8_mm(const int8_t* A, const float* sa, const int8_t* B, const float* sb, const float* addend,
                    const void* bias, int bias_dtype, int M, int N, int K, void* y, int y_dtype, hipStream_t s);
 bool int8_mm_tiled_supported(int M, int N, int K);
+// hipGraph editing before instantiation (graph_memset.hip): node-type census (counts[type] for
+// type < ncounts; returns the node count, -1 on error) and memset nodes -> fill-kernel nodes
+// (returns how many were replaced, -1 on error)
+int graph_node_census(void* graph, int* counts, int ncounts);
+int graph_replace_memsets(void* graph);
+
 // LLM.int8 decode path (csrc/kernels/int8_decode.hip): M <= 32 rows, K % 64 == 0, K <= kInt8DecodeMaxK.
 // Outlier detection, activation quantisation and the int8 GEMV with the outlier columns fused, in two
 // launches and no host read. ws: int8_decode_ws_bytes(M, K) bytes, 16-B aligned.
@@ -389,9 +395,8 @@ hipError_t bn_backward(const BnBwdArgs& a, hipStream_t s);
 // without storing dY. g, y: [M, N] bf16; x: [M, K]; w: [N, K]; dx: [M, K]; dw: [N, K] bf16.
 bool conv1x1_bwd_supported(int K, int N);
 int64_t conv1x1_bwd_ws_floats(int M, int K, int N);
-int conv1x1_bwd_num_tickets(int M, int K, int N);
 hipError_t conv1x1_bwd(const void* g, const void* y, const void* x, const void* w, const float* coef, void* dx,
-                       void* dw, float* ws, int* tickets, int M, int K, int N, hipStream_t s);
+                       void* dw, float* ws, int M, int K, int N, hipStream_t s);
 // y = ReLU?(x*scale + shift (+ residual)) per channel (eval-mode BN, or any affine epilogue)
 hipError_t bn_apply(const void* x, const void* residual, void* y, int dtype, const float* scale, const float* shift,
                     int64_t M, int C, int relu, hipStream_t s);

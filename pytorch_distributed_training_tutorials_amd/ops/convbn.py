@@ -68,11 +68,10 @@ class ConvBwdLink:
     conv's backward then computes dY on the fly inside its data- and weight-gradient GEMMs. None:
     the BN ran its full backward (the conv receives dY itself)."""
 
-    __slots__ = ("coef", "tickets")
+    __slots__ = ("coef",)
 
-    def __init__(self, tickets):
+    def __init__(self):
         self.coef = None
-        self.tickets = tickets
 
 
 class _Conv1x1StatsFn(torch.autograd.Function):
@@ -103,7 +102,7 @@ class _Conv1x1StatsFn(torch.autograd.Function):
             if not g2.is_contiguous():
                 g2 = g2.contiguous()
             x2 = x.permute(0, 2, 3, 1).reshape(-1, cin)
-            dx2, dw2 = native().conv1x1_bwd(g2, y2, x2, w.reshape(cout, cin), coef, link.tickets)
+            dx2, dw2 = native().conv1x1_bwd(g2, y2, x2, w.reshape(cout, cin), coef)
             dx = dx2.view(n, h, wd, cin).permute(0, 3, 1, 2) if ctx.needs_input_grad[0] else None
             dw = dw2.view(cout, cin, 1, 1) if ctx.needs_input_grad[1] else None
             return dx, dw, *([None] * 10)
@@ -215,10 +214,7 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: torch
     cin, cout = conv.in_channels, conv.out_channels
     clink = None
     if _BWD and torch.is_grad_enabled() and native().conv1x1_bwd_supported(cin, cout):
-        bt = bn._bwd_tickets
-        if bt.numel() < native().conv1x1_bwd_num_tickets(M, cin, cout) or bt.device != x.device:
-            raise RuntimeError("conv_bn_act: BN backward ticket buffer too small or off-device")
-        clink = ConvBwdLink(bt)
+        clink = ConvBwdLink()
     y, stats = _Conv1x1StatsFn.apply(x, w, bn.weight, bn.bias, bn.running_mean if track else None,
                                      bn.running_var if track else None, bn.num_batches_tracked if track else None,
                                      float(bn.momentum), float(bn.eps), tickets, tile, clink)

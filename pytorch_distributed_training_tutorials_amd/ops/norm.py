@@ -230,8 +230,6 @@ class BatchNorm2d(nn.BatchNorm2d):
         # tickets of the statistics merge when a 1x1 conv's epilogue computes this BN's statistics
         # (ops/convbn.py; (merge groups + 1) x column tiles, re-armed in-kernel)
         self.register_buffer("_gemm_tickets", torch.zeros(1024, dtype=torch.int32), persistent=False)
-        # tickets of the fused conv1x1 backward's weight-gradient merge (ops/convbn.py ConvBwdLink)
-        self.register_buffer("_bwd_tickets", torch.zeros(64, dtype=torch.int32), persistent=False)
 
     def forward(self, x, residual=None, relu: bool = False, link: bool = False):
         self._check_input_dim(x)

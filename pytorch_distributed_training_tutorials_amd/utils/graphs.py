@@ -27,11 +27,16 @@ the ResNet-50 train loop NB03:969-992.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable
 
 import torch
 
 from ..ops.fused_step import WatchedGraph
+
+# memset nodes -> fill-kernel nodes before instantiation (csrc/kernels/graph_memset.hip); 0: keep them
+_MEMSET_FIX = os.environ.get("PTDT_GRAPH_MEMSET_FIX", "1") != "0"
+_MEMSET_NODE_TYPE = 2  # hipGraphNodeTypeMemset
 
 
 def _detach(out):
@@ -75,7 +80,7 @@ class GraphedStep:
         rc = getattr(self.comm, "handle", None) if self.comm is not None else None
         before = rc.captured if rc is not None else 0
         self.graph = None  # the old graph (and its memory pool) goes first
-        g = torch.cuda.CUDAGraph()
+        g = torch.cuda.CUDAGraph(keep_graph=True)
         with torch.cuda.graph(g, stream=self._stream, capture_error_mode="thread_local"):
             # detached: a captured loss that keeps its autograd graph alive also keeps every
             # parameter's AccumulateGrad node alive -- nodes created on the capture stream, which
@@ -83,6 +88,15 @@ class GraphedStep:
             # DDP hooks run on the capture stream while their inputs come from the eager one
             # (cross-stream frees of gradient buffers)
             self.outputs = _detach(self.fn())
+        # edit the raw graph before instantiation: MIOpen's hipMemsetAsync calls (atomic
+        # weight-gradient solvers) become fill-kernel nodes (profiles/r4_graph_memset.md)
+        from .. import native
+
+        raw = g.raw_cuda_graph()
+        census = native().graph_node_census(raw)
+        self.node_count, self.memset_nodes = int(census[0]), int(census[1 + _MEMSET_NODE_TYPE])
+        self.memsets_replaced = native().graph_replace_memsets(raw) if _MEMSET_FIX else 0
+        g.instantiate()
         torch.cuda.synchronize(self.device)
         self.graph = WatchedGraph(g, rc, (rc.captured - before) if rc is not None else 0)
         self.captures += 1
