@@ -878,6 +878,15 @@ std::vector<int64_t> graph_node_census_(int64_t graph) {
   return out;  // [total, count of hipGraphNodeType 0, 1, ...]
 }
 
+// hipMemsetAsync of a whole tensor (byte value) on the current stream: a capturable memset for the
+// graph-editing tests (tests/test_graphs_gpu.py); the framework's own paths issue none
+void memset_async_(Tensor t, int64_t value) {
+  check_gpu(t, "t");
+  TORCH_CHECK(t.is_contiguous(), "memset_async_: contiguous tensor");
+  c10::hip::HIPGuard guard(t.device().index());
+  hip_check(hipMemsetAsync(t.data_ptr(), (int)value, t.numel() * t.element_size(), cur_stream(t)), "memset_async_");
+}
+
 int64_t graph_replace_memsets_(int64_t graph) {
   const int r = graph_replace_memsets(reinterpret_cast<void*>(graph));
   TORCH_CHECK(r >= 0, "graph_replace_memsets: hipGraph edit failed");
@@ -1471,6 +1480,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv1x1_bwd", &conv1x1_bwd_, "fused BN-apply + 1x1 conv data and weight gradients (bf16)");
   m.def("conv1x1_bwd_supported", &conv1x1_bwd_supported_);
   m.def("graph_node_census", &graph_node_census_, "node count and per-hipGraphNodeType counts of a raw hipGraph_t");
+  m.def("memset_async_", &memset_async_, "hipMemsetAsync of a whole tensor (tests of the graph memset rewrite)");
   m.def("graph_replace_memsets", &graph_replace_memsets_, "replace a raw hipGraph_t's memset nodes by fill-kernel nodes");
   m.def("int8_decode", &int8_decode_, "LLM.int8 decode path (M <= 32): outliers + quantise + int8 GEMV, no host sync");
   m.def("int8_decode_supported", &int8_decode_supported);

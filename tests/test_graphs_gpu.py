@@ -94,6 +94,33 @@ def test_col_sum_replay_after_eager_launches(dev, native):
         torch.testing.assert_close(out, want, rtol=1e-4, atol=1e-3, msg=lambda m: f"round {rnd}: {m}")
 
 
+def test_graph_memset_nodes_replaced(dev, native):
+    """GraphedStep rewrites a captured hipMemsetAsync into a fill-kernel node before instantiation
+    (csrc/kernels/graph_memset.hip; profiles/r4_graph_memset.md) and the replay still zeroes the buffer,
+    also after eager memsets of other buffers."""
+    from pytorch_distributed_training_tutorials_amd.utils.graphs import GraphedStep
+
+    buf = torch.full((1000,), 7.0, device=dev)
+    half = torch.full((4099,), 3, dtype=torch.int16, device=dev)  # odd byte count
+
+    def fn():
+        native.memset_async_(buf, 0)
+        buf.add_(1.0)
+        native.memset_async_(half, 0)
+        half.add_(2)
+
+    gs = GraphedStep(fn, dev, warmup=1)
+    assert gs.memset_nodes >= 2 and gs.memsets_replaced == gs.memset_nodes
+    other = torch.empty(4096, device=dev)
+    for _ in range(3):
+        native.memset_async_(other, 0)  # eager memsets between replays
+        buf.fill_(5.0)
+        half.fill_(9)
+        gs()
+        torch.cuda.synchronize(dev)
+        assert bool((buf == 1.0).all()) and bool((half == 2).all())
+
+
 def test_col_sum_deterministic(dev, native):
     """Bias gradients are fixed-order sums: bit-identical across launches (no atomics)."""
     for rows, cols in ((128, 1000), (32, 1), (20000, 96), (3, 4100)):
