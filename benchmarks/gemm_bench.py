@@ -70,7 +70,7 @@ def main():
             def auto():
                 outs["auto"] = gemm_nt_big(A, Bt, torch.bfloat16)
             variants["auto"] = auto
-            variants["big256"] = lambda: C_.gemm_big_(A, Bt, Cb)  # default schedule (3)
+            variants["big256"] = lambda: C_.gemm_big_(A, Bt, Cb)  # default schedule (4)
             for sc in a.extra_sched:
                 variants[f"big256_sched{sc}"] = (lambda sc=sc: C_.gemm_big_(A, Bt, Cb, sched=sc))
             variants["big128"] = lambda: C_.gemm_big_(A, Bt, Cb, tile=128)

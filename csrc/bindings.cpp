@@ -693,7 +693,7 @@ void gemm_big_(Tensor A, Tensor Bt, Tensor C, c10::optional<Tensor> bias, bool r
   g.alpha = (float)alpha;
   g.beta = (float)beta;
   g.tile = tile == 128 ? 128 : 256;
-  g.sched = sched < 0 ? (g.tile == 256 ? 3 : 0) : (int)sched;  // 256 tile: the 8-phase schedule
+  g.sched = sched < 0 ? (g.tile == 256 ? 4 : 0) : (int)sched;  // 256 tile: 8-phase schedule, grouped tile order
   g.split_k = split_k > 1 ? (int)split_k : 1;
   TORCH_CHECK(g.split_k == 1 || (C.scalar_type() == at::kFloat && !relu && beta == 0.0),
               "gemm_big: split-K accumulates fp32 atomics: C must be f32 (pre-zeroed), no relu/beta");

@@ -792,12 +792,32 @@ __device__ __forceinline__ void vm_wait_n(int n) {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int OUT>
+// GRP > 0: tiles ordered in groups of GRP tile rows, column-major inside a group, so one XCD's
+// contiguous chunk of the grid (xcd_remap) is a GRP x (chunk / GRP) block: its concurrently running
+// workgroups share GRP A panels and a few B panels in that XCD's L2 instead of one A panel and ~32
+// B panels (row-major order).
+template <int GRP>
+__device__ __forceinline__ void tile_coords(int tile, int tm, int tn, int& bm, int& bn) {
+  if constexpr (GRP == 0) {
+    bm = tile / tn;
+    bn = tile % tn;
+  } else {
+    const int per = GRP * tn;
+    const int grp = tile / per, first = grp * GRP;
+    const int gsz = min(tm - first, GRP);
+    const int in = tile - grp * per;
+    bm = first + in % gsz;
+    bn = in / gsz;
+  }
+}
+
+template <int OUT, int GRP>
 __global__ void __launch_bounds__(512) gemm_bf16_p8_kernel(BigGemmArgs g, int tm, int tn, int kt_per) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   constexpr int FI = 8, FJ = 4;
-  const int tile = xcd_remap(blockIdx.x, tm * tn);
-  const int m0 = (tile / tn) * 256, n0 = (tile % tn) * 256;
+  int bm, bn;
+  tile_coords<GRP>(xcd_remap(blockIdx.x, tm * tn), tm, tn, bm, bn);
+  const int m0 = bm * 256, n0 = bn * 256;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wid >> 2, wc = wid & 3;
@@ -916,9 +936,9 @@ __global__ void __launch_bounds__(512) gemm_bf16_p8_kernel(BigGemmArgs g, int tm
   }
 }
 
-template <int OUT>
+template <int OUT, int GRP>
 hipError_t launch_p8(const BigGemmArgs& g, int split, hipStream_t s) {
-  const void* fn = reinterpret_cast<const void*>(&gemm_bf16_p8_kernel<OUT>);
+  const void* fn = reinterpret_cast<const void*>(&gemm_bf16_p8_kernel<OUT, GRP>);
   static bool attr_set = false;
   if (!attr_set) {
     PTDT_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, P8LDS));
@@ -928,7 +948,7 @@ hipError_t launch_p8(const BigGemmArgs& g, int split, hipStream_t s) {
   const int nk = g.K / BK;
   const int kt_per = (nk + split - 1) / split;
   split = (nk + kt_per - 1) / kt_per;
-  hipLaunchKernelGGL((gemm_bf16_p8_kernel<OUT>), dim3(tm * tn, split), dim3(512), P8LDS, s, g, tm, tn, kt_per);
+  hipLaunchKernelGGL((gemm_bf16_p8_kernel<OUT, GRP>), dim3(tm * tn, split), dim3(512), P8LDS, s, g, tm, tn, kt_per);
   return hipGetLastError();
 }
 
@@ -1040,8 +1060,20 @@ hipError_t gemm_bf16_big(const BigGemmArgs& g, hipStream_t s) {
     return g.out_dtype == kF32 ? launch_piece<1>(g, 1, s) : launch_piece<0>(g, 1, s);
   }
   if (g.sched == 3) {
-    if (split > 1) return launch_p8<2>(g, split, s);
-    return g.out_dtype == kF32 ? launch_p8<1>(g, 1, s) : launch_p8<0>(g, 1, s);
+    if (split > 1) return launch_p8<2, 0>(g, split, s);
+    return g.out_dtype == kF32 ? launch_p8<1, 0>(g, 1, s) : launch_p8<0, 0>(g, 1, s);
+  }
+  if (g.sched == 4) {  // 8-phase with grouped tile order (8 tile rows per group)
+    if (split > 1) return launch_p8<2, 8>(g, split, s);
+    return g.out_dtype == kF32 ? launch_p8<1, 8>(g, 1, s) : launch_p8<0, 8>(g, 1, s);
+  }
+  if (g.sched == 5) {  // group of 4 tile rows (A/B of the group size)
+    if (split > 1) return launch_p8<2, 4>(g, split, s);
+    return g.out_dtype == kF32 ? launch_p8<1, 4>(g, 1, s) : launch_p8<0, 4>(g, 1, s);
+  }
+  if (g.sched == 6) {  // group of 16 tile rows
+    if (split > 1) return launch_p8<2, 16>(g, split, s);
+    return g.out_dtype == kF32 ? launch_p8<1, 16>(g, 1, s) : launch_p8<0, 16>(g, 1, s);
   }
   return hipErrorInvalidValue;
 }

@@ -238,7 +238,7 @@ struct BigGemmArgs {
   const void* bias; int bias_dtype;
   int relu;
   float alpha, beta;
-  int sched;    // 0: read-then-multiply per K-tile, 1: ping-pong wave pairs, 2: ping-pong fed from a 10-piece LDS ring, 3: 8-phase quadrant schedule (default, 256 tile)
+  int sched;    // 0: read-then-multiply per K-tile, 1: ping-pong wave pairs, 2: ping-pong fed from a 10-piece LDS ring, 3: 8-phase quadrant schedule, 4: 3 with grouped tile order (default, 256 tile), 5 / 6: group of 4 / 16 rows
   int tile;     // 256: 256x256 block tile (8 waves), 128: 128x128 (4 waves, 2 workgroups per CU)
   int split_k;  // >1: K split over gridDim.y, fp32 atomics into a pre-zeroed f32 C (no ReLU/beta)
 };

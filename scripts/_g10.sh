@@ -1,0 +1,4 @@
+cd $GRAFT_REPO_ROOT
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -p no:cacheprovider --no-header --tb=short > gpurun_out/t_all10.log 2>&1 || exit 1
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke10.log 2>&1 || exit 2
+timeout -k 10 400 python -u bench.py > gpurun_out/bench10.json 2> gpurun_out/bench10.err || exit 3

@@ -121,7 +121,7 @@ def test_gemm_layouts(native, dev, dtype, M, N, K, layout):
 @pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 1024), (300, 200, 128), (120, 1000, 2048),
                                    (1, 257, 64), (1000, 17, 192)])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("sched", [0, 1, 2, 3])
+@pytest.mark.parametrize("sched", [0, 1, 2, 3, 4, 5, 6])
 def test_gemm_big_matches_fp32(native, dev, M, N, K, out_dtype, sched):
     """256x256 LDS-DMA kernel: C = A.Bt^T (+bias, ReLU, alpha/beta) vs fp32 on the same bf16 operands;
     asymmetric operands catch a transposed C write, edge shapes the clamped rows."""
