@@ -26,6 +26,10 @@ import uuid
 _SLOT = 64  # bytes per rank: one cache line, one writer
 
 
+class SetupFailed(RuntimeError):
+    """Raised on EVERY rank when any rank could not create or map the shared page."""
+
+
 class NodeSpinBarrier:
     def __init__(self, comm, timeout_s: float = 60.0):
         self.rank, self.world = comm.rank, comm.world
@@ -33,19 +37,35 @@ class NodeSpinBarrier:
         name = comm.all_gather_object(f"ptdt_spin_{os.getpid()}_{uuid.uuid4().hex[:12]}")[0]  # rank 0's
         self.path = os.path.join("/dev/shm", name)
         size = max(mmap.PAGESIZE, _SLOT * self.world)
+        self.mm = None
+        err = ""
         if self.rank == 0:
-            fd = os.open(self.path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
-            os.ftruncate(fd, size)
-            os.close(fd)
-        comm.barrier()
-        fd = os.open(self.path, os.O_RDWR)
-        try:
-            self.mm = mmap.mmap(fd, size)
-        finally:
-            os.close(fd)
-        comm.barrier()
-        if self.rank == 0:  # every rank has it mapped: the name can go (the mapping stays valid)
-            os.unlink(self.path)
+            try:
+                fd = os.open(self.path, os.O_CREAT | os.O_EXCL | os.O_RDWR, 0o600)
+                os.ftruncate(fd, size)
+                os.close(fd)
+            except OSError as e:
+                err = f"rank 0: {e}"
+        # every step agrees across ranks (a rank that raised alone would leave the others in a barrier)
+        errs = [e for e in comm.all_gather_object(err) if e]
+        if not errs:
+            try:
+                fd = os.open(self.path, os.O_RDWR)
+                try:
+                    self.mm = mmap.mmap(fd, size)
+                finally:
+                    os.close(fd)
+            except OSError as e:
+                err = f"rank {self.rank}: {e}"
+            errs = [e for e in comm.all_gather_object(err) if e]
+        if self.rank == 0:  # every rank has it mapped (or gave up): the name can go
+            try:
+                os.unlink(self.path)
+            except OSError:
+                pass
+        if errs:
+            self.close()
+            raise SetupFailed("; ".join(errs))
         self.epoch = 0
         self._offs = [r * _SLOT for r in range(self.world)]
 
@@ -68,7 +88,8 @@ class NodeSpinBarrier:
 
     def close(self):
         try:
-            self.mm.close()
+            if self.mm is not None:
+                self.mm.close()
         except Exception:  # noqa: BLE001
             pass
 
@@ -77,6 +98,9 @@ def create(comm, timeout_s: float = 60.0):
     """A barrier over ``comm``'s ranks when they all share this node (else None)."""
     world = comm.world
     local = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-    if world <= 1 or local != world or not os.path.isdir("/dev/shm"):
+    if world <= 1 or local != world:
         return None
-    return NodeSpinBarrier(comm, timeout_s)
+    try:
+        return NodeSpinBarrier(comm, timeout_s)
+    except SetupFailed:  # collective: every rank falls back to the collective barrier together
+        return None
