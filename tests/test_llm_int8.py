@@ -172,3 +172,23 @@ def test_llm_int8_decode_llama_shape(dev):
     y = m(x)
     ref = llm_int8_reference(x, m.weight_q, m.weight_scale, None, m.threshold)
     torch.testing.assert_close(y, ref, rtol=1e-2, atol=1e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [5, 32])
+def test_llm_int8_decode_many_outliers_across_workgroups(dev, M):
+    """fp32 decode with 40 outlier columns spread over the four 512-column statistics workgroups of
+    K = 2048 (several per workgroup, one in the last chunk): the per-workgroup lists concatenate in
+    column order and the product matches the reference to fp32 rounding."""
+    from pytorch_distributed_training_tutorials_amd.ops.quant import Int8Linear, llm_int8_reference
+
+    torch.manual_seed(M)
+    lin = torch.nn.Linear(2048, 200, device=dev)
+    m = Int8Linear.from_linear(lin, llm_int8=True)
+    x = torch.randn(M, 2048, device=dev)
+    cols = torch.randperm(2047, generator=torch.Generator().manual_seed(M))[:39].tolist() + [2047]
+    for j, col in enumerate(cols):
+        x[j % M, col] = 10.0 + j
+    y = m(x)
+    ref = llm_int8_reference(x, m.weight_q, m.weight_scale, m.bias, m.threshold)
+    torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-4)
