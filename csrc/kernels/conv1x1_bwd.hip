@@ -270,7 +270,7 @@ bool bwd_dispatch(int K, int N, F&& f) {
     f(std::integral_constant<int, k>{}, std::integral_constant<int, n>{}); \
     return true;                                                            \
   }
-  PTDT_C1B(64, 64) PTDT_C1B(64, 256) PTDT_C1B(256, 64)
+  PTDT_C1B(64, 64) PTDT_C1B(64, 256) PTDT_C1B(256, 64) PTDT_C1B(256, 128)
 #undef PTDT_C1B
   return false;
 }

@@ -50,6 +50,8 @@ _STREAM = os.environ.get("PTDT_CONVBN_STREAM", "1") != "0"
 # fused backward (BN apply + 1x1 data and weight gradients, csrc/kernels/conv1x1_bwd.hip) where an
 # instance exists; 0: the BN's full backward, then MIOpen's convolution_backward
 _BWD = os.environ.get("PTDT_CONVBN_BWD", "1") != "0"
+# A/B of single shapes: "KxN,KxN" (input x output channels) keep the unfused backward
+_BWD_SKIP = {tuple(int(v) for v in t.split("x")) for t in os.environ.get("PTDT_CONVBN_BWD_SKIP", "").split(",") if t}
 _CHOICE: dict[tuple, bool] = {}  # (M, K, N, tile) -> fused is faster (PTDT_CONVBN=auto)
 
 
@@ -213,7 +215,7 @@ def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: torch
         raise RuntimeError(f"conv_bn_act: BN ticket buffer too small ({tickets.numel()} < {need}) or off-device")
     cin, cout = conv.in_channels, conv.out_channels
     clink = None
-    if _BWD and torch.is_grad_enabled() and native().conv1x1_bwd_supported(cin, cout):
+    if _BWD and torch.is_grad_enabled() and (cin, cout) not in _BWD_SKIP and native().conv1x1_bwd_supported(cin, cout):
         clink = ConvBwdLink()
     y, stats = _Conv1x1StatsFn.apply(x, w, bn.weight, bn.bias, bn.running_mean if track else None,
                                      bn.running_var if track else None, bn.num_batches_tracked if track else None,

@@ -170,7 +170,8 @@ def test_resnet50_step_uses_fused_kernels(dev, monkeypatch):
     assert e1 <= 1.5 * e2 + 1e-2, f"whole-model gradient error: fused {e1:.3g} vs unfused {e2:.3g}"
 
 
-@pytest.mark.parametrize("M,K,N", [(6272, 64, 256), (6272, 256, 64), (4000, 64, 64), (100003, 64, 256), (131, 256, 64)])
+@pytest.mark.parametrize("M,K,N", [(6272, 64, 256), (6272, 256, 64), (4000, 64, 64), (100003, 64, 256), (131, 256, 64),
+                                   (5000, 256, 128)])
 def test_conv1x1_bwd_matches_reference(native, dev, M, K, N):
     """csrc/kernels/conv1x1_bwd.hip against fp32 PyTorch: dY = A g + B y + C (rounded to bf16, as the
     unfused BN apply stores it), dX = dY W, dW = dY^T X; M not a multiple of the 64-row block; two
@@ -194,7 +195,7 @@ def test_conv1x1_bwd_matches_reference(native, dev, M, K, N):
     assert torch.equal(dx, dx2) and torch.equal(dw, dw2)
 
 
-@pytest.mark.parametrize("inplanes,planes,downsample", [(256, 64, False), (64, 64, True)])
+@pytest.mark.parametrize("inplanes,planes,downsample", [(256, 64, False), (64, 64, True), (256, 128, True)])
 def test_bottleneck_fused_backward_matches_unfused_backward(dev, monkeypatch, inplanes, planes, downsample):
     """conv+BN fused forward in both runs; the backward fused (BN reduce pass, then BN-apply + data and
     weight gradients in one kernel) vs the BN's full backward + MIOpen's convolution_backward."""
