@@ -28,9 +28,8 @@ __global__ void __launch_bounds__(kThreads) quant_kernel(const T* w, int64_t col
   for (int64_t c = threadIdx.x; c < cols; c += kThreads) amax = fmaxf(amax, fabsf(Cvt<T>::load(wr, c)));
   amax = block_max(amax, red);
   const float sc = amax > 0.f ? amax / 127.f : 1.f;
-  const float inv = 1.f / sc;
   for (int64_t c = threadIdx.x; c < cols; c += kThreads) {
-    float v = rintf(Cvt<T>::load(wr, c) * inv);
+    float v = rintf(Cvt<T>::load(wr, c) / sc);  // IEEE division: the reference's round(w / s) bit for bit
     v = fminf(fmaxf(v, -127.f), 127.f);
     q[r * cols + c] = (int8_t)v;
   }

@@ -7,7 +7,8 @@
 //                    per chunk, the workgroup's outlier columns in column order, and per row the
 //                    absmax over its non-outlier columns (a per-workgroup partial).
 //   i8_decode_quant  same partition: the row scales (max over the stats partials, fixed order) and x
-//                    quantised to int8 (rint(x / s), outlier columns 0, padding rows M..Mp-1 0).
+//                    quantised to int8 (rint(x / s) with a true division, outlier columns 0, padding
+//                    rows M..Mp-1 0).
 //   i8_decode_gemv   one workgroup per 16 output features, 4 or 8 waves splitting K: each lane streams
 //                    16 weight bytes per 64-deep K step (plain loads -- non-temporal ones measured 7-15 % slower -- 8 steps in flight) into
 //                    v_mfma_i32_16x16x64_i8 against the quantised rows (L2-resident); exact int32
@@ -138,7 +139,7 @@ __global__ void __launch_bounds__(256) i8_decode_quant_kernel(const T* __restric
                                                               const float* __restrict__ rowpart,
                                                               int8_t* __restrict__ xq, float* __restrict__ sx) {
   __shared__ float part[32 * 32];
-  __shared__ float sinv[32];
+  __shared__ float ssc[32];
   const int tid = threadIdx.x, lane = tid & 63, rg = tid >> 6;
   const int nch = K >> 3;
   const int c = blockIdx.x * kStatChunks + lane;
@@ -155,7 +156,7 @@ __global__ void __launch_bounds__(256) i8_decode_quant_kernel(const T* __restric
     float a = 0.f;
     for (int b = 0; b < nsb; ++b) a = fmaxf(a, part[b * 32 + tid]);  // exact: order-free
     const float sc = a > 0.f ? a / 127.f : 1.f;
-    sinv[tid] = 1.f / sc;
+    ssc[tid] = sc;
     if (blockIdx.x == 0 && tid < Mp) sx[tid] = tid < M ? sc : 1.f;
   }
   __syncthreads();
@@ -164,11 +165,11 @@ __global__ void __launch_bounds__(256) i8_decode_quant_kernel(const T* __restric
   for (int u = 0; u < 8; ++u) {
     const int m = m0 + u;
     if (m >= Mp) break;
-    const float inv = sinv[m < M ? m : 0];
+    const float sc = ssc[m < M ? m : 0];  // x / s (IEEE division, as the reference), not x * (1 / s)
     uint32_t w[2] = {0u, 0u};
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float q = (m < M && !(ob & (1u << e))) ? rintf(v[u][e] * inv) : 0.f;
+      float q = (m < M && !(ob & (1u << e))) ? rintf(v[u][e] / sc) : 0.f;
       q = fminf(fmaxf(q, -127.f), 127.f);
       w[e >> 2] |= ((uint32_t)(int32_t)q & 0xffu) << (8 * (e & 3));
     }

@@ -73,9 +73,8 @@ __global__ void __launch_bounds__(kThreads) row_quant_kernel(const T* __restrict
     if (!(mask && mask[k])) amax = fmaxf(amax, fabsf(Cvt<T>::load(xr, k)));
   amax = block_max(amax, red);
   const float sc = amax > 0.f ? amax / 127.f : 1.f;
-  const float inv = 1.f / sc;
   for (int k = threadIdx.x; k < K; k += kThreads) {
-    float v = (mask && mask[k]) ? 0.f : rintf(Cvt<T>::load(xr, k) * inv);
+    float v = (mask && mask[k]) ? 0.f : rintf(Cvt<T>::load(xr, k) / sc);  // IEEE division, as the reference
     v = fminf(fmaxf(v, -127.f), 127.f);
     q[r * K + k] = (int8_t)v;
   }
