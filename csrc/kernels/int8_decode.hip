@@ -277,15 +277,31 @@ struct Ws {
   int* ocnt;
   int* olist;
 };
+// byte offsets of the workspace pieces (all 16-B aligned: K % 64 == 0)
+struct WsLayout {
+  size_t sx, cbits, rowpart, ocnt, olist, total;
+};
+WsLayout ws_layout(int M, int K) {
+  const size_t Mp = M <= 16 ? 16 : 32, nsb = (size_t)stats_blocks(K);
+  WsLayout l;
+  l.sx = Mp * (size_t)K;
+  l.cbits = l.sx + 32 * sizeof(float);
+  l.rowpart = l.cbits + ((size_t)(K >> 3) + 15) / 16 * 16;
+  l.ocnt = l.rowpart + nsb * 32 * sizeof(float);
+  l.olist = l.ocnt + nsb * sizeof(int);
+  l.total = l.olist + nsb * kListCap * sizeof(int);
+  return l;
+}
 Ws carve(void* base, int M, int K) {
-  const int Mp = M <= 16 ? 16 : 32, nsb = stats_blocks(K);
+  const WsLayout l = ws_layout(M, K);
+  uint8_t* const b = static_cast<uint8_t*>(base);
   Ws w;
-  w.xq = static_cast<int8_t*>(base);
-  w.sx = reinterpret_cast<float*>(w.xq + (size_t)Mp * K);
-  w.cbits = reinterpret_cast<uint8_t*>(w.sx + 32);
-  w.rowpart = reinterpret_cast<float*>(w.cbits + ((size_t)(K >> 3) + 15) / 16 * 16);
-  w.ocnt = reinterpret_cast<int*>(w.rowpart + (size_t)nsb * 32);
-  w.olist = w.ocnt + nsb;
+  w.xq = reinterpret_cast<int8_t*>(b);
+  w.sx = reinterpret_cast<float*>(b + l.sx);
+  w.cbits = b + l.cbits;
+  w.rowpart = reinterpret_cast<float*>(b + l.rowpart);
+  w.ocnt = reinterpret_cast<int*>(b + l.ocnt);
+  w.olist = reinterpret_cast<int*>(b + l.olist);
   return w;
 }
 
@@ -318,10 +334,7 @@ hipError_t launch_t(const void* xv, int M, int K, float thr, const int8_t* W, co
 
 }  // namespace
 
-size_t int8_decode_ws_bytes(int M, int K) {
-  const Ws w = carve(nullptr, M, K);
-  return reinterpret_cast<size_t>(w.olist + (size_t)stats_blocks(K) * kListCap) + 16;
-}
+size_t int8_decode_ws_bytes(int M, int K) { return ws_layout(M, K).total + 16; }
 
 bool int8_decode_supported(int M, int N, int K) {
   return M >= 1 && M <= 32 && N >= 1 && K >= 64 && K % 64 == 0 && K <= kInt8DecodeMaxK;
