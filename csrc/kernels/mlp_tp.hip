@@ -111,10 +111,11 @@ __device__ __forceinline__ float sgd1(float& w, float& m, float g, bool first, f
 // lines) instead of 64 words strided by Din (64 separate uncached transactions), and one
 // poll instruction reads them back the same way -- round 2's flat-index pushes were
 // 3.3K scattered uncached writes per step (share-GPU W=2: 6.4 us/step vs 2.8 at W=1).
-// Polls of 2 peers are in flight together; the loop is uniform (ballot exit,
+// Polls of G peers are in flight together (G = 3 for the index-CE / vector-staging instances, whose registers allow
+// it: W = 4 in one poll round, W = 8 in 3 -- 2 for the others); the loop is uniform (ballot exit,
 // every lane re-polls its whole set), contributions are summed in rank order (own value
 // from the register): bit-identical replicas. Padded values (zero gradients) travel too.
-template <int NV>
+template <int NV, int G>
 __device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq, float (&v)[NV], int wave, int lane) {
   const int parity = (int)(seq & 1u);
   const uint64_t hi = (uint64_t)seq << 32;
@@ -133,7 +134,6 @@ __device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq,
 #pragma unroll
   for (int k = 0; k < NV; ++k) acc[k] = 0.f;
   bool ok = true;
-  constexpr int G = 2;  // peers polled together (VGPR budget: 2 waves share SIMD 0 with the helper)
   for (int p0 = 0; p0 < x.world; p0 += G) {
     uint64_t w[G][NV];
     auto issue = [&]() {
@@ -254,6 +254,44 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   };
   auto list = [&](int e) { return elist + (e % 3) * d.estride; };
   auto stage = [&](int slot) { return stage0 + slot * St::FLOATS; };
+
+  // ---- resident state of the compute waves, loaded first so that its latency hides under the
+  // sampler lists and the staging below (hipcc also spills less this way: 0-41 vs 1-46 VGPRs): this wave's W1 rows (b1 as column Din) and W2 columns in
+  // MFMA result layouts, so the gradients land on them lane for lane and SGD runs in registers:
+  //   w1r[mt][i] = W1aug[unit 16w + c][input 16 mt + 4q + i]   (= dW1^T's layout)
+  //   w2t[i]     = W2[class 4q + i][unit 16w + c]              (= dW2's layout)
+  //   b2c        = b2[class c] (= db2's layout: the column sums of dZ^T)
+  const int unit = 16 * w + c;
+  float w1r[MT][4], m1r[MT][4], w2t[4], m2t[4], b2c = 0.f, mb2c = 0.f;
+  int opt_step = 0;
+  uint32_t seq = 0u;
+  bool failed = false;
+  auto load_state = [&]() {
+    const auto P = gptr(a.P);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int in = 16 * mt + 4 * q + i;
+        const int off = in < Din ? d.oW1 + unit * Din + in : (hb && in == Din ? d.ob1 + unit : -1);
+        w1r[mt][i] = off >= 0 ? P[off] : 0.f;
+        m1r[mt][i] = (off >= 0 && use_mom) ? a.mom[off] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int cls = 4 * q + i;
+      const bool real = cls < Dout;
+      w2t[i] = real ? P[d.oW2 + cls * H + unit] : 0.f;
+      m2t[i] = (real && use_mom) ? a.mom[d.oW2 + cls * H + unit] : 0.f;
+    }
+    b2c = (hb && c < Dout) ? P[d.ob2 + c] : 0.f;
+    mb2c = (hb && c < Dout && use_mom) ? a.mom[d.ob2 + c] : 0.f;
+    opt_step = a.opt_step ? *a.opt_step : 0;
+    seq = AR ? *a.ar.seq : 0u;
+    failed = AR && *a.ar.err != 0;
+  };
+  if (w < NW) load_state();
 
   // ---- sampler lists: epoch e0 whole, epoch e0+1 up to batch j0 (entries of later
   // positions are produced S+1 steps ahead inside the loop)
@@ -483,39 +521,10 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   }
 
   // ================================================================ compute waves
-  // ---- resident state: this wave's W1 rows (b1 as column Din) and W2 columns in
-  // MFMA result layouts, so the gradients land on them lane for lane and SGD runs
-  // in registers:
-  //   w1r[mt][i] = W1aug[unit 16w + c][input 16 mt + 4q + i]   (= dW1^T's layout)
-  //   w2t[i]     = W2[class 4q + i][unit 16w + c]              (= dW2's layout)
-  const auto P = gptr(a.P);
-  // b2c = b2[class c] (= db2's layout: the column sums of dZ^T), mirrored to LDS for the forward
-  float w1r[MT][4], m1r[MT][4], w2t[4], m2t[4], b2c, mb2c;
-  const int unit = 16 * w + c;
+  // (resident state loaded at the top of the kernel; its forward-layout LDS mirrors now)
 #pragma unroll
-  for (int mt = 0; mt < MT; ++mt) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int in = 16 * mt + 4 * q + i;
-      const int off = in < Din ? d.oW1 + unit * Din + in : (hb && in == Din ? d.ob1 + unit : -1);
-      w1r[mt][i] = off >= 0 ? P[off] : 0.f;
-      m1r[mt][i] = (off >= 0 && use_mom) ? a.mom[off] : 0.f;
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int cls = 4 * q + i;
-    const bool real = cls < Dout;
-    w2t[i] = real ? P[d.oW2 + cls * H + unit] : 0.f;
-    m2t[i] = (real && use_mom) ? a.mom[d.oW2 + cls * H + unit] : 0.f;
-    W2m[cls * LD2 + c] = w2t[i];  // forward layout copy: W2[class c][unit 4q + s] at c*LD2 + 4q + s
-  }
-  b2c = (hb && c < Dout) ? P[d.ob2 + c] : 0.f;
-  mb2c = (hb && c < Dout && use_mom) ? a.mom[d.ob2 + c] : 0.f;
+  for (int i = 0; i < 4; ++i) W2m[(4 * q + i) * LD2 + c] = w2t[i];  // W2[class c][unit 4q + s] at c*LD2 + 4q + s
   if (q == 0) B2m[c] = b2c;
-  int opt_step = a.opt_step ? *a.opt_step : 0;
-  uint32_t seq = AR ? *a.ar.seq : 0u;
-  bool failed = AR && *a.ar.err != 0;
 
   // last step's (averaged) gradients, written to the DDP bucket at the end
   float lg1[MT][4], lg2[4], ldb2 = 0.f;
@@ -785,7 +794,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
           v[4 * MT + i] = gv2[i];
         }
         v[4 * MT + 4] = db2;  // b2[class c]: the same value in every wave (identical loss in every wave)
-        failed = !tp_allreduce_lm<NV>(a.ar, seq, v, w, l);
+        failed = !tp_allreduce_lm<NV, (LOSS == kLossCEIndex && VX) ? 3 : 2>(a.ar, seq, v, w, l);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
 #pragma unroll
