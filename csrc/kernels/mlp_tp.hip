@@ -112,7 +112,8 @@ __device__ __forceinline__ float sgd1(float& w, float& m, float g, bool first, f
 // poll instruction reads them back the same way -- round 2's flat-index pushes were
 // 3.3K scattered uncached writes per step (share-GPU W=2: 6.4 us/step vs 2.8 at W=1).
 // Polls of G peers are in flight together (G = 3 for the index-CE / vector-staging instances, whose registers allow
-// it: W = 4 in one poll round, W = 8 in 3 -- 2 for the others); the loop is uniform (ballot exit,
+// it: the W - 1 other ranks in ceil((W - 1) / G) poll rounds, W = 4 in one and W = 8 in 3 -- 2 for the
+// others); the loop is uniform (ballot exit,
 // every lane re-polls its whole set), contributions are summed in rank order (own value
 // from the register): bit-identical replicas. Padded values (zero gradients) travel too.
 template <int NV, int G>
@@ -134,15 +135,17 @@ __device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq,
 #pragma unroll
   for (int k = 0; k < NV; ++k) acc[k] = 0.f;
   bool ok = true;
-  for (int p0 = 0; p0 < x.world; p0 += G) {
+  bool own = false;  // this rank's value added (rank order: just before the first higher peer)
+  const int np = x.world - 1;  // the OTHER ranks, polled in groups of G in increasing rank order
+  auto peer = [&](int i) { return i < x.rank ? i : i + 1; };
+  for (int i0 = 0; i0 < np; i0 += G) {
     uint64_t w[G][NV];
     auto issue = [&]() {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        const int p = p0 + g;
-        const bool real = p < x.world && p != x.rank;  // uniform
+        const bool real = i0 + g < np;  // uniform
         const uint64_t PTDT_GLOBAL* src =
-            (const uint64_t PTDT_GLOBAL*)x.local + (int64_t)(parity * x.world + (real ? p : 0)) * x.max_elems + base;
+            (const uint64_t PTDT_GLOBAL*)x.local + (int64_t)(parity * x.world + (real ? peer(i0 + g) : 0)) * x.max_elems + base;
 #pragma unroll
         for (int k = 0; k < NV; ++k)
           w[g][k] = real ? __hip_atomic_load(src + k * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : hi;
@@ -166,12 +169,19 @@ __device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq,
     if (!ok) break;
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      const int p = p0 + g;
-      if (p >= x.world) break;
+      if (i0 + g >= np) break;
+      if (!own && peer(i0 + g) > x.rank) {
 #pragma unroll
-      for (int k = 0; k < NV; ++k) acc[k] += p == x.rank ? v[k] : __uint_as_float((uint32_t)w[g][k]);
+        for (int k = 0; k < NV; ++k) acc[k] += v[k];
+        own = true;
+      }
+#pragma unroll
+      for (int k = 0; k < NV; ++k) acc[k] += __uint_as_float((uint32_t)w[g][k]);
     }
   }
+  if (!own)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) acc[k] += v[k];
   const float inv = 1.f / (float)x.world;
 #pragma unroll
   for (int k = 0; k < NV; ++k) v[k] = acc[k] * inv;
