@@ -416,6 +416,32 @@ def spin_barrier_check(rank, world, port, out_dir):
     destroy_process_group()
 
 
+def spin_barrier_setup_failure(rank, world, port, out_dir, failing_rank):
+    """One rank cannot map the shared page: every rank gets None from spin_barrier.create (nobody is
+    left waiting in a collective), and no /dev/shm file is left behind."""
+    _init(rank, world, port)
+    from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+    from pytorch_distributed_training_tutorials_amd.utils import spin_barrier
+
+    os.environ["LOCAL_WORLD_SIZE"] = str(world)
+    c = comm_mod.get_default(None)
+    if rank == failing_rank:
+        real_mmap = spin_barrier.mmap.mmap
+
+        def broken(*a, **k):
+            raise OSError(28, "No space left on device (injected)")
+
+        spin_barrier.mmap.mmap = broken
+    bar = spin_barrier.create(c)
+    if rank == failing_rank:
+        spin_barrier.mmap.mmap = real_mmap
+    c.barrier()
+    left = [f for f in os.listdir("/dev/shm") if f.startswith(f"ptdt_spin_")]
+    torch.save({"none": bar is None, "left": left}, os.path.join(out_dir, f"r{rank}.pt"))
+    destroy_process_group()
+
+
 def tuning_agree(rank, world, port, out_dir):
     """Each rank 'times' a different winner; utils.tuning.agree hands every rank rank 0's."""
     _init(rank, world, port)

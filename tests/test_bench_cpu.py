@@ -85,3 +85,18 @@ def test_spin_barrier_releases_together(tmp_path):
         for r in res:
             assert r["leave"][rnd] >= arrive  # released only after the last arrival
         assert max(r["leave"][rnd] for r in res) - arrive < 0.05  # and promptly
+
+
+@pytest.mark.parametrize("failing_rank", [0, 2])
+def test_spin_barrier_setup_failure_is_collective(tmp_path, failing_rank):
+    """A rank that cannot create or map the shared page makes EVERY rank fall back to the collective
+    barrier (create returns None everywhere) instead of leaving the others blocked."""
+    import torch
+    from torch.multiprocessing import spawn
+
+    from tests import _workers
+
+    world = 3
+    spawn(_workers.spin_barrier_setup_failure, args=(world, free_port(), str(tmp_path), failing_rank), nprocs=world)
+    res = [torch.load(os.path.join(tmp_path, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    assert all(r["none"] for r in res)
