@@ -320,6 +320,9 @@ def run_persistent(args, rank, world, dev, comm):
             # entry -> position known, -> epoch list in LDS, -> past the barrier (waits forced in this pass)
             phase["prologue_split_us"] = [round(v[k] * 0.01 / nl, 2) for k in (11, 12, 13)]
         if which.startswith("tp"):  # each wave's barrier + logit-sum phase (load balance)
+            nl = math.ceil(args.steps / chunk)
+            # kernel entry -> lists/init done, -> past the barrier, -> step 0 staged (10 ns ticks, per launch)
+            phase["prologue_split_us"] = [round(v[k] * 0.01 / nl, 2) for k in (17, 18, 19)]
             nw = int(which.split(":")[1].split("w")[0])
             phase["logit_sum_per_wave"] = [round(x / args.steps, 1) for x in v[9:9 + nw]]
             phase["barrier_wait_per_wave"] = [round(x / args.steps, 1) for x in v[9 + nw:9 + 2 * nw]]

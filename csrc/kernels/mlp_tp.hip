@@ -218,6 +218,15 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   constexpr int LDX = St::LDX, LDXT = St::LDXT, LD2 = kTpLD2, LDT = kTpLDT;
   extern __shared__ float lds[];
   const TpDims d = tp_dims(a, pa);
+  // diagnostic (ST): kernel entry and three prologue marks (10 ns ticks; waits forced at each mark)
+  const int64_t r_entry = ST ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  int64_t r_pro[3] = {0, 0, 0};
+  auto pstamp = [&](int k) {
+    if constexpr (ST) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      r_pro[k] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    }
+  };
   const int tid = (int)threadIdx.x;
   const int T = (int)blockDim.x;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -359,15 +368,22 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     for (int e = e0 + 1; e <= e0 + 3; ++e) keys_store(e);
   // staged batch slots: zeros, and the constant-1 input column (b1 rides in W1's
   // column Din) in X and X^T; the per-step writes only touch columns < Din
-  const float one = hb ? 1.f : 0.f;
-  for (int e = tid; e < 3 * St::FLOATS; e += T) {
-    const int o = e % St::FLOATS;
-    float v = 0.f;
-    if (o < St::XT_OFF) v = (o % LDX) == Din ? one : 0.f;
-    else if (o < St::Y_OFF) v = ((o - St::XT_OFF) / LDXT == Din && (o - St::XT_OFF) % LDXT < 32) ? one : 0.f;
-    stage0[e] = v;
-  }
+  // (16-B zero stores, then the constant-1 entries after a barrier: the per-element index
+  // arithmetic of a one-pass fill cost ~1-2 us of every launch's prologue)
+  static_assert(St::FLOATS % 4 == 0, "float4 fill");
+  for (int e = tid; e < 3 * St::FLOATS / 4; e += T) reinterpret_cast<f4*>(stage0)[e] = f4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();
+  if (hb) {
+    for (int e = tid; e < 3 * 64; e += T) {  // per slot: X[row][Din] and X^T[Din][row], rows 0..31
+      float* const st = stage0 + (e >> 6) * St::FLOATS;
+      const int r = e & 31;
+      if ((e & 63) < 32) st[r * LDX + Din] = 1.f;
+      else st[St::XT_OFF + Din * LDXT + r] = 1.f;
+    }
+  }
+  pstamp(0);  // lists, keys, staging-slot init (and the compute waves' state loads) done
+  __syncthreads();
+  pstamp(1);
   if (tid == 0 && pa.idx == nullptr) list_cache_publish(lc, e0);
 
   // Helper wave (w == NW): owns the sampler lists and the batch staging, so the NW compute
@@ -497,6 +513,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     stage_write(0);
   }
   __syncthreads();
+  pstamp(2);  // step 0's batch staged: the loop starts
 
   const float inv_full = 1.f / (float)(LOSS == kLossMSE ? B * Dout : B);
   const int ce0 = e0, cj0 = j0;
@@ -881,6 +898,8 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       for (int k = 0; k < 7; ++k) pa.stamps[k] += acc_t[k];
       pa.stamps[7] += (int64_t)__builtin_amdgcn_s_memtime() - t_begin;
       pa.stamps[8] += (int64_t)__builtin_amdgcn_s_memrealtime() - r_begin;
+      if (pa.stamps_n >= 20)  // prologue marks relative to kernel entry: [17] lists/init [18] barrier [19] staged
+        for (int k = 0; k < 3; ++k) pa.stamps[17 + k] += r_pro[k] - r_entry;
     }
     if (a.opt_step) *a.opt_step = opt_step;
     if (AR) *a.ar.seq = seq;
