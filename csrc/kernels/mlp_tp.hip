@@ -364,8 +364,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     fp.n = (uint32_t)k[7];
     return fp;
   };
-  if (feistel && tid == 0)
-    for (int e = e0 + 1; e <= e0 + 3; ++e) keys_store(e);
+  if (feistel && (tid & 63) == 0 && (tid >> 6) < 3) keys_store(e0 + 1 + (tid >> 6));  // one epoch per wave, in parallel
   // staged batch slots: zeros, and the constant-1 input column (b1 rides in W1's
   // column Din) in X and X^T; the per-step writes only touch columns < Din
   // (16-B zero stores, then the constant-1 entries after a barrier: the per-element index
