@@ -97,6 +97,11 @@ def main(argv=None):
     y = torch.randint(0, 1000, (a.batch_size,), device=dev)
     amp = a.dtype == "bf16"
     mode = "off" if (a.no_graph or a.impl != "native") else a.graph
+    if mode == "auto" and world > 1 and os.environ.get("PTDT_GRAPH_MULTI", "0") != "1":
+        # RCCL collectives captured in a replayed step have only run at world 1 (RCCL refuses two
+        # ranks on one GPU, so no one-GPU rehearsal exists): the default stays eager across GPUs;
+        # --graph on or PTDT_GRAPH_MULTI=1 opts in
+        mode = "off"
     graphed = mode != "off"
     from pytorch_distributed_training_tutorials_amd.utils.graphs import GraphedStep
 
