@@ -894,8 +894,20 @@ int64_t graph_replace_memsets_(int64_t graph) {
 }
 
 // LLM.int8 decode (M <= 32): y = int8 product with outlier columns, two launches, no host sync
+// pre-shuffled weights for the decode GEMV (int8_decode.hip): [ceil(N / 16) * 16 * K] int8
+Tensor int8_decode_pack_(Tensor q) {
+  check_gpu(q, "weight_q");
+  TORCH_CHECK(q.dim() == 2 && q.scalar_type() == at::kChar && q.is_contiguous() && q.size(1) % 64 == 0,
+              "int8_decode_pack: contiguous int8 [N, K], K % 64 == 0");
+  c10::hip::HIPGuard guard(q.device().index());
+  const int N = (int)q.size(0), K = (int)q.size(1);
+  Tensor p = at::empty({(int64_t)int8_decode_packed_bytes(N, K)}, q.options());
+  hip_check(int8_decode_pack(q.data_ptr<int8_t>(), N, K, p.data_ptr<int8_t>(), cur_stream(q)), "int8_decode_pack");
+  return p;
+}
+
 Tensor int8_decode_(Tensor x, Tensor q, Tensor sw, c10::optional<Tensor> bias, double threshold,
-                    const std::string& out_dtype) {
+                    const std::string& out_dtype, c10::optional<Tensor> packed) {
   check_gpu(x, "x");
   check_gpu(q, "weight_q");
   TORCH_CHECK(x.dim() == 2 && q.dim() == 2 && q.scalar_type() == at::kChar && x.size(1) == q.size(1),
@@ -917,7 +929,14 @@ Tensor int8_decode_(Tensor x, Tensor q, Tensor sw, c10::optional<Tensor> bias, d
     x = x.contiguous().clone();  // the prep kernel reads 16-B chunks
   Tensor ws = at::empty({(int64_t)int8_decode_ws_bytes((int)M, (int)K)}, x.options().dtype(at::kByte));
   Tensor y = at::empty({M, N}, x.options().dtype(scalar_of(out_dtype)));
-  hip_check(int8_decode(x.data_ptr(), dt_of16(x), (int)M, (int)K, (float)threshold, q.data_ptr<int8_t>(),
+  const int8_t* wp = nullptr;
+  if (packed.has_value() && packed->defined()) {
+    TORCH_CHECK(packed->scalar_type() == at::kChar && packed->is_contiguous() && packed->is_cuda() &&
+                    packed->numel() == (int64_t)int8_decode_packed_bytes((int)N, (int)K),
+                "int8_decode: packed weights from int8_decode_pack");
+    wp = packed->data_ptr<int8_t>();
+  }
+  hip_check(int8_decode(x.data_ptr(), dt_of16(x), (int)M, (int)K, (float)threshold, q.data_ptr<int8_t>(), wp,
                         sw.data_ptr<float>(), bp, bias_dt, (int)N, y.data_ptr(), dt_of16(y), ws.data_ptr(),
                         cur_stream(x)),
             "int8_decode");
@@ -1482,7 +1501,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("graph_node_census", &graph_node_census_, "node count and per-hipGraphNodeType counts of a raw hipGraph_t");
   m.def("memset_async_", &memset_async_, "hipMemsetAsync of a whole tensor (tests of the graph memset rewrite)");
   m.def("graph_replace_memsets", &graph_replace_memsets_, "replace a raw hipGraph_t's memset nodes by fill-kernel nodes");
-  m.def("int8_decode", &int8_decode_, "LLM.int8 decode path (M <= 32): outliers + quantise + int8 GEMV, no host sync");
+  m.def("int8_decode", &int8_decode_, "LLM.int8 decode path (M <= 32): outliers + quantise + int8 GEMV, no host sync",
+        py::arg("x"), py::arg("q"), py::arg("sw"), py::arg("bias"), py::arg("threshold"), py::arg("out_dtype"),
+        py::arg("packed") = py::none());
+  m.def("int8_decode_pack", &int8_decode_pack_, "pre-shuffled int8 weights for the decode GEMV");
   m.def("int8_decode_supported", &int8_decode_supported);
   m.def("sum_all", &sum_all_);
   m.def("philox_", &philox_);

@@ -179,12 +179,16 @@ __global__ void __launch_bounds__(256) i8_decode_quant_kernel(const T* __restric
 
 // MT: 16-row M tiles (Mp = 16 MT). K % 64 == 0. NWV waves split K (8 when there are too few
 // 16-feature workgroups to fill the chip with 4). nsb: stats workgroups (outlier lists).
-template <typename T, int MT, int NWV>
+// PACKED: the weights come pre-shuffled (i8_decode_pack_kernel) -- each wave's load of one K step is
+// one contiguous KiB -- instead of 16 rows x 64 B out of the row-major [N, K]; the outlier columns
+// still read the row-major copy.
+template <typename T, int MT, int NWV, bool PACKED>
 __global__ void __launch_bounds__(64 * NWV) i8_decode_gemv_kernel(const T* __restrict__ x, const int8_t* __restrict__ xq,
                                                                   const float* __restrict__ sx,
                                                                   const int* __restrict__ ocnt,
                                                                   const int* __restrict__ olist, int nsb,
                                                                   const int8_t* __restrict__ W,
+                                                                  const int8_t* __restrict__ Wp,
                                                                   const float* __restrict__ sw, const void* bias,
                                                                   int bias_dtype, void* y, int y_dtype, int M, int N,
                                                                   int K) {
@@ -198,7 +202,7 @@ __global__ void __launch_bounds__(64 * NWV) i8_decode_gemv_kernel(const T* __res
   const int nr = n < N ? n : N - 1;  // edge rows load a real row, never store
   const int nk = K >> 6;
   const int s0 = (w * nk) / NWV, s1 = ((w + 1) * nk) / NWV;
-  const int8_t* const wp = W + (int64_t)nr * K + 16 * g;
+  const int8_t* const wp = PACKED ? Wp + ((int64_t)blockIdx.x * nk * 64 + lane) * 16 : W + (int64_t)nr * K + 16 * g;
   const int8_t* xp[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) xp[i] = xq + (int64_t)(16 * i + c) * K + 16 * g;
@@ -210,7 +214,7 @@ __global__ void __launch_bounds__(64 * NWV) i8_decode_gemv_kernel(const T* __res
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int k = (s + u < s1 ? s + u : s1 - 1) << 6;  // clamped tail re-reads a real step, unused
-      b[u] = PTDT_I8_WLOAD(reinterpret_cast<const i32x4*>(wp + k));
+      b[u] = PTDT_I8_WLOAD(reinterpret_cast<const i32x4*>(wp + (PACKED ? (int64_t)k * 16 : (int64_t)k)));
 #pragma unroll
       for (int i = 0; i < MT; ++i) a[u][i] = *reinterpret_cast<const i32x4*>(xp[i] + k);
     }
@@ -265,6 +269,23 @@ __global__ void __launch_bounds__(64 * NWV) i8_decode_gemv_kernel(const T* __res
     }
 }
 
+// Pre-shuffle for the GEMV: Wp[tile][step][lane] = the 16 bytes lane (c, g) = (lane & 15, lane >> 4) of
+// 16-feature tile `tile` loads at K step `step`: W[16 tile + c][64 step + 16 g ..] (rows past N repeat
+// row N - 1, never stored). One thread per 16 B.
+__global__ void __launch_bounds__(256) i8_decode_pack_kernel(const int8_t* __restrict__ W, int N, int K,
+                                                             int8_t* __restrict__ Wp, int64_t chunks) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= chunks) return;
+  const int nk = K >> 6;
+  const int lane = (int)(i & 63);
+  const int64_t blk = i >> 6;
+  const int step = (int)(blk % nk);
+  const int64_t tile = blk / nk;
+  const int64_t n = min<int64_t>(tile * 16 + (lane & 15), N - 1);
+  *reinterpret_cast<i32x4*>(Wp + i * 16) =
+      *reinterpret_cast<const i32x4*>(W + n * K + 64 * step + 16 * (lane >> 4));
+}
+
 int stats_blocks(int K) { return ((K >> 3) + kStatChunks - 1) / kStatChunks; }
 
 // workspace: xq [Mp][K] int8 | sx [32] f32 | cbits [K/8] (16-B padded) | rowpart [nsb][32] f32 | ocnt [nsb] |
@@ -306,8 +327,8 @@ Ws carve(void* base, int M, int K) {
 }
 
 template <typename T>
-hipError_t launch_t(const void* xv, int M, int K, float thr, const int8_t* W, const float* sw, const void* bias,
-                    int bias_dtype, int N, void* y, int y_dtype, const Ws& ws, hipStream_t s) {
+hipError_t launch_t(const void* xv, int M, int K, float thr, const int8_t* W, const int8_t* Wp, const float* sw,
+                    const void* bias, int bias_dtype, int N, void* y, int y_dtype, const Ws& ws, hipStream_t s) {
   const T* x = static_cast<const T*>(xv);
   const int nsb = stats_blocks(K), Mp = M <= 16 ? 16 : 32;
   hipLaunchKernelGGL(i8_decode_stats_kernel<T>, dim3(nsb), dim3(256), 0, s, x, M, K, thr, ws.cbits, ws.rowpart,
@@ -318,15 +339,23 @@ hipError_t launch_t(const void* xv, int M, int K, float thr, const int8_t* W, co
   PTDT_HIP_CHECK(hipGetLastError());
   const dim3 grid((unsigned)((N + 15) / 16));
   const bool wide = (N + 15) / 16 < 512;  // < 2 workgroups per CU: 8 waves each
-#define PTDT_I8G(mt, nw)                                                                                          \
-  hipLaunchKernelGGL((i8_decode_gemv_kernel<T, mt, nw>), grid, dim3(64 * nw), 0, s, x, ws.xq, ws.sx, ws.ocnt, ws.olist, \
-                     nsb, W, sw, bias, bias_dtype, y, y_dtype, M, N, K)
-  if (Mp == 16) {
-    if (wide) PTDT_I8G(1, 8);
-    else PTDT_I8G(1, 4);
+#define PTDT_I8G(mt, nw, pk)                                                                                      \
+  hipLaunchKernelGGL((i8_decode_gemv_kernel<T, mt, nw, pk>), grid, dim3(64 * nw), 0, s, x, ws.xq, ws.sx, ws.ocnt,      \
+                     ws.olist, nsb, W, Wp, sw, bias, bias_dtype, y, y_dtype, M, N, K)
+  if (Wp) {
+    if (Mp == 16) {
+      if (wide) PTDT_I8G(1, 8, true);
+      else PTDT_I8G(1, 4, true);
+    } else {
+      if (wide) PTDT_I8G(2, 8, true);
+      else PTDT_I8G(2, 4, true);
+    }
+  } else if (Mp == 16) {
+    if (wide) PTDT_I8G(1, 8, false);
+    else PTDT_I8G(1, 4, false);
   } else {
-    if (wide) PTDT_I8G(2, 8);
-    else PTDT_I8G(2, 4);
+    if (wide) PTDT_I8G(2, 8, false);
+    else PTDT_I8G(2, 4, false);
   }
 #undef PTDT_I8G
   return hipGetLastError();
@@ -340,17 +369,29 @@ bool int8_decode_supported(int M, int N, int K) {
   return M >= 1 && M <= 32 && N >= 1 && K >= 64 && K % 64 == 0 && K <= kInt8DecodeMaxK;
 }
 
-hipError_t int8_decode(const void* x, int x_dtype, int M, int K, float threshold, const int8_t* W, const float* sw,
-                       const void* bias, int bias_dtype, int N, void* y, int y_dtype, void* ws, hipStream_t s) {
+size_t int8_decode_packed_bytes(int N, int K) { return (size_t)((N + 15) / 16) * 16 * (size_t)K; }
+
+hipError_t int8_decode_pack(const int8_t* W, int N, int K, int8_t* Wp, hipStream_t s) {
+  if (N < 1 || K < 64 || K % 64 != 0 || (reinterpret_cast<uintptr_t>(W) & 15) || (reinterpret_cast<uintptr_t>(Wp) & 15))
+    return hipErrorInvalidValue;
+  const int64_t chunks = (int64_t)int8_decode_packed_bytes(N, K) / 16;
+  hipLaunchKernelGGL(i8_decode_pack_kernel, dim3((unsigned)((chunks + 255) / 256)), dim3(256), 0, s, W, N, K, Wp, chunks);
+  return hipGetLastError();
+}
+
+hipError_t int8_decode(const void* x, int x_dtype, int M, int K, float threshold, const int8_t* W, const int8_t* Wp,
+                       const float* sw, const void* bias, int bias_dtype, int N, void* y, int y_dtype, void* ws,
+                       hipStream_t s) {
   if (!int8_decode_supported(M, N, K)) return hipErrorInvalidValue;
-  if ((reinterpret_cast<uintptr_t>(W) & 15) || (reinterpret_cast<uintptr_t>(ws) & 15) ||
+  if ((reinterpret_cast<uintptr_t>(W) & 15) || (reinterpret_cast<uintptr_t>(Wp) & 15) ||
+      (reinterpret_cast<uintptr_t>(ws) & 15) ||
       (reinterpret_cast<uintptr_t>(x) & 15))
     return hipErrorInvalidValue;
   const Ws w = carve(ws, M, K);
   if (x_dtype == kF32)
-    return launch_t<float>(x, M, K, threshold, W, sw, bias, bias_dtype, N, y, y_dtype, w, s);
-  if (x_dtype == kF16) return launch_t<_Float16>(x, M, K, threshold, W, sw, bias, bias_dtype, N, y, y_dtype, w, s);
-  return launch_t<uint16_t>(x, M, K, threshold, W, sw, bias, bias_dtype, N, y, y_dtype, w, s);
+    return launch_t<float>(x, M, K, threshold, W, Wp, sw, bias, bias_dtype, N, y, y_dtype, w, s);
+  if (x_dtype == kF16) return launch_t<_Float16>(x, M, K, threshold, W, Wp, sw, bias, bias_dtype, N, y, y_dtype, w, s);
+  return launch_t<uint16_t>(x, M, K, threshold, W, Wp, sw, bias, bias_dtype, N, y, y_dtype, w, s);
 }
 
 }  // namespace ptdt

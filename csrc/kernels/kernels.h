@@ -320,8 +320,13 @@ int graph_replace_memsets(void* graph);
 constexpr int kInt8DecodeMaxK = 16384;
 size_t int8_decode_ws_bytes(int M, int K);
 bool int8_decode_supported(int M, int N, int K);
-hipError_t int8_decode(const void* x, int x_dtype, int M, int K, float threshold, const int8_t* W, const float* sw,
-                       const void* bias, int bias_dtype, int N, void* y, int y_dtype, void* ws, hipStream_t s);
+// Wp: optional pre-shuffled copy of W (int8_decode_pack, int8_decode_packed_bytes(N, K) bytes) for
+// contiguous weight loads in the GEMV; nullptr reads the row-major W.
+hipError_t int8_decode(const void* x, int x_dtype, int M, int K, float threshold, const int8_t* W, const int8_t* Wp,
+                       const float* sw, const void* bias, int bias_dtype, int N, void* y, int y_dtype, void* ws,
+                       hipStream_t s);
+size_t int8_decode_packed_bytes(int N, int K);
+hipError_t int8_decode_pack(const int8_t* W, int N, int K, int8_t* Wp, hipStream_t s);
 
 // BatchNorm(train stats applied) + ReLU fused epilogue over NCHW (csrc/kernels/elementwise.hip)
 hipError_t bn_relu_apply(const void* x, int dtype, const float* scale, const float* shift, int64_t N,

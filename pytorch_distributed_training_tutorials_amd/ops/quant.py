@@ -32,6 +32,8 @@ from .._ext import native, use_native
 _NATIVE_DTYPES = (torch.float32, torch.bfloat16, torch.float16)
 _DECODE = __import__("os").environ.get("PTDT_INT8_DECODE", "1") != "0"  # 0: decode shapes take the GEMM path
 _DTYPE_NAME = {torch.float32: "float32", torch.bfloat16: "bfloat16", torch.float16: "float16"}
+# 0: the decode GEMV reads the row-major int8 weights instead of a pre-shuffled copy (A/B)
+_PACKED = __import__("os").environ.get("PTDT_I8_PACKED", "1") != "0"
 
 
 def quantize_rowwise(w: torch.Tensor):
@@ -93,6 +95,16 @@ class Int8Linear(nn.Module):
     def dequantized_weight(self) -> torch.Tensor:
         return self.weight_q.float() * self.weight_scale[:, None]
 
+    def _decode_packed(self, C):
+        """The decode GEMV's pre-shuffled copy of ``weight_q`` (one contiguous KiB per wave load),
+        rebuilt when the weights change (storage or in-place version)."""
+        key = (self.weight_q.data_ptr(), self.weight_q._version)
+        cache = getattr(self, "_packed_cache", None)
+        if cache is None or cache[0] != key:
+            cache = (key, C.int8_decode_pack(self.weight_q))
+            self._packed_cache = cache
+        return cache[1]
+
     def _llm_int8(self, x2: torch.Tensor) -> torch.Tensor:
         b = self.bias
         if not use_native(x2) or x2.dtype not in _NATIVE_DTYPES or self.in_features % 16 != 0:
@@ -104,7 +116,8 @@ class Int8Linear(nn.Module):
         if _DECODE and C.int8_decode_supported(x2.shape[0], self.out_features, self.in_features):
             # decode shapes (<= 32 tokens): outliers, quantisation and the int8 GEMV with the outlier
             # columns fused, two launches, no host read (csrc/kernels/int8_decode.hip)
-            return C.int8_decode(x2, self.weight_q, self.weight_scale, b, self.threshold, _DTYPE_NAME[x2.dtype])
+            return C.int8_decode(x2, self.weight_q, self.weight_scale, b, self.threshold, _DTYPE_NAME[x2.dtype],
+                                 self._decode_packed(C) if _PACKED else None)
         mask = C.int8_col_outliers(x2, self.threshold)
         cols = mask.nonzero().flatten()  # host read: usually a handful of features
         xq, sx = C.int8_quant_rows(x2, mask if cols.numel() else None)

@@ -192,3 +192,35 @@ def test_llm_int8_decode_many_outliers_across_workgroups(dev, M):
     y = m(x)
     ref = llm_int8_reference(x, m.weight_q, m.weight_scale, m.bias, m.threshold)
     torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_llm_int8_decode_packed_weights(dev):
+    """The decode GEMV's pre-shuffled weight copy (int8_decode_pack): its layout (tile, K step, lane)
+    against a PyTorch re-arrangement, the packed and row-major GEMVs bit-identical (same int32
+    products in the same order), and the cache rebuilt after an in-place weight update."""
+    from pytorch_distributed_training_tutorials_amd import native
+    from pytorch_distributed_training_tutorials_amd.ops.quant import Int8Linear, llm_int8_reference
+
+    C = native()
+    torch.manual_seed(11)
+    N, K = 37, 192
+    q = torch.randint(-127, 128, (N, K), device=dev, dtype=torch.int8)
+    p = C.int8_decode_pack(q)
+    tiles = (N + 15) // 16
+    rows = torch.clamp(torch.arange(tiles * 16, device=dev), max=N - 1)
+    qq = q[rows].view(tiles, 16, K // 64, 4, 16)  # [tile, c, step, g, byte]
+    want = qq.permute(0, 2, 3, 1, 4).reshape(-1)  # [tile, step, lane = 16 g + c, byte]
+    assert torch.equal(p, want)
+    lin = torch.nn.Linear(K, N, device=dev, dtype=torch.bfloat16)
+    m = Int8Linear.from_linear(lin, llm_int8=True)
+    x = torch.randn(9, K, device=dev, dtype=torch.bfloat16)
+    x[2, 70] = 30.0
+    a = C.int8_decode(x, m.weight_q, m.weight_scale, m.bias, m.threshold, "bfloat16", C.int8_decode_pack(m.weight_q))
+    b = C.int8_decode(x, m.weight_q, m.weight_scale, m.bias, m.threshold, "bfloat16", None)
+    assert torch.equal(a, b)
+    m(x)
+    m.weight_q.mul_(-1)
+    y = m(x)
+    torch.testing.assert_close(y, llm_int8_reference(x, m.weight_q, m.weight_scale, m.bias, m.threshold),
+                               rtol=1e-2, atol=1e-2)
