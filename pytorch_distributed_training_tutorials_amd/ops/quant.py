@@ -24,6 +24,8 @@ launches, no host read.) fp32, bf16 and fp16 activations run natively
 """
 from __future__ import annotations
 
+import weakref
+
 import torch
 import torch.nn as nn
 
@@ -97,13 +99,14 @@ class Int8Linear(nn.Module):
 
     def _decode_packed(self, C):
         """The decode GEMV's pre-shuffled copy of ``weight_q`` (one contiguous KiB per wave load),
-        rebuilt when the weights change (storage or in-place version)."""
-        key = (self.weight_q.data_ptr(), self.weight_q._version)
+        rebuilt when the weights change: another tensor (a weak reference, so a recycled address
+        cannot alias) or an in-place update (version counter)."""
+        w = self.weight_q
         cache = getattr(self, "_packed_cache", None)
-        if cache is None or cache[0] != key:
-            cache = (key, C.int8_decode_pack(self.weight_q))
+        if cache is None or cache[0]() is not w or cache[1] != w._version:
+            cache = (weakref.ref(w), w._version, C.int8_decode_pack(w))
             self._packed_cache = cache
-        return cache[1]
+        return cache[2]
 
     def _llm_int8(self, x2: torch.Tensor) -> torch.Tensor:
         b = self.bias

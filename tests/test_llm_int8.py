@@ -224,3 +224,27 @@ def test_llm_int8_decode_packed_weights(dev):
     y = m(x)
     torch.testing.assert_close(y, llm_int8_reference(x, m.weight_q, m.weight_scale, m.bias, m.threshold),
                                rtol=1e-2, atol=1e-2)
+
+
+def test_decode_packed_cache_tracks_weight_identity_and_version():
+    """The pre-shuffled weight cache (Int8Linear._decode_packed) is rebuilt after an in-place weight
+    update and after the buffer is replaced by another tensor, and reused otherwise (CPU: a stub
+    packer stands in for the native one)."""
+    from pytorch_distributed_training_tutorials_amd.ops.quant import Int8Linear
+
+    calls = []
+
+    class Packer:
+        def int8_decode_pack(self, w):
+            calls.append(1)
+            return w.clone()
+
+    m, C = Int8Linear(64, 16), Packer()
+    p = m._decode_packed(C)
+    assert m._decode_packed(C) is p and len(calls) == 1
+    m.weight_q.add_(1)
+    m._decode_packed(C)
+    assert len(calls) == 2
+    m.weight_q = torch.zeros(16, 64, dtype=torch.int8)
+    m._decode_packed(C)
+    assert len(calls) == 3
