@@ -6,7 +6,7 @@
 //                    rows: ONE round of 16-B loads; column absmax -> outlier bits (|x| > threshold)
 //                    per chunk, the workgroup's outlier columns in column order, and per row the
 //                    absmax over its non-outlier columns (a per-workgroup partial).
-//   i8_decode_quant  same partition: the row scales (max over the stats partials, fixed order) and x
+//   i8_decode_quant  same columns x Mp / 8 row groups: the row scales (max over the stats partials, fixed order) and x
 //                    quantised to int8 (rint(x / s) with a true division, outlier columns 0, padding
 //                    rows M..Mp-1 0).
 //   i8_decode_gemv   one workgroup per 16 output features, 4 or 8 waves splitting K: each lane streams
@@ -131,8 +131,10 @@ __device__ __forceinline__ void store_val(void* p, int dtype, int64_t i, float v
   else static_cast<uint16_t*>(p)[i] = f32_to_bf16(v);
 }
 
-// grid: as the stats kernel. Row scales from the stats partials (all loads in one round), then this
-// workgroup's 8-column chunks of every row quantised (8 int8 per store); workgroup 0 publishes sx.
+// grid: (stats workgroups, Mp / 8 row groups). Row scales from the stats partials (all loads in one
+// round), then this workgroup's 8-column chunks of its 8 rows quantised, 2 rows per thread (8 int8
+// per store); workgroup (0, 0) publishes sx. The IEEE divisions are dependent instruction chains:
+// spreading the rows over Mp / 8 times more workgroups shortens each wave's chain 4x.
 template <typename T>
 __global__ void __launch_bounds__(256) i8_decode_quant_kernel(const T* __restrict__ x, int M, int Mp, int K, int nsb,
                                                               const uint8_t* __restrict__ cbits,
@@ -140,29 +142,29 @@ __global__ void __launch_bounds__(256) i8_decode_quant_kernel(const T* __restric
                                                               int8_t* __restrict__ xq, float* __restrict__ sx) {
   __shared__ float part[32 * 32];
   __shared__ float ssc[32];
-  const int tid = threadIdx.x, lane = tid & 63, rg = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, sub = tid >> 6;
   const int nch = K >> 3;
   const int c = blockIdx.x * kStatChunks + lane;
   const bool cv = c < nch;
   const int cc = cv ? c : nch - 1;
-  const int m0 = 8 * rg;
+  const int m0 = 8 * blockIdx.y + 2 * sub;
   for (int i = tid; i < nsb * 32; i += 256) part[i] = rowpart[i];
   const uint32_t ob = cbits[cc];
-  float v[8][8];
+  float v[2][8];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) load8(x + (int64_t)(m0 + u < M ? m0 + u : M - 1) * K + 8 * cc, v[u]);
+  for (int u = 0; u < 2; ++u) load8(x + (int64_t)(m0 + u < M ? m0 + u : M - 1) * K + 8 * cc, v[u]);
   __syncthreads();
   if (tid < 32) {
     float a = 0.f;
     for (int b = 0; b < nsb; ++b) a = fmaxf(a, part[b * 32 + tid]);  // exact: order-free
     const float sc = a > 0.f ? a / 127.f : 1.f;
     ssc[tid] = sc;
-    if (blockIdx.x == 0 && tid < Mp) sx[tid] = tid < M ? sc : 1.f;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid < Mp) sx[tid] = tid < M ? sc : 1.f;
   }
   __syncthreads();
   if (!cv) return;
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
+  for (int u = 0; u < 2; ++u) {
     const int m = m0 + u;
     if (m >= Mp) break;
     const float sc = ssc[m < M ? m : 0];  // x / s (IEEE division, as the reference), not x * (1 / s)
@@ -334,8 +336,8 @@ hipError_t launch_t(const void* xv, int M, int K, float thr, const int8_t* W, co
   hipLaunchKernelGGL(i8_decode_stats_kernel<T>, dim3(nsb), dim3(256), 0, s, x, M, K, thr, ws.cbits, ws.rowpart,
                      ws.ocnt, ws.olist);
   PTDT_HIP_CHECK(hipGetLastError());
-  hipLaunchKernelGGL(i8_decode_quant_kernel<T>, dim3(nsb), dim3(256), 0, s, x, M, Mp, K, nsb, ws.cbits, ws.rowpart,
-                     ws.xq, ws.sx);
+  hipLaunchKernelGGL(i8_decode_quant_kernel<T>, dim3(nsb, Mp / 8), dim3(256), 0, s, x, M, Mp, K, nsb, ws.cbits,
+                     ws.rowpart, ws.xq, ws.sx);
   PTDT_HIP_CHECK(hipGetLastError());
   const dim3 grid((unsigned)((N + 15) / 16));
   const bool wide = (N + 15) / 16 < 512;  // < 2 workgroups per CU: 8 waves each
