@@ -8,7 +8,7 @@
 //                    absmax over its non-outlier columns (a per-workgroup partial).
 //   i8_decode_quant  same columns x Mp / 8 row groups: the row scales (max over the stats partials, fixed order) and x
 //                    quantised to int8 (rint(x / s) with a true division, outlier columns 0, padding
-//                    rows M..Mp-1 0).
+//                    rows M..Mp-1 0), stored in the GEMV's MFMA operand order (1 KiB per K step).
 //   i8_decode_gemv   one workgroup per 16 output features, 4 or 8 waves splitting K: each lane streams
 //                    16 weight bytes per 64-deep K step (plain loads -- non-temporal ones measured 7-15 % slower -- 8 steps in flight) into
 //                    v_mfma_i32_16x16x64_i8 against the quantised rows (L2-resident); exact int32
@@ -175,7 +175,11 @@ __global__ void __launch_bounds__(256) i8_decode_quant_kernel(const T* __restric
       q = fminf(fmaxf(q, -127.f), 127.f);
       w[e >> 2] |= ((uint32_t)(int32_t)q & 0xffu) << (8 * (e & 3));
     }
-    *reinterpret_cast<uint2*>(xq + (int64_t)m * K + 8 * c) = make_uint2(w[0], w[1]);
+    // MFMA operand order (as the packed weights): 16-row tile m / 16, K step, lane (m % 16, g), byte
+    const int kk = 8 * c;
+    const int64_t off = (((int64_t)(m >> 4) * (K >> 6) + (kk >> 6)) * 64 + ((kk & 63) >> 4) * 16 + (m & 15)) * 16 +
+                        (kk & 15);
+    *reinterpret_cast<uint2*>(xq + off) = make_uint2(w[0], w[1]);
   }
 }
 
@@ -207,7 +211,7 @@ __global__ void __launch_bounds__(64 * NWV) i8_decode_gemv_kernel(const T* __res
   const int8_t* const wp = PACKED ? Wp + ((int64_t)blockIdx.x * nk * 64 + lane) * 16 : W + (int64_t)nr * K + 16 * g;
   const int8_t* xp[MT];
 #pragma unroll
-  for (int i = 0; i < MT; ++i) xp[i] = xq + (int64_t)(16 * i + c) * K + 16 * g;
+  for (int i = 0; i < MT; ++i) xp[i] = xq + ((int64_t)i * nk * 64 + lane) * 16;  // operand order: 1 KiB per step
   i32x4 acc[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i] = i32x4{0, 0, 0, 0};
@@ -218,7 +222,7 @@ __global__ void __launch_bounds__(64 * NWV) i8_decode_gemv_kernel(const T* __res
       const int k = (s + u < s1 ? s + u : s1 - 1) << 6;  // clamped tail re-reads a real step, unused
       b[u] = PTDT_I8_WLOAD(reinterpret_cast<const i32x4*>(wp + (PACKED ? (int64_t)k * 16 : (int64_t)k)));
 #pragma unroll
-      for (int i = 0; i < MT; ++i) a[u][i] = *reinterpret_cast<const i32x4*>(xp[i] + k);
+      for (int i = 0; i < MT; ++i) a[u][i] = *reinterpret_cast<const i32x4*>(xp[i] + (int64_t)k * 16);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
