@@ -6,23 +6,26 @@
 //                    rows: ONE round of 16-B loads; column absmax -> outlier bits (|x| > threshold)
 //                    per chunk, the workgroup's outlier columns in column order, and per row the
 //                    absmax over its non-outlier columns (a per-workgroup partial).
-//   i8_decode_quant  same columns x Mp / 8 row groups: the row scales (max over the stats partials, fixed order) and x
-//                    quantised to int8 (rint(x / s) with a true division, outlier columns 0, padding
-//                    rows M..Mp-1 0), stored in the GEMV's MFMA operand order (1 KiB per K step).
+//   i8_decode_quant  same columns x Mp / 8 row-group workgroups: the row scales (max over the stats
+//                    partials, fixed order) and x quantised to int8 (rint(x / s) with a true division,
+//                    outlier columns 0, padding rows M..Mp-1 0), stored in the GEMV's MFMA operand
+//                    order (1 KiB per 16-row tile and K step).
 //   i8_decode_gemv   one workgroup per 16 output features, 4 or 8 waves splitting K: each lane streams
-//                    16 weight bytes per 64-deep K step (plain loads -- non-temporal ones measured 7-15 % slower -- 8 steps in flight) into
-//                    v_mfma_i32_16x16x64_i8 against the quantised rows (L2-resident); exact int32
-//                    partials meet in LDS in wave order; the epilogue dequantises and adds the
-//                    outlier columns' fp32 products (x[:, o] * q[n, o] * sw[n], in column order) and
-//                    the bias.
+//                    16 weight bytes per 64-deep K step (plain loads -- non-temporal ones measured
+//                    7-15 % slower -- 8 steps in flight) into v_mfma_i32_16x16x64_i8 against the
+//                    quantised rows (L2-resident); with the pre-shuffled weights (i8_decode_pack) both
+//                    operands of a step are one contiguous KiB per wave. Exact int32 partials meet in
+//                    LDS in wave order; the epilogue dequantises and adds the outlier columns' fp32
+//                    products (x[:, o] * q[n, o] * sw[n], in column order) and the bias.
 //
 // At decode shapes the product is a weight stream (Llama-7B MLP up-projection: 11008 x 4096
 // int8 = 45 MB, 1 byte per weight where fp16 reads 2). Round 3 (separate outlier / quantise kernels,
 // a host read of the outlier mask, a gathered fp32 matmul, the tiled int8 GEMM): 80 us at M = 16
-// against 20 us for torch's fp16 GEMV. Round 4's first two-launch version ran the statistics and
-// the quantisation in ONE workgroup: 12-36 us of dependent load rounds before the GEMV started
-// (profiles/r4_int8_decode_kernels.md); quantising on the fly inside the GEMV instead repeated the
-// work in every one of its workgroups (GEMV 16 -> 28 us).
+// against 20 us for torch's fp16 GEMV; round 4: 17.3-18.0 us (profiles/r4_int8_decode_xq_ab.jsonl).
+// Measured and dropped: the statistics and quantisation in ONE workgroup (12-36 us of dependent load
+// rounds), quantising on the fly inside the GEMV (the work repeated in every workgroup: GEMV
+// 16 -> 28 us), one launch with a cross-workgroup wait (12.4 us) or with every workgroup recomputing
+// all column maxima (24 us).
 #include "common.h"
 #include "kernels.h"
 
