@@ -516,9 +516,9 @@ def _timed(comm, dev, fn, label: str = "headline"):
     us), then every rank reads CLOCK_MONOTONIC (one clock per node), runs ``fn``, syncs and reads
     it again. The per-rank stamps are gathered afterwards: ``start_skew_us`` = max - min of the
     start stamps, ``window_us`` = last end - first start (the whole-node wall window)."""
-    comm.barrier()
+    spin = _spin(comm)  # resolved BEFORE the barrier: its first call imports a module (~0.4 ms), and a GPU
+    comm.barrier()      # left idle that long adds ~8-13 us to the next launch (profiles/r5_driver_timeline.md)
     _sync(dev)
-    spin = _spin(comm)
     if spin is not None:
         spin.wait()
     m0 = time.clock_gettime_ns(time.CLOCK_MONOTONIC)

@@ -5,6 +5,8 @@
 // before launching (a bad launch on MI355X can reset the whole node) and
 // launches on the caller's current HIP stream, so all of them are capturable
 // into hipGraphs via torch.cuda.graph.
+#include <time.h>
+
 #include <map>
 #include <mutex>
 #include <utility>
@@ -286,6 +288,12 @@ void fused_mlp_persistent_py(Tensor X, c10::optional<Tensor> Yf, c10::optional<T
 // kernel chosen, LDS attribute set, tensors kept alive. launch(n) is a bare
 // hipLaunchKernel on the caller's current stream -- the short-run fixed cost
 // (bench --steps 20, one launch per Trainer.train) is the kernel, not the host.
+int64_t mono_ns() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (int64_t)t.tv_sec * 1000000000 + t.tv_nsec;
+}
+
 class PersistentPlan {
  public:
   PersistentPlan(Tensor X, c10::optional<Tensor> Yf, c10::optional<Tensor> Yi, Tensor P, Tensor G,
@@ -333,6 +341,62 @@ class PersistentPlan {
     launch_impl(n, pos, (int)(pos / S), (int)(pos % S));
   }
   int64_t capacity() const { return capacity_; }
+  ~PersistentPlan() {
+    if (ev_) hipEventDestroy(ev_);
+  }
+  // launch timeline probe (tools/driver_timeline.py): the engine stamps its realtime counter
+  // into tl[0..3] (a device or host-mapped int64 address; 0 turns it off)
+  void set_timeline(int64_t addr) { L_.p.tl = reinterpret_cast<int64_t*>(addr); }
+  // CLOCK_MONOTONIC ns right before / after the last hipLaunchKernel of this plan
+  std::vector<int64_t> last_launch_ns() const { return {L_.host_ns[0], L_.host_ns[1]}; }
+  // Timeline probe: launch n steps at pos and wait for them with one of the runtime's completion
+  // paths, all in C++ (mode 0 hipDeviceSynchronize, 1 hipStreamSynchronize, 2 hipEventRecord +
+  // hipEventSynchronize, 3 hipExtLaunchKernel with a stop event + hipEventSynchronize, 4 spin on
+  // hipStreamQuery, 5 hipExtLaunchKernel with a stop event + spin on hipEventQuery). Returns
+  // CLOCK_MONOTONIC ns [before the launch call, after it, when the wait returned].
+  std::vector<int64_t> launch_wait_at(int64_t n, int64_t pos, int64_t mode) {
+    TORCH_CHECK(n > 0 && n <= capacity_ && pos >= 0, "launch_wait_at: bad n / pos");
+    TORCH_CHECK(mode >= 0 && mode <= 5, "launch_wait_at: mode 0..5");
+    const int64_t S = steps_per_epoch_;
+    c10::hip::HIPGuard guard(dev_);
+    hipStream_t st = c10::hip::getCurrentHIPStream(dev_).stream();
+    if (ev_ == nullptr) hip_check(hipEventCreate(&ev_), "hipEventCreate");
+    const int64_t t0 = mono_ns();
+    if (mode == 3 || mode == 5) {
+      L_.p.n_steps = (int)n;
+      L_.p.cursor_host_pos = -1;
+      L_.p.has_start = 1;
+      L_.p.start_e = (int)(pos / S);
+      L_.p.start_j = (int)(pos % S);
+      void* args[] = {&L_.a, &L_.p};
+      hip_check(hipExtLaunchKernel(L_.fn, dim3(1), dim3(L_.threads), args, L_.lds, st, nullptr, ev_, 0),
+                "hipExtLaunchKernel");
+    } else {
+      launch_impl(n, pos, (int)(pos / S), (int)(pos % S));
+      if (mode == 2) hip_check(hipEventRecord(ev_, st), "hipEventRecord");
+    }
+    const int64_t t1 = mono_ns();
+    switch (mode) {
+      case 0: hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize"); break;
+      case 1: hip_check(hipStreamSynchronize(st), "hipStreamSynchronize"); break;
+      case 2:
+      case 3: hip_check(hipEventSynchronize(ev_), "hipEventSynchronize"); break;
+      case 4: {
+        hipError_t e;
+        while ((e = hipStreamQuery(st)) == hipErrorNotReady) {
+        }
+        hip_check(e, "hipStreamQuery");
+        break;
+      }
+      default: {
+        hipError_t e;
+        while ((e = hipEventQuery(ev_)) == hipErrorNotReady) {
+        }
+        hip_check(e, "hipEventQuery");
+      }
+    }
+    return {t0, t1, mono_ns()};
+  }
 
  private:
   std::vector<Tensor> keep_;
@@ -341,7 +405,60 @@ class PersistentPlan {
   int dev_;
   int64_t steps_per_epoch_ = 0;
   PersistLaunch L_;
+  hipEvent_t ev_ = nullptr;  // timeline probe (launch_wait_at)
 };
+
+// Host-mapped, coherent int64 words a kernel can store into and the host can poll
+// (launch timelines: tools/driver_timeline.py).
+class HostMapped {
+ public:
+  explicit HostMapped(int64_t n) : n_(n) {
+    TORCH_CHECK(n > 0 && n <= (1 << 20), "HostMapped: 1..2^20 words");
+    hip_check(hipHostMalloc((void**)&h_, n * sizeof(int64_t), hipHostMallocMapped | hipHostMallocCoherent),
+              "hipHostMalloc(HostMapped)");
+    hip_check(hipHostGetDevicePointer((void**)&d_, h_, 0), "hipHostGetDevicePointer(HostMapped)");
+    zero();
+  }
+  ~HostMapped() {
+    if (h_) hipHostFree(h_);
+  }
+  HostMapped(const HostMapped&) = delete;
+  HostMapped& operator=(const HostMapped&) = delete;
+  void zero() {
+    volatile int64_t* v = h_;
+    for (int64_t k = 0; k < n_; ++k) v[k] = 0;
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  }
+  std::vector<int64_t> read() const {
+    volatile int64_t* v = h_;
+    std::vector<int64_t> out(n_);
+    for (int64_t k = 0; k < n_; ++k) out[k] = v[k];
+    return out;
+  }
+  // spin until word k is non-zero; CLOCK_MONOTONIC ns when it was seen, -1 after timeout_ns
+  int64_t spin(int64_t k, int64_t timeout_ns) const {
+    TORCH_CHECK(k >= 0 && k < n_);
+    volatile int64_t* v = h_ + k;
+    const int64_t t0 = mono_ns();
+    for (;;) {
+      if (*v != 0) return mono_ns();
+      const int64_t t = mono_ns();
+      if (t - t0 > timeout_ns) return -1;
+    }
+  }
+  int64_t device_ptr() const { return reinterpret_cast<int64_t>(d_); }
+
+ private:
+  int64_t n_;
+  int64_t* h_ = nullptr;
+  int64_t* d_ = nullptr;
+};
+
+std::vector<std::vector<int64_t>> clock_calibrate_py(int64_t n) {
+  std::vector<int64_t> a(n), b(n), c(n);
+  hip_check(clock_calibrate((int)n, a.data(), b.data(), c.data()), "clock_calibrate");
+  return {a, b, c};
+}
 
 // Which persistent engine fused_mlp_persistent would run for this configuration
 // ("workgroup", or "wave:L<lanes per row>R<rows per lane group>K<features per lane>").
@@ -885,6 +1002,26 @@ void memset_async_(Tensor t, int64_t value) {
   TORCH_CHECK(t.is_contiguous(), "memset_async_: contiguous tensor");
   c10::hip::HIPGuard guard(t.device().index());
   hip_check(hipMemsetAsync(t.data_ptr(), (int)value, t.numel() * t.element_size(), cur_stream(t)), "memset_async_");
+}
+
+std::vector<std::vector<int64_t>> graph_memset_params_(int64_t graph) {
+  std::vector<std::vector<int64_t>> out;
+  TORCH_CHECK(graph_memset_params(reinterpret_cast<void*>(graph), &out) >= 0, "graph_memset_params: query failed");
+  return out;
+}
+
+// a standalone graph with one memset node over t's storage (the runtime's memset-node path alone)
+void graph_memset_run_(Tensor t, int64_t value, int64_t esize, int64_t width, int64_t height, int64_t pitch,
+                       int64_t reps) {
+  check_gpu(t, "t");
+  const int64_t rows = height > 0 ? height : 1;
+  const int64_t span = (rows - 1) * (pitch > 0 ? pitch : width * esize) + width * esize;
+  TORCH_CHECK(esize == 1 || esize == 2 || esize == 4, "graph_memset_run: element size 1, 2 or 4");
+  TORCH_CHECK(span <= t.numel() * t.element_size(), "graph_memset_run: the memset exceeds the tensor");
+  c10::hip::HIPGuard guard(t.device().index());
+  hip_check(graph_memset_run(t.data_ptr(), (uint32_t)value, (int)esize, (size_t)width, (size_t)height,
+                             (size_t)pitch, (int)reps, cur_stream(t)),
+            "graph_memset_run");
 }
 
 int64_t graph_replace_memsets_(int64_t graph) {
@@ -1467,7 +1604,28 @@ PYBIND11_MODULE(_C, m) {
            py::arg("idx") = py::none(), py::arg("lcache") = py::none(), py::arg("idx_e0") = 0)
       .def("launch", &PersistentPlan::launch, py::arg("n_steps"), py::arg("cursor_pos") = -1)
       .def("launch_at", &PersistentPlan::launch_at, py::arg("n_steps"), py::arg("pos"))
-      .def_property_readonly("capacity", &PersistentPlan::capacity);
+      .def_property_readonly("capacity", &PersistentPlan::capacity)
+      .def("set_timeline", &PersistentPlan::set_timeline, py::arg("addr"))
+      .def("last_launch_ns", &PersistentPlan::last_launch_ns)
+      .def("launch_wait_at", &PersistentPlan::launch_wait_at, py::arg("n_steps"), py::arg("pos"), py::arg("mode"),
+           py::call_guard<py::gil_scoped_release>());
+  py::class_<HostMapped, std::shared_ptr<HostMapped>>(m, "HostMapped")
+      .def(py::init<int64_t>(), py::arg("n"))
+      .def("zero", &HostMapped::zero)
+      .def("read", &HostMapped::read)
+      .def("spin", &HostMapped::spin, py::arg("k"), py::arg("timeout_ns"), py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("device_ptr", &HostMapped::device_ptr);
+  m.def("clock_calibrate", &clock_calibrate_py, py::arg("n"), py::call_guard<py::gil_scoped_release>());
+  m.def("mono_ns", &mono_ns);
+  // raw synchronisation primitives with a CLOCK_MONOTONIC return stamp (timeline probes)
+  m.def("hip_device_sync_ns", []() {
+    hip_check(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    return mono_ns();
+  });
+  m.def("hip_stream_sync_ns", [](int64_t dev) {
+    hip_check(hipStreamSynchronize(c10::hip::getCurrentHIPStream((int)dev).stream()), "hipStreamSynchronize");
+    return mono_ns();
+  });
   m.def("persistent_engine", &persistent_engine, py::arg("B"), py::arg("Din"), py::arg("H"), py::arg("Dout"),
         py::arg("loss_kind"), py::arg("num_samples"), py::arg("world"), py::arg("variant") = 0,
         py::arg("has_bias") = true);
@@ -1500,6 +1658,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv1x1_bwd_supported", &conv1x1_bwd_supported_);
   m.def("graph_node_census", &graph_node_census_, "node count and per-hipGraphNodeType counts of a raw hipGraph_t");
   m.def("memset_async_", &memset_async_, "hipMemsetAsync of a whole tensor (tests of the graph memset rewrite)");
+  m.def("graph_memset_params", &graph_memset_params_,
+        "memset nodes of a raw hipGraph_t: [dst, value, elementSize, width, height, pitch] each");
+  m.def("graph_memset_run", &graph_memset_run_, py::arg("t"), py::arg("value"), py::arg("esize"), py::arg("width"),
+        py::arg("height"), py::arg("pitch"), py::arg("reps") = 1);
   m.def("graph_replace_memsets", &graph_replace_memsets_, "replace a raw hipGraph_t's memset nodes by fill-kernel nodes");
   m.def("int8_decode", &int8_decode_, "LLM.int8 decode path (M <= 32): outliers + quantise + int8 GEMV, no host sync",
         py::arg("x"), py::arg("q"), py::arg("sw"), py::arg("bias"), py::arg("threshold"), py::arg("out_dtype"),

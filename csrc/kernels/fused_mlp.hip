@@ -31,6 +31,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include <time.h>
 #include "sampler.h"
 
 namespace ptdt {
@@ -1053,7 +1054,13 @@ hipError_t persistent_launch(PersistLaunch& L, int n_steps, int64_t cursor_host_
   L.p.start_e = start_e;
   L.p.start_j = start_j;
   void* args[] = {&L.a, &L.p};
-  return hipLaunchKernel(L.fn, dim3(1), dim3(L.threads), args, L.lds, s);
+  timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  const hipError_t e = hipLaunchKernel(L.fn, dim3(1), dim3(L.threads), args, L.lds, s);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  L.host_ns[0] = (int64_t)t0.tv_sec * 1000000000 + t0.tv_nsec;
+  L.host_ns[1] = (int64_t)t1.tv_sec * 1000000000 + t1.tv_nsec;
+  return e;
 }
 
 hipError_t fused_mlp_persistent(const FusedMlpArgs& a, const PersistArgs& p, hipStream_t s) {

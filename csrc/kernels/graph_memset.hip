@@ -91,4 +91,48 @@ int graph_replace_memsets(void* graph) {
   return replaced;
 }
 
+// Parameters of every memset node (graph order): dst, value, elementSize, width, height, pitch.
+int graph_memset_params(void* graph, std::vector<std::vector<int64_t>>* out) {
+  hipGraph_t g = static_cast<hipGraph_t>(graph);
+  size_t n = 0;
+  if (hipGraphGetNodes(g, nullptr, &n) != hipSuccess) return -1;
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n && hipGraphGetNodes(g, nodes.data(), &n) != hipSuccess) return -1;
+  out->clear();
+  for (auto nd : nodes) {
+    hipGraphNodeType t;
+    if (hipGraphNodeGetType(nd, &t) != hipSuccess) return -1;
+    if (t != hipGraphNodeTypeMemset) continue;
+    hipMemsetParams mp{};
+    if (hipGraphMemsetNodeGetParams(nd, &mp) != hipSuccess) return -1;
+    out->push_back({(int64_t)reinterpret_cast<uintptr_t>(mp.dst), (int64_t)mp.value, (int64_t)mp.elementSize,
+                    (int64_t)mp.width, (int64_t)mp.height, (int64_t)mp.pitch});
+  }
+  return (int)out->size();
+}
+
+// One memset node with the given parameters in a fresh graph, instantiated and launched
+// `reps` times on stream s (synchronised): the runtime's memset-node path in isolation.
+hipError_t graph_memset_run(void* dst, uint32_t value, int esize, size_t width, size_t height, size_t pitch,
+                            int reps, hipStream_t s) {
+  hipGraph_t g = nullptr;
+  PTDT_HIP_CHECK(hipGraphCreate(&g, 0));
+  hipMemsetParams mp{};
+  mp.dst = dst;
+  mp.value = value;
+  mp.elementSize = (unsigned)esize;
+  mp.width = width;
+  mp.height = height;
+  mp.pitch = pitch;
+  hipGraphNode_t nd;
+  hipError_t e = hipGraphAddMemsetNode(&nd, g, nullptr, 0, &mp);
+  hipGraphExec_t ex = nullptr;
+  if (e == hipSuccess) e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  for (int r = 0; r < reps && e == hipSuccess; ++r) e = hipGraphLaunch(ex, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (ex) hipGraphExecDestroy(ex);
+  hipGraphDestroy(g);
+  return e;
+}
+
 }  // namespace ptdt

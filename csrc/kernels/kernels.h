@@ -88,6 +88,10 @@ struct PersistArgs {
   // caller guarantees the device cursor holds (start_e, start_j), and the wave/TP engines
   // take it from the kernel arguments instead of a dependent load at kernel entry
   int has_start, start_e, start_j;
+  // optional launch timeline (tools/driver_timeline.py): thread 0 stores the 100 MHz realtime
+  // counter at [0] kernel entry, [1] past the prologue barrier, [2] after the last step,
+  // [3] after the final parameter / cursor stores. May point at host-mapped memory.
+  int64_t* tl;
 };
 // Engine choice: the register-resident single-wave engine (linear_wave.hip) runs
 // Linear(Din, Dout) models with B <= 64 and small Dout; everything else runs the
@@ -124,7 +128,17 @@ struct PersistLaunch {
   size_t lds = 0;
   FusedMlpArgs a{};
   PersistArgs p{};
+  int64_t host_ns[2] = {0, 0};  // CLOCK_MONOTONIC right before / after the last hipLaunchKernel
 };
+// Timeline probe support (timeline.hip): thread 0 of wave 0 writes the realtime counter.
+__device__ __forceinline__ void tl_mark(int64_t* tl, int k) {
+  if (tl != nullptr && threadIdx.x == 0)
+    __hip_atomic_store(tl + k, (int64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// Host <-> device clock calibration: a 1-thread kernel answers n host pings (flag[k] = k + 1)
+// with its realtime counter in out[k]; host-mapped buffers. Returns per ping
+// (host ns before the flag store, host ns when the answer was seen, device ticks).
+hipError_t clock_calibrate(int n, int64_t* host_set, int64_t* host_seen, int64_t* dev_ticks);
 hipError_t fused_mlp_persistent_prepare(const FusedMlpArgs& a, const PersistArgs& p, PersistLaunch* out);
 hipError_t persistent_launch(PersistLaunch& L, int n_steps, int64_t cursor_host_pos, hipStream_t s,
                              int start_e = -1, int start_j = 0);
@@ -313,6 +327,12 @@ bool int8_mm_tiled_supported(int M, int N, int K);
 // (returns how many were replaced, -1 on error)
 int graph_node_census(void* graph, int* counts, int ncounts);
 int graph_replace_memsets(void* graph);
+}  // namespace ptdt
+#include <vector>
+namespace ptdt {
+int graph_memset_params(void* graph, std::vector<std::vector<int64_t>>* out);
+hipError_t graph_memset_run(void* dst, uint32_t value, int esize, size_t width, size_t height, size_t pitch,
+                            int reps, hipStream_t s);
 
 // LLM.int8 decode path (csrc/kernels/int8_decode.hip): M <= 32 rows, K % 64 == 0, K <= kInt8DecodeMaxK.
 // Outlier detection, activation quantisation and the int8 GEMV with the outlier columns fused, in two

@@ -939,6 +939,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   extern __shared__ int elist[];
   // diagnostic (stamps): kernel entry, for the prologue share of a launch (stamps[10], 10 ns ticks)
   const int64_t r_entry = pa.stamps != nullptr ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
+  tl_mark(pa.tl, 0);
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int B = a.B, Din = a.Din;
   const int estride = al4(pa.num_samples);
@@ -1000,6 +1001,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   float* const lring = reinterpret_cast<float*>(elist + 2 * estride + 16);  // after the 8 u64 timer slots
   __syncthreads();
   pstamp(2);
+  tl_mark(pa.tl, 1);
   if (wave != 0) {
     const int ht = (int)threadIdx.x - 64, hn = kThreads - 64;
     int64_t lo = pos0;
@@ -1376,6 +1378,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     ++barriers;
   }
   if (ring) __syncthreads();  // final barrier: the helpers reduce the remaining losses
+  tl_mark(pa.tl, 2);
 
   if (i == 0) {
     const auto Pw = gptr_w(a.P);
@@ -1414,6 +1417,10 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
         pa.stamps[13] += r_pro[2] - r_pro[1];
       }
     }
+  }
+  if (pa.tl != nullptr) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the final stores issued above are done
+    tl_mark(pa.tl, 3);
   }
 }
 

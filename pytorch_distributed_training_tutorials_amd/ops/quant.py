@@ -17,8 +17,8 @@ and multiplied int8 x int8 -> int32 on MFMA (``v_mfma_i32_16x16x64_i8``,
 csrc/kernels/int8_mm.hip), dequantised in the epilogue where the outlier product
 and the bias are added. (Gathering the outlier columns reads their indices on
 the host, as bitsandbytes does -- except at decode shapes, <= 32 tokens, where
-csrc/kernels/int8_decode.hip fuses the outlier columns into an int8 GEMV: two
-launches, no host read.) fp32, bf16 and fp16 activations run natively
+csrc/kernels/int8_decode.hip fuses the outlier columns into an int8 GEMV: three
+launches -- column statistics, row quantisation, GEMV -- and no host read.) fp32, bf16 and fp16 activations run natively
 (the reference's load_in_8bit Llama is fp16); the plain-PyTorch
 ``llm_int8_reference`` is the CPU path and the numerics reference only.
 """
@@ -97,16 +97,28 @@ class Int8Linear(nn.Module):
     def dequantized_weight(self) -> torch.Tensor:
         return self.weight_q.float() * self.weight_scale[:, None]
 
+    def invalidate_packed(self) -> None:
+        """Drop the decode GEMV's pre-shuffled weight copy (rebuilt on the next decode call).
+        Needed only after writes the version counter cannot see -- through ``weight_q.data``
+        or another alias of the storage; ``load_state_dict`` calls it itself."""
+        self._packed_cache = None
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        super()._load_from_state_dict(*args, **kwargs)
+        self.invalidate_packed()
+
     def _decode_packed(self, C):
         """The decode GEMV's pre-shuffled copy of ``weight_q`` (one contiguous KiB per wave load),
         rebuilt when the weights change: another tensor (a weak reference, so a recycled address
-        cannot alias) or an in-place update (version counter)."""
+        cannot alias), an in-place update of ``weight_q`` itself (version counter), or an explicit
+        :meth:`invalidate_packed` / ``load_state_dict``. Writes through ``weight_q.data`` bump a
+        different version counter: call :meth:`invalidate_packed` after them."""
         w = self.weight_q
         cache = getattr(self, "_packed_cache", None)
-        if cache is None or cache[0]() is not w or cache[1] != w._version:
-            cache = (weakref.ref(w), w._version, C.int8_decode_pack(w))
+        if cache is None or cache[0]() is not w or cache[1] != w._version or cache[2] != w.data_ptr():
+            cache = (weakref.ref(w), w._version, w.data_ptr(), C.int8_decode_pack(w))
             self._packed_cache = cache
-        return cache[2]
+        return cache[3]
 
     def _llm_int8(self, x2: torch.Tensor) -> torch.Tensor:
         b = self.bias
@@ -118,7 +130,7 @@ class Int8Linear(nn.Module):
         x2 = x2.contiguous()
         if _DECODE and C.int8_decode_supported(x2.shape[0], self.out_features, self.in_features):
             # decode shapes (<= 32 tokens): outliers, quantisation and the int8 GEMV with the outlier
-            # columns fused, two launches, no host read (csrc/kernels/int8_decode.hip)
+            # columns fused, three launches, no host read (csrc/kernels/int8_decode.hip)
             return C.int8_decode(x2, self.weight_q, self.weight_scale, b, self.threshold, _DTYPE_NAME[x2.dtype],
                                  self._decode_packed(C) if _PACKED else None)
         mask = C.int8_col_outliers(x2, self.threshold)

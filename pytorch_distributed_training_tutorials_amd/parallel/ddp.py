@@ -264,6 +264,10 @@ class DistributedDataParallel(nn.Module):
         self._queued = False
         self._flush_casts()  # anything a bucket never completed (e.g. no_sync accumulation)
         self.reducer.finalize()
+        if self.world_size > 1:
+            from ..utils import tuning
+
+            tuning.spmd_end()
 
     def _maybe_rebuild(self):
         if not self._rebuild or self._rebuilt or self.reducer.iteration < 1:
@@ -289,6 +293,14 @@ class DistributedDataParallel(nn.Module):
                 self._flush_casts()
                 self._fwd_stream = torch.cuda.current_stream(self.device)
                 self._remaining = {b: len(ps) for b, ps in enumerate(self._buckets)}
+        if self.world_size > 1:  # ranks run the same shapes in lock step until this step's backward ends
+            from ..utils import tuning  # (utils imports this module: no top-level import)
+
+            tuning.spmd_begin(self.comm)
+            out = self.module(*args, **kwargs)
+            if not torch.is_grad_enabled():
+                tuning.spmd_end()
+            return out
         return self.module(*args, **kwargs)
 
     @contextlib.contextmanager

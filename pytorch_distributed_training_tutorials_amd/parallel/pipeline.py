@@ -18,20 +18,27 @@ one process per GPU, each owning one stage:
   stage ``s+1`` works on ``i-1``; ``micro_batches == 1`` is the reference's
   naive, fully serialised split.
 
-Wire protocol: EVERY activation / gradient message is preceded by a fixed
-88-byte header ``int64[11] = [dtype, ndim, n_micro, d0..d7]`` on the same peer
-pair, so the receiver sizes each buffer from what was actually sent, and
-learns the step's micro-batch count from stage 0 -- a partial last batch
-(20 -> 8 rows) or an uneven micro-batch split (18 rows / 4 = 5,5,5,3; 6 rows /
-4 = 2,2,2) needs no configuration and cannot desynchronise the stages. The last
-stage slices its targets by the row counts it actually receives.
+Wire protocol (one host round trip per step per stage, none per micro-batch):
+at the start of a step stage ``s`` sends stage ``s+1`` ONE step header --
+``int64[3 + 7 + 64] = [dtype, ndim, n_micro, trailing dims d1..d7, rows_0 ..
+rows_{n_micro-1}]``, written after its first micro-batch forward (the first point
+where the output's dtype and trailing dims are known). The receiver reads it on
+the host once, and from then on sizes every payload of the step from it: forward
+activations are ``[rows_i, *trailing]``, and backward gradients carry no header
+at all (a gradient has the shape and dtype of the activation it belongs to, which
+both ends already hold). A partial last batch (20 -> 8 rows) or an uneven
+micro-batch split (18 rows / 4 = 5,5,5,3; 6 rows / 4 = 2,2,2) needs no
+configuration: stage 0's chunking travels down the pipeline in the headers. A
+stage whose output changes dtype or trailing shape between micro-batches, or
+changes the row count, raises instead of desynchronising. The last stage slices
+its targets by the row counts it receives.
 
 Overlap (GPU): sends and receives run on a dedicated P2P HIP stream. A send
 waits (stream event) for the compute stream that produced the tensor and the
 host returns immediately, so stage ``s`` computes micro-batch ``i+1`` while
-micro-batch ``i`` is on the link; a receive blocks the host only on the
-88-byte header (side-stream event), and the compute stream waits for the
-payload with a stream dependency, never a device-wide sync.
+micro-batch ``i`` is on the link; payload receives are pure stream dependencies
+(the compute stream waits for the P2P stream), so after the step header the host
+never waits on a peer.
 
 Micro-batch losses are weighted by their row share (``rows_i / rows``), so a
 mean-reduced loss over an uneven split equals the full-batch loss.
@@ -43,20 +50,28 @@ import torch.nn as nn
 
 _DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3, torch.int64: 4, torch.int32: 5}
 _DT_INV = {v: k for k, v in _DT.items()}
-_HDR = 11  # [dtype, ndim, n_micro, d0..d7]
-_MAXDIM = _HDR - 3
+_MAXDIM = 8   # tensor rank (leading row dim + 7 trailing)
+_MAXMB = 64   # micro-batches per step
+_HDR = 3 + (_MAXDIM - 1) + _MAXMB  # [dtype, ndim, n_micro, d1..d7, rows_0..rows_63]
 
 
-def _header(t: torch.Tensor, n_micro: int) -> torch.Tensor:
-    if t.dim() > _MAXDIM:
-        raise ValueError(f"PipelineStage: tensors of rank <= {_MAXDIM} only (got {t.dim()})")
+def _step_header(t: torch.Tensor, rows) -> torch.Tensor:
+    """The step header of a link: ``t`` is micro-batch 0's payload, ``rows`` every micro-batch's rows."""
+    if t.dim() < 1 or t.dim() > _MAXDIM:
+        raise ValueError(f"PipelineStage: activations of rank 1..{_MAXDIM} only (got {t.dim()})")
     if t.dtype not in _DT:
         raise ValueError(f"PipelineStage: unsupported dtype {t.dtype}")
-    return torch.tensor([_DT[t.dtype], t.dim(), n_micro, *t.shape] + [0] * (_MAXDIM - t.dim()), dtype=torch.int64)
+    if not 1 <= len(rows) <= _MAXMB:
+        raise ValueError(f"PipelineStage: 1..{_MAXMB} micro-batches per step (got {len(rows)})")
+    trail = list(t.shape[1:])
+    return torch.tensor([_DT[t.dtype], t.dim(), len(rows), *trail, *([0] * (_MAXDIM - 1 - len(trail))),
+                         *rows, *([0] * (_MAXMB - len(rows)))], dtype=torch.int64)
 
 
 def _parse(h):
-    return _DT_INV[h[0]], h[3:3 + h[1]], h[2]
+    """-> (dtype, trailing dims, per-micro-batch rows)."""
+    nd, nm = h[1], h[2]
+    return _DT_INV[h[0]], tuple(h[3:3 + nd - 1]), list(h[3 + _MAXDIM - 1:3 + _MAXDIM - 1 + nm])
 
 
 class PipelineStage:
@@ -82,40 +97,28 @@ class PipelineStage:
         gpu = self.device.type == "cuda" and getattr(comm, "native", False)
         self._side = torch.cuda.Stream(self.device) if (gpu and overlap) else None
         self.messages = 0  # payload messages sent + received (tests / tracing)
+        self.headers = 0   # step headers received: one per step on every stage but the first
 
     # ---------------------------------------------------------------- p2p helpers
-    def _send(self, t: torch.Tensor, peer: int, n_micro: int = 0):
-        t = t.detach().contiguous()
-        hdr = _header(t, n_micro)
-        self.messages += 1
-        if t.device.type != "cuda":
+    def _send_header(self, hdr: torch.Tensor, peer: int):
+        if self.device.type != "cuda":
             self.comm.send(hdr, peer)
-            self.comm.send(t, peer)
             return
         if self._side is None:
-            self.comm.send(hdr.to(t.device), peer)
-            self.comm.send(t, peer)
+            self.comm.send(hdr.to(self.device), peer)
             return
-        cur = torch.cuda.current_stream(self.device)
-        self._side.wait_stream(cur)  # the payload is produced on the compute stream
         with torch.cuda.stream(self._side):
             h = hdr.pin_memory().to(self.device, non_blocking=True)
             self.comm.send(h, peer)
-            self.comm.send(t, peer)
-        # the caching allocator must not hand these blocks to the compute stream before the send read them
-        t.record_stream(self._side)
         h.record_stream(self._side)
 
-    def _recv(self, peer: int):
-        """-> (tensor, n_micro announced by the sender)."""
-        self.messages += 1
+    def _recv_header(self, peer: int):
+        """The step header from ``peer``: the one host wait of a step on this link."""
+        self.headers += 1
         if self.device.type != "cuda":
             hdr = torch.zeros(_HDR, dtype=torch.int64)
             self.comm.recv(hdr, peer)
-            dt, shape, nm = _parse(hdr.tolist())
-            buf = torch.empty(shape, dtype=dt)
-            self.comm.recv(buf, peer)
-            return buf, nm
+            return _parse(hdr.tolist())
         stream = self._side or torch.cuda.current_stream(self.device)
         with torch.cuda.stream(stream):
             hd = torch.empty(_HDR, dtype=torch.int64, device=self.device)
@@ -124,15 +127,41 @@ class PipelineStage:
             hh.copy_(hd, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(stream)
-        ev.synchronize()  # host waits for the 88-byte header only
-        dt, shape, nm = _parse(hh.tolist())
-        with torch.cuda.stream(stream):
-            buf = torch.empty(shape, dtype=dt, device=self.device)
+        ev.synchronize()
+        return _parse(hh.tolist())
+
+    def _send(self, t: torch.Tensor, peer: int):
+        """A payload (no header): the receiver knows its shape from the step header / its own tensors."""
+        t = t.detach().contiguous()
+        self.messages += 1
+        if t.device.type != "cuda" or self._side is None:
+            self.comm.send(t, peer)
+            return
+        cur = torch.cuda.current_stream(self.device)
+        self._side.wait_stream(cur)  # the payload is produced on the compute stream
+        with torch.cuda.stream(self._side):
+            self.comm.send(t, peer)
+        # the caching allocator must not hand the block to the compute stream before the send read it
+        t.record_stream(self._side)
+
+    def _recv(self, shape, dtype, peer: int) -> torch.Tensor:
+        """A payload of known shape: on GPU a stream dependency only (no host wait)."""
+        self.messages += 1
+        if self.device.type != "cuda":
+            buf = torch.empty(shape, dtype=dtype)
             self.comm.recv(buf, peer)
-        if self._side is not None:
-            torch.cuda.current_stream(self.device).wait_stream(self._side)
-            buf.record_stream(torch.cuda.current_stream(self.device))
-        return buf, nm
+            return buf
+        if self._side is None:
+            buf = torch.empty(shape, dtype=dtype, device=self.device)
+            self.comm.recv(buf, peer)
+            return buf
+        with torch.cuda.stream(self._side):
+            buf = torch.empty(shape, dtype=dtype, device=self.device)
+            self.comm.recv(buf, peer)
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_stream(self._side)
+        buf.record_stream(cur)
+        return buf
 
     def synchronize(self):
         """Wait for every P2P this stage issued (end of step / before reading results)."""
@@ -146,19 +175,22 @@ class PipelineStage:
         ``module``'s parameters (call the optimizer afterwards). Any batch size
         works, including a partial last batch and splits that are not a multiple of
         ``micro_batches``; no stage is told the batch size."""
-        xs = list(x.chunk(self.micro_batches)) if self.first else None
-        n_mb = len(xs) if xs is not None else None  # later stages: from the first header
+        if self.first:
+            xs = list(x.chunk(self.micro_batches))
+            rows = [int(c.shape[0]) for c in xs]
+        else:
+            dt, trail, rows = self._recv_header(self.stage - 1)
+        n_mb = len(rows)
         rows_total = target.shape[0] if self.last else None
         inputs, outputs, losses = [], [], []
+        out_meta = None
         row = 0
-        i = 0
-        while n_mb is None or i < n_mb:  # fill: all forwards
+        for i in range(n_mb):  # fill: all forwards
             if self.first:
                 inp = xs[i].to(self.device, non_blocking=True)
             else:
-                inp, nm = self._recv(self.stage - 1)
+                inp = self._recv((rows[i], *trail), dt, self.stage - 1)
                 inp.requires_grad_(True)
-                n_mb = nm if n_mb is None else n_mb
             out = self.module(inp)
             inputs.append(inp)
             if self.last:
@@ -171,16 +203,25 @@ class PipelineStage:
                 losses.append(loss)
                 outputs.append(loss)
             else:
-                self._send(out, self.stage + 1, n_mb)
+                if out.dim() < 1 or out.shape[0] != rows[i]:
+                    raise RuntimeError(f"PipelineStage {self.stage}: a stage must keep the row count "
+                                       f"({rows[i]} rows in, {tuple(out.shape)} out)")
+                meta = (out.dtype, tuple(out.shape[1:]))
+                if out_meta is None:
+                    out_meta = meta
+                    self._send_header(_step_header(out, rows), self.stage + 1)
+                elif meta != out_meta:
+                    raise RuntimeError(f"PipelineStage {self.stage}: micro-batch {i} output {meta} differs from "
+                                       f"micro-batch 0's {out_meta} (one step header per step)")
+                self._send(out, self.stage + 1)
                 outputs.append(out)
-            i += 1
         if self.last and row != rows_total:
             raise RuntimeError(f"PipelineStage: received {row} rows for a target of {rows_total}")
         for i in reversed(range(len(outputs))):  # drain: backwards in reverse
             if self.last:
                 outputs[i].backward()
-            else:
-                g, _ = self._recv(self.stage + 1)
+            else:  # d(output): the shape and dtype of the activation this stage sent
+                g = self._recv(outputs[i].shape, outputs[i].dtype, self.stage + 1)
                 outputs[i].backward(g)
             if not self.first:
                 gi = inputs[i].grad
@@ -193,10 +234,15 @@ class PipelineStage:
     @torch.no_grad()
     def forward(self, x: torch.Tensor | None = None) -> torch.Tensor | None:
         """Inference through the pipeline; returns the output on the last stage."""
-        inp = x.to(self.device) if self.first else self._recv(self.stage - 1)[0]
+        if self.first:
+            inp = x.to(self.device)
+        else:
+            dt, trail, rows = self._recv_header(self.stage - 1)
+            inp = self._recv((rows[0], *trail), dt, self.stage - 1)
         out = self.module(inp)
         if not self.last:
-            self._send(out, self.stage + 1, 1)
+            self._send_header(_step_header(out, [int(out.shape[0])]), self.stage + 1)
+            self._send(out, self.stage + 1)
             self.synchronize()
             return None
         return out

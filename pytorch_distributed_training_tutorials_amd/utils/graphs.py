@@ -95,6 +95,8 @@ class GraphedStep:
         raw = g.raw_cuda_graph()
         census = native().graph_node_census(raw)
         self.node_count, self.memset_nodes = int(census[0]), int(census[1 + _MEMSET_NODE_TYPE])
+        # [dst, value, elementSize, width, height, pitch] of each captured memset (diagnostics)
+        self.memset_params = [list(map(int, p)) for p in native().graph_memset_params(raw)] if self.memset_nodes else []
         self.memsets_replaced = native().graph_replace_memsets(raw) if _MEMSET_FIX else 0
         g.instantiate()
         torch.cuda.synchronize(self.device)
@@ -106,13 +108,21 @@ class GraphedStep:
         return self.graph.n_collectives
 
     def eager(self):
-        """Run the step eagerly. The next replay re-captures first: on ROCm 7 a memset node of an
-        instantiated graph (MIOpen's atomic weight-gradient solvers zero their outputs with
-        hipMemsetAsync) stops zeroing its whole buffer once eager hipMemsetAsync calls have run after
-        the instantiation (tools/graph_memset_repro.hip, profiles/r4_graph_memset.md) -- replaying the
-        old graph after eager steps summed weight gradients onto stale memory (the round-3 ResNet-50
-        ``--graph auto`` divergence)."""
-        self._dirty = True
+        """Run the step eagerly. If the instantiated graph still holds memset nodes (the rewrite is
+        off, ``PTDT_GRAPH_MEMSET_FIX=0``, or a node could not be rewritten) the next replay
+        re-captures first: on ROCm 7 a memset node of an instantiated graph (MIOpen's atomic
+        weight-gradient solvers zero their outputs with hipMemsetAsync) stopped zeroing its buffer
+        once eager hipMemsetAsync calls had run after the instantiation (profiles/r4_graph_memset.md,
+        profiles/r5_graph_memset.md) -- replaying the old graph after eager steps summed weight
+        gradients onto stale memory (the round-3 ResNet-50 ``--graph auto`` divergence). With every
+        memset node rewritten as a fill kernel there is nothing to re-capture.
+
+        A re-capture runs ``fn``'s Python body once more under capture: its host-side effects
+        (DDP forward counters, reducer preparation, logging -- guard those with
+        ``torch.cuda.is_current_stream_capturing()``) happen again, and it pays a capture, an
+        instantiation and a new memory pool."""
+        if self.memset_nodes > self.memsets_replaced:
+            self._dirty = True
         return self.fn()
 
     def __call__(self):

@@ -95,6 +95,12 @@ for s in "$@"; do
     resnet)    jstep resnet_ddp 600 python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5
                jstep resnet_ddp 600 python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5 --impl torch ;;
     prof_resnet) prof resnet 600 python3 benchmarks/resnet_ddp.py --steps 3 --warmup 2 ;;
+    tl0)       # round-5 fixed-cost baseline: prologue split + kernel/HIP-API trace of the driver command
+               jstep tl0_stamps 300 python3 bench.py --steps 20 --warmup 5 --stamps --no_mlp_side --no_ref
+               step prof_tl0 300 rocprofv3 --kernel-trace --hip-trace --stats --output-format csv -d "$O/prof_${T}_tl0" -o run -- python3 bench.py --steps 20 --warmup 5 --no_mlp_side --no_ref ;;
+    tl)        jstep timeline 300 python3 tools/driver_timeline.py ;;
+    memset)    jstep memset_probe 600 python3 benchmarks/graph_memset_probe.py ;;
+    mlpstamps) jstep mlpstamps 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --stamps --no_ref ;;
     prof)      prof driver 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
                prof reference 300 python3 bench.py --engine reference --steps 200 --warmup 20 ;;
     pmc_tp)    pmc tp1 "$P1" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side

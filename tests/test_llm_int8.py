@@ -248,3 +248,12 @@ def test_decode_packed_cache_tracks_weight_identity_and_version():
     m.weight_q = torch.zeros(16, 64, dtype=torch.int8)
     m._decode_packed(C)
     assert len(calls) == 3
+    # a write through .data bypasses the version counter: the explicit hook drops the copy
+    m.weight_q.data.copy_(torch.ones(16, 64, dtype=torch.int8))
+    m.invalidate_packed()
+    assert torch.equal(m._decode_packed(C), m.weight_q) and len(calls) == 4
+    # load_state_dict invalidates by itself
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    sd["weight_q"].fill_(3)
+    m.load_state_dict(sd)
+    assert torch.equal(m._decode_packed(C), sd["weight_q"]) and len(calls) == 5

@@ -47,6 +47,12 @@ def test_pipeline_matches_single_process(tmp_path, world, micro, batches):
     for r in rs[:-1]:
         assert r["losses"] == [None] * len(batches)
     assert rs[-1]["losses"] == pytest.approx(losses, rel=1e-5)
+    # one step header per step per receiving stage, none per micro-batch / backward message
+    assert rs[0]["headers"] == 0
+    assert all(r["headers"] == len(batches) for r in rs[1:])
+    n_mb = sum(len(torch.zeros(b).chunk(micro)) for b in batches)
+    assert rs[0]["messages"] == 2 * n_mb            # forward sends + gradient receives, payloads only
+    assert all(r["messages"] == 4 * n_mb for r in rs[1:-1])
 
 
 def test_inprocess_model_parallel_cpu_matches_unsplit():
