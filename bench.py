@@ -271,8 +271,13 @@ def run_persistent(args, rank, world, dev, comm):
         # the bench counts its own steps from cursor 0, so every launch names its start
         # position (launch_at: no dependent cursor load at kernel entry)
         plan = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses, variant=variant)
-        for d in range(0, n_warm, chunk):
-            plan.launch(min(chunk, n_warm - d))
+        # the W warm-up steps: one launch through the timed region's own sequence (_untimed) when they
+        # fit one launch, so the timed launch below is the second of its kind in this process
+        if n_warm <= chunk:
+            _untimed(comm, dev, lambda: plan.launch_at(n_warm, 0))
+        else:
+            for d in range(0, n_warm, chunk):
+                plan.launch(min(chunk, n_warm - d))
         if os.environ.get("PTDT_BENCH_DEVICE_CURSOR") == "1":  # A/B: start from the device cursor
             launch_at = lambda n, p: plan.launch(n)  # noqa: E731
         else:
@@ -368,8 +373,7 @@ def _mlp_side(args, rank, world, dev, comm, xg):
     n_w, n_t = max(args.warmup, 1), args.steps
     losses = torch.zeros(max(n_w, n_t), device=dev)
     plan = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses)
-    plan.launch_at(n_w, 0)
-    torch.cuda.synchronize(dev)
+    _untimed(comm, dev, lambda: plan.launch_at(n_w, 0))
     t = _timed(comm, dev, lambda: plan.launch_at(n_t, n_w), label="mlp_side")
     failed = xg is not None and _xgmi_failed(comm, dev, xg, "MLP side measurement")
     return {"mlp_us_per_step": None if failed else round(1e6 * t / n_t, 3),
@@ -510,14 +514,49 @@ def _spin(comm):
     return _SPIN[key]
 
 
+_GPU_WARM_MS = float(os.environ.get("PTDT_BENCH_GPU_WARM_MS", "0"))
+_WARM_BUF: dict = {}
+
+
+def _gpu_warm(dev, ms: float) -> None:
+    """A/B knob (default off): ~``ms`` of HBM streaming right before a timed region (untimed, no
+    training work). Measured counter-productive: the fresh-process 20-step window went from 29-30 us
+    to 34-37 us with 2 ms of it (profiles/r5_driver_timeline.md) -- what helps is running the
+    warm-up steps through the timed region's own sequence (_untimed)."""
+    if dev.type != "cuda" or ms <= 0:
+        return
+    buf = _WARM_BUF.get(dev.index)
+    if buf is None:
+        buf = _WARM_BUF[dev.index] = torch.zeros(16 << 20, device=dev)  # 64 MiB: ~30 us per pass
+    for _ in range(max(1, int(ms * 1000 / 30))):
+        buf.add_(1.0)
+    torch.cuda.synchronize(dev)
+
+
+def _untimed(comm, dev, fn) -> None:
+    """The timed region's exact sequence (spin barrier resolved, barrier, sync, launch, sync) with
+    nothing recorded: the bench runs its warm-up steps through it, so the timed launch is not the
+    first of its kind in the process (the first such launch after setup measured 29-30 us for the
+    20-step window, the next ones 23-24 us; profiles/r5_driver_timeline.md)."""
+    spin = _spin(comm)
+    comm.barrier()
+    _sync(dev)
+    if spin is not None:
+        spin.wait()
+    fn()
+    _sync(dev)
+
+
 def _timed(comm, dev, fn, label: str = "headline"):
-    """Elapsed seconds of ``fn`` (MAX over ranks): collective barrier + device sync, then the
-    node-local spin barrier (ranks released within ~1-2 us instead of the collective's tens of
-    us), then every rank reads CLOCK_MONOTONIC (one clock per node), runs ``fn``, syncs and reads
-    it again. The per-rank stamps are gathered afterwards: ``start_skew_us`` = max - min of the
-    start stamps, ``window_us`` = last end - first start (the whole-node wall window)."""
+    """Elapsed seconds of ``fn`` (MAX over ranks): GPU power-state warm-up (untimed, _gpu_warm),
+    collective barrier + device sync, then the node-local spin barrier (ranks released within
+    ~1-2 us instead of the collective's tens of us), then every rank reads CLOCK_MONOTONIC (one
+    clock per node), runs ``fn``, syncs and reads it again. The per-rank stamps are gathered
+    afterwards: ``start_skew_us`` = max - min of the start stamps, ``window_us`` = last end - first
+    start (the whole-node wall window)."""
     spin = _spin(comm)  # resolved BEFORE the barrier: its first call imports a module (~0.4 ms), and a GPU
-    comm.barrier()      # left idle that long adds ~8-13 us to the next launch (profiles/r5_driver_timeline.md)
+    _gpu_warm(dev, _GPU_WARM_MS)  # left idle that long adds ~8-13 us to the next launch
+    comm.barrier()
     _sync(dev)
     if spin is not None:
         spin.wait()
@@ -634,6 +673,7 @@ def main(argv=None):
         extra["speedup_vs_torch"] = round(value / extra["ref_samples_per_s"], 3)
     dl.set_phase("report")
     extra["timing"] = dict(_TIMINGS)
+    extra["gpu_warmup_ms_before_timed"] = _GPU_WARM_MS if dev.type == "cuda" else 0.0
     rec = _record(args, world, value, elapsed, extra)
     if args.share_gpu:
         rec["rehearsal"] = f"{world} ranks sharing cuda:0 (no xGMI hop): protocol/correctness check, not a scaling number"

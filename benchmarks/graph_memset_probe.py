@@ -62,6 +62,14 @@ def main(argv=None):
     ap.add_argument("--replays", type=int, default=4)
     ap.add_argument("--lr", type=float, default=0.1)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--synthetic", action="store_true",
+                    help="the captured step's memset parameters (sizes, value, dst alignment mod 4 KiB) as "
+                         "hipMemsetAsync calls captured alone into one torch graph, plus a memset of another "
+                         "value; replayed with eager memsets / fills in between; counts unzeroed bytes per replay")
+    ap.add_argument("--trace_only", action="store_true",
+                    help="capture WITHOUT the rewrite and replay twice, each replay bracketed by philox_kernel "
+                         "markers, nothing else: run under rocprofv3 --kernel-trace and read the replays' dispatch "
+                         "order / queues with tools/graph_replay_order.py")
     a = ap.parse_args(argv)
     torch.backends.cudnn.benchmark, torch.backends.cudnn.deterministic = True, False
     from pytorch_distributed_training_tutorials_amd import native as _native
@@ -97,6 +105,65 @@ def main(argv=None):
     y = torch.randint(0, 1000, (a.batch,), device=dev, generator=torch.Generator(device=dev).manual_seed(5))
 
     results = {}
+    if a.synthetic:
+        params = [(0, 1, 131072, 3584)] * 4 + [(0, 1, 131072, 0)] * 3 + [(0, 1, 65536, 0), (0, 1, 32768, 3584),
+                                                                        (0, 1, 32768, 3584), (0, 1, 8192, 3584)]
+        bufs, views = [], []
+        for value, esize, width, align in params:
+            b = torch.empty(width + 8192, dtype=torch.uint8, device=dev)
+            off = (align - b.data_ptr()) % 4096
+            bufs.append(b)
+            views.append(b[off:off + width])
+        other = torch.empty(3 * 4096 + 100, dtype=torch.uint8, device=dev)
+        side = torch.cuda.Stream(dev)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=side):
+            for v in views:
+                native.memset_async_(v, 0)
+            native.memset_async_(other, 0x3F)  # a memset of another value in the same graph
+        for mode in ("plain", "eager_memsets_between", "eager_fills_between"):
+            bad = []
+            for rep in range(4):
+                for v in views:
+                    v.fill_(0xAB)
+                if mode == "eager_memsets_between":
+                    for n in (4096, 1000, 3 * 4096 + 7, 131072):
+                        native.memset_async_(torch.empty(n, dtype=torch.uint8, device=dev), 0x11)
+                elif mode == "eager_fills_between":
+                    torch.empty(1 << 20, device=dev).fill_(1.0)
+                torch.cuda.synchronize(dev)
+                g.replay()
+                torch.cuda.synchronize(dev)
+                bad.append([int((v != 0).sum()) for v in views] + [int((other != 0x3F).sum())])
+            emit({"what": "synthetic", "mode": mode, "unset_bytes_per_replay": bad})
+        env.destroy_process_group()
+        return
+    if a.trace_only:
+        graphs._MEMSET_FIX = False
+        model, ddp, opt = build()
+
+        def step():
+            ddp.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+                out = ddp(x)
+            loss = cross_entropy(out.float(), y)
+            loss.backward()
+            opt.step()
+            return loss
+
+        gs = graphs.GraphedStep(step, dev, comm=comm, warmup=3)
+        emit({"what": "nodes", "nodes": gs.node_count, "memset_nodes": gs.memset_nodes,
+              "params": [dict(zip(("dst", "value", "esize", "width", "height", "pitch"), p)) for p in gs.memset_params]})
+        marker = torch.empty(64, device=dev)
+        for _ in range(2):
+            native.philox_(marker, 1, 0, 1)  # marker: philox_kernel runs nowhere else in this process
+            torch.cuda.synchronize(dev)
+            gs()
+            torch.cuda.synchronize(dev)
+        native.philox_(marker, 1, 0, 1)
+        torch.cuda.synchronize(dev)
+        env.destroy_process_group()
+        return
     for fix in (False, True):
         graphs._MEMSET_FIX = fix
         model, ddp, opt = build()

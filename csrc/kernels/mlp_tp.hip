@@ -583,30 +583,33 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     const float* const st = stage(sc);
 
     // ---------------- fwd1: HT = W1aug . Xaug^T (this wave's 16 units x 32 rows), ReLU
-    f4 h[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    // four independent accumulation chains (tile x K-step parity) instead of two: a dependent
+    // v_mfma_f32_16x16x4_f32 waits for its predecessor's result, independent ones pipeline
+    f4 h[2][2] = {{{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}};
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
+      for (int t = 0; t < 2; ++t) {
         const f4 xb = *reinterpret_cast<const f4*>(st + (16 * t + c) * LDX + 16 * mt + 4 * q);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) h[t] = mfma4(w1r[mt][s], xb[s], h[t]);
+        for (int s = 0; s < 4; ++s) h[t][s & 1] = mfma4(w1r[mt][s], xb[s], h[t][s & 1]);
       }
     }
     float ht[2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ht[t][i] = fmaxf(h[t][i], 0.f);
+      for (int i = 0; i < 4; ++i) ht[t][i] = fmaxf(h[t][0][i] + h[t][1][i], 0.f);
 
     // ---------------- fwd2 partial: ZT_w = W2[:, slice] . HT (K steps permuted: unit 4q + s)
     const f4 a2 = *reinterpret_cast<const f4*>(W2m + c * LD2 + 4 * q);
-    f4 z[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f4 zz[2][2] = {{{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      z[0] = mfma4(a2[s], ht[0][s], z[0]);
-      z[1] = mfma4(a2[s], ht[1][s], z[1]);
+      zz[0][s & 1] = mfma4(a2[s], ht[0][s], zz[0][s & 1]);
+      zz[1][s & 1] = mfma4(a2[s], ht[1][s], zz[1][s & 1]);
     }
+    const f4 z[2] = {zz[0][0] + zz[0][1], zz[1][0] + zz[1][1]};
     {
       // tile-major planes: consecutive lanes read consecutive 16 B (no bank conflicts)
       f4* dst = reinterpret_cast<f4*>(xbuf + (par * NW + w) * 512 + l * 4);
@@ -761,12 +764,13 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
         xa[t][mt] = *reinterpret_cast<const f4*>(st + St::XT_OFF + (16 * mt + c) * LDXT + 16 * t + 4 * q);
-    f4 dh[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    f4 dhh[2][2] = {{{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      dh[0] = mfma4(g[0][s], w2t[s], dh[0]);
-      dh[1] = mfma4(g[1][s], w2t[s], dh[1]);
+      dhh[0][s & 1] = mfma4(g[0][s], w2t[s], dhh[0][s & 1]);
+      dhh[1][s & 1] = mfma4(g[1][s], w2t[s], dhh[1][s & 1]);
     }
+    f4 dh[2] = {dhh[0][0] + dhh[0][1], dhh[1][0] + dhh[1][1]};
     // transposed reads: H[row 16t + 4q + s][unit c] (ReLU mask, dW2's B) and
     // dZ[row 16t + 4q + s][class c] (dW2's A)
     f4 hT[2], dzT[2];
@@ -784,19 +788,27 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     db2 = rows4_sum(db2);
 
     // ---------------- dW2 = dZ^T . H (K = rows), dW1aug^T = Xaug^T . dH (K = rows)
-    f4 gw2 = {0.f, 0.f, 0.f, 0.f};
-    f4 gw1[MT];
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) gw1[mt] = f4{0.f, 0.f, 0.f, 0.f};
+    // one accumulation chain per row tile (t), added at the end: independent MFMAs pipeline
+    f4 gw2p[2], gw1p[2][MT];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
+      gw2p[t] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        gw2 = mfma4(dzT[t][s], hT[t][s], gw2);
+      for (int mt = 0; mt < MT; ++mt) gw1p[t][mt] = f4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) gw1[mt] = mfma4(xa[t][mt][s], dh[t][s], gw1[mt]);
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        gw2p[t] = mfma4(dzT[t][s], hT[t][s], gw2p[t]);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) gw1p[t][mt] = mfma4(xa[t][mt][s], dh[t][s], gw1p[t][mt]);
       }
     }
+    const f4 gw2 = gw2p[0] + gw2p[1];
+    f4 gw1[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) gw1[mt] = gw1p[0][mt] + gw1p[1][mt];
     mfma_settle();  // uniform branches follow (hb, tick, the all-reduce's failed check)
     tick(4);
 

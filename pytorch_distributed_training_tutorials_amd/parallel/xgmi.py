@@ -31,11 +31,13 @@ class XgmiAllReduce:
         self.rank = comm.rank
         self.max_elems = max_elems
         self.x = None
+        self.why = None  # why the one-shot path is off (None: it is on); reported by benchmarks
         handle = b""
         try:  # every rank reaches every collective below, whatever fails locally
             self.x = native().XgmiComm(self.rank, self.world, max_elems, self.device.index or 0)
             handle = self.x.handle()
         except RuntimeError as e:
+            self.why = f"buffer setup failed on rank {self.rank}: {e}"
             print(f"[ptdt] xGMI buffer setup failed on rank {self.rank}: {e}", flush=True)
         # device ordinals travel with the handles: open() refuses a peer device with no
         # direct access path (then every rank falls back to RCCL)
@@ -46,11 +48,16 @@ class XgmiAllReduce:
             try:
                 self.x.open(handles, [d for _, d in pairs])
             except RuntimeError as e:  # e.g. peer access unavailable
+                self.why = f"IPC open failed on rank {self.rank}: {e}"
                 print(f"[ptdt] xGMI all-reduce unavailable on rank {self.rank}: {e}", flush=True)
                 ok_open = 0
         self.ok = self._agree(ok_open)
+        if not self.ok and self.why is None:
+            self.why = "another rank could not set up or open the IPC buffers"
         if self.ok and self_test:
             self.ok = self._agree(int(self._self_test()))
+            if not self.ok:
+                self.why = "self-test failed (a rank saw wrong sums or a poll timeout)"
 
     def _agree(self, v: int) -> bool:
         return min(self.comm.all_gather_object(int(v))) == 1

@@ -13,6 +13,7 @@ mkdir -p gpurun_out
 T=${TAG:-l}
 O=gpurun_out
 PORT=$((29500 + RANDOM % 1000))
+PF=0
 
 step() {  # name secs cmd...   (stdout+stderr -> $O/$T_name.log)
   local name=$1 secs=$2; shift 2
@@ -100,6 +101,11 @@ for s in "$@"; do
                step prof_tl0 300 rocprofv3 --kernel-trace --hip-trace --stats --output-format csv -d "$O/prof_${T}_tl0" -o run -- python3 bench.py --steps 20 --warmup 5 --no_mlp_side --no_ref ;;
     tl)        jstep timeline 300 python3 tools/driver_timeline.py ;;
     memset)    jstep memset_probe 600 python3 benchmarks/graph_memset_probe.py ;;
+    memsyn)    jstep memset_syn 300 python3 benchmarks/graph_memset_probe.py --synthetic ;;
+    memtrace)  step prof_memtrace 600 rocprofv3 --kernel-trace --output-format csv -d "$O/prof_${T}_memtrace" -o run -- python3 benchmarks/graph_memset_probe.py --trace_only
+               timeout -k 5 120 python3 tools/graph_replay_order.py "$O/prof_${T}_memtrace/run_kernel_trace.csv" \
+                 > "$O/${T}_replay_order.txt" 2>&1; echo "replay_order exit $?"; tail -5 "$O/${T}_replay_order.txt"
+               rm -rf "$O/prof_${T}_memtrace" ;;  # ~200k dispatches (MIOpen find): too big to copy back
     mlpstamps) jstep mlpstamps 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --stamps --no_ref ;;
     prof)      prof driver 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
                prof reference 300 python3 bench.py --engine reference --steps 200 --warmup 20 ;;
@@ -124,7 +130,12 @@ for s in "$@"; do
                done ;;
     bntest)    # BN numerics under non-default geometry
                tstep pytest_bn 300 env PTDT_BN_DIR=15 PTDT_BN_AU=4 PTDT_BN_APPLY_BLOCKS=0 $PYTEST tests/test_norm.py ;;
-    run:*)     step "run" 600 bash -c "${s#run:}" ;;  # ad-hoc: run:'python3 benchmarks/x.py'
+    run:*)     step "run" 600 bash -c "${s#run:}" ;;
+    pyfail:*)  # one pytest selection whose failure report is printed to stdout (gpurun's tail)
+               PF=$((PF + 1)); L="$O/${T}_pyfail$PF.log"
+               timeout -k 10 600 python3 -u -m pytest -q -rf --timeout 120 --timeout-method thread ${s#pyfail:} \
+                 > "$L" 2>&1; c=$?; grep -E "^E  |^FAILED|passed|failed" "$L" | head -30
+               echo "pyfail$PF exit $c"; [ $c -le 1 ] || [ $c -eq 5 ] || exit $c ;;  # ad-hoc: run:'python3 benchmarks/x.py'
     *)         echo "unknown stage $s"; exit 2 ;;
   esac
 done

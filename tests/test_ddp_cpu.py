@@ -134,3 +134,17 @@ def test_tuning_table_pins_choice(tmp_path, monkeypatch):
     out = tmp_path / "dump.json"
     tuning.dump(str(out))
     assert json.loads(out.read_text())["linear"]["nt,128,1000,2048"] == "library"
+
+
+def test_native_resnet_ddp_host_logic_cpu(tmp_path):
+    """CPU / gloo dry run of the multi-GPU ResNet DDP case (tests/test_multi_gpu.py): the same worker,
+    fp32 -- bucket rebuild and the averaged all-reduce == one process accumulating the micro-batches."""
+    from . import _mgpu_workers
+
+    world = 2
+    spawn(_mgpu_workers.resnet_ddp, args=(world, free_port(), str(tmp_path), False), nprocs=world)
+    res = _load(tmp_path, world)
+    assert all(r["in_sync"] for r in res)
+    assert all(r["rebuilt"] and r["buckets"] >= 2 for r in res)
+    ref = _mgpu_workers.resnet_reference(world, gpu=False)
+    torch.testing.assert_close(res[0]["params"], ref, rtol=1e-4, atol=1e-5)

@@ -222,3 +222,67 @@ def test_graphed_resnet_ddp_step_matches_eager(pg, dev):
     torch.testing.assert_close(torch.tensor(lb), torch.tensor(la), rtol=2e-3, atol=2e-3)
     for k in sa:
         torch.testing.assert_close(sb[k], sa[k], rtol=2e-3, atol=2e-4, msg=lambda m, k=k: f"{k}: {m}")
+
+
+def test_graph_replay_with_miopen_memset_nodes_tracks_eager(pg, dev):
+    """The configuration that diverged: exhaustive-find MIOpen solvers
+    (cudnn.benchmark=True) whose atomic weight-gradient kernels zero their outputs with
+    hipMemsetAsync, so the captured ResNet-50 step holds memset nodes. GraphedStep rewrites every one
+    (memsets_replaced == memset_nodes > 0) and 4 replays from a snapshot follow 4 eager steps from the
+    same snapshot within 2e-3 (benchmarks/graph_memset_probe.py: without the rewrite the 2nd replay's
+    loss is ~1e19; profiles/r5_graph_memset.md)."""
+    from pytorch_distributed_training_tutorials_amd import native
+    from pytorch_distributed_training_tutorials_amd.models.resnet import resnet50
+    from pytorch_distributed_training_tutorials_amd.ops.loss import cross_entropy
+    from pytorch_distributed_training_tutorials_amd.ops.optim import FusedSGD
+    from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
+    from pytorch_distributed_training_tutorials_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_distributed_training_tutorials_amd.utils import graphs
+
+    old = torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark
+    torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = False, True
+    try:
+        comm = comm_mod.get_default(dev)
+        torch.manual_seed(0)
+        model = resnet50(num_classes=1000).to(dev).to(memory_format=torch.channels_last)
+        ddp = DistributedDataParallel(model, device_ids=[dev.index], comm=comm)
+        # small steps: the atomic solvers' run-to-run noise stays far below the tolerance (at lr 0.1
+        # two EAGER runs from one snapshot already differ by ~5 % after 4 steps)
+        opt = FusedSGD(model.parameters(), lr=0.002, momentum=0.9, weight_decay=1e-4, bf16_shadow=True)
+        x = torch.empty(32, 3, 128, 128, device=dev)
+        native().philox_(x, 1234, 0, 1)
+        x = x.contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 1000, (32,), device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+
+        def step():
+            ddp.zero_grad()
+            with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+                out = ddp(x)
+            loss = cross_entropy(out.float(), y)
+            loss.backward()
+            opt.step()
+            return loss
+
+        gs = graphs.GraphedStep(step, dev, comm=comm, warmup=3)
+        assert gs.memset_nodes > 0, "no memset node captured: the test no longer covers the failing path"
+        assert gs.memsets_replaced == gs.memset_nodes
+        live = [p.data for p in model.parameters()]
+        live += [sh for p in model.parameters() if (sh := getattr(p, "_ptdt_bf16", None)) is not None]
+        live += [opt.state[p]["momentum_buffer"] for p in model.parameters() if "momentum_buffer" in opt.state.get(p, {})]
+        live += list(model.buffers()) + list(opt._counters.values()) + list(ddp.reducer.bucket_tensors())
+        snap = [t.detach().clone() for t in live]
+        rl = [float(gs()) for _ in range(4)]
+        torch.cuda.synchronize(dev)
+        pa = [p.detach().float().clone() for p in model.parameters()]
+        with torch.no_grad():
+            for t, s in zip(live, snap):
+                t.copy_(s)
+        el = [float(step()) for _ in range(4)]
+        torch.cuda.synchronize(dev)
+        pb = [p.detach().float().clone() for p in model.parameters()]
+    finally:
+        torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
+    assert all(torch.isfinite(torch.tensor(rl)))
+    torch.testing.assert_close(torch.tensor(rl), torch.tensor(el), rtol=2e-3, atol=2e-3)
+    for a, b in zip(pa, pb):
+        torch.testing.assert_close(a, b, rtol=2e-3, atol=2e-3)

@@ -237,3 +237,47 @@ def test_stream_pipeline_two_gpus_matches_single_queue_pipeline():
     torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-6)
     worst = max(((ga - gb).abs().max() / (gb.abs().max() + 1e-30)).item() for ga, gb in zip(outs[0][1], outs[1][1]))
     assert worst <= 1e-5, worst
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_native_resnet_ddp_multi_gpu_equals_accumulated_single_process(tmp_path, world):
+    """Native ResNet DDP at world > 1 -- grad sinks, deferred bf16 casts, bucket rebuild (VERDICT r4 #6a):
+    replicas bitwise equal, parameters == one process accumulating the ranks' micro-batches. World 1
+    runs the same worker on a one-GPU box (the GPU-only paths without the all-reduce)."""
+    if N_GPU < world:
+        pytest.skip(f"needs {world} GPUs, {N_GPU} visible")
+    spawn(_mgpu_workers.resnet_ddp, args=(world, free_port(), str(tmp_path), True), nprocs=world)
+    res = _ranks(tmp_path, world)
+    assert all(r["in_sync"] for r in res)
+    assert all(r["rebuilt"] and r["buckets"] >= 2 for r in res)
+    assert res[0]["sinks"] > 0 and res[0]["deferred"]
+    ref = _mgpu_workers.resnet_reference(world, gpu=True)
+    torch.testing.assert_close(res[0]["params"], ref, rtol=2e-2, atol=2e-3)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_graphed_step_with_rccl_collectives_multi_gpu(tmp_path, world):
+    """GraphedStep with the DDP all-reduces captured at world > 1 (VERDICT r4 #6b): replay == eager."""
+    if N_GPU < world:
+        pytest.skip(f"needs {world} GPUs, {N_GPU} visible")
+    spawn(_mgpu_workers.graphed_ddp_gpu, args=(world, free_port(), str(tmp_path)), nprocs=world)
+    res = _ranks(tmp_path, world)
+    assert all(r["in_sync"] for r in res)
+    assert all(r["n_collectives"] >= (1 if world > 1 else 0) for r in res)
+    for r in res:
+        torch.testing.assert_close(torch.tensor(r["replay_losses"]), torch.tensor(r["eager_losses"]),
+                                   rtol=1e-5, atol=1e-6)
+        assert r["max_gap"] < 1e-5
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_xgmi_self_test_and_peer_matrix(tmp_path, world):
+    """The one-shot xGMI path's self-test across devices, with the peer-access matrix printed
+    (VERDICT r4 #6c): on an xGMI-connected node every pair must have direct access."""
+    if N_GPU < world:
+        pytest.skip(f"needs {world} GPUs, {N_GPU} visible")
+    spawn(_mgpu_workers.xgmi_peer_matrix, args=(world, free_port(), str(tmp_path)), nprocs=world)
+    res = _ranks(tmp_path, world)
+    print("peer-access matrix:", res[0]["matrix"], "xGMI ok:", [r["ok"] for r in res], res[0]["why"])
+    assert all(all(row[:world]) for row in res[0]["matrix"][:world])
+    assert all(r["ok"] for r in res), res[0]["why"]

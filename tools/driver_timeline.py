@@ -25,6 +25,9 @@ Variants (one JSON line each, medians over the reps, plus the calibration line):
   nostamp  timeline off (the stamps' own cost: compare total_us with bench)
   idle2ms  as bench after a 2 ms host sleep (GPU idle before the launch)
   busyNNN  as bench after NNN us of host busy-waiting (GPU idle, CPU awake)
+  cold     as bench after a 50 ms host sleep (GPU power state dropped)
+  coldwN   as cold, then N ms of streaming kernels before the barrier (power-state ramp back up)
+  benchexact  bench.py's own _timed() around the launch (window from its CLOCK_MONOTONIC stamps)
   waitK    launch + wait entirely in C++ (PersistentPlan.launch_wait_at mode K: 0 hipDeviceSynchronize,
            1 hipStreamSynchronize, 2 event record + synchronize, 3 hipExtLaunchKernel stop event +
            synchronize, 4 hipStreamQuery spin, 5 ext-launch stop event + hipEventQuery spin), then the
@@ -64,7 +67,7 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--variants", default="bench,spin,hipsync,nostamp,idle2ms,busy20,busy100,busy500,"
-                                          "wait0,wait1,wait2,wait3,wait4,wait5")
+                                          "wait0,wait1,wait2,wait3,wait4,wait5,cold,coldw0.2,coldw1,coldw5,benchexact")
     ap.add_argument("--out", default=None)
     a = ap.parse_args(argv)
 
@@ -88,6 +91,7 @@ def main(argv=None):
     losses = torch.zeros(max(a.steps, a.warmup, 1), device=dev)
     plan = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses)
     hm = C.HostMapped(8)
+    warm = torch.empty(64 << 20, device=dev)  # 256 MiB for the power-state ramp variants
     pos = 0
     plan.launch_at(a.warmup, pos)
     pos += a.warmup
@@ -104,6 +108,15 @@ def main(argv=None):
         for r in range(a.reps + 2):
             hm.zero()
             plan.set_timeline(0 if var == "nostamp" else hm.device_ptr)
+            if var.startswith("cold"):
+                time.sleep(0.05)
+                if var.startswith("coldw"):  # ~N ms of HBM streaming (2 x 256 MiB per add_, ~0.1 ms each)
+                    for _ in range(max(1, int(float(var[5:]) * 10))):
+                        warm.add_(1.0)
+            if var == "benchexact":
+                torch.cuda.synchronize(dev)
+                bench._timed(comm, dev, lambda: plan.launch_at(a.steps, pos), label="tl")
+                h2 = None
             comm.barrier()
             torch.cuda.synchronize(dev)
             if var == "idle2ms":
@@ -114,6 +127,14 @@ def main(argv=None):
                     pass
             seen = None
             waited = None
+            if var == "benchexact":  # the launch already ran inside bench._timed
+                w_us = bench._TIMINGS["tl"]["window_us"]
+                pos += a.steps
+                if r >= 2:
+                    rows.append({"total_us": w_us})
+                else:
+                    first.append(w_us)
+                continue
             if var.startswith("wait"):
                 h0, h1, waited = plan.launch_wait_at(a.steps, pos, int(var[4:]))
                 torch.cuda.synchronize(dev)
