@@ -136,9 +136,9 @@ def main(argv=None):
     if graphed:  # utils/graphs.py: eager warm-up steps on a side stream, then one hipGraph per step
         eager = step
         if mode == "auto":
-            # eager rounds FIRST, then capture and replay rounds: never a replay after eager steps
-            # (an instantiated graph's memset nodes misbehave once eager memsets ran after it;
-            # GraphedStep.eager re-captures for that case, profiles/r4_graph_memset.md)
+            # eager rounds FIRST, then capture and replay rounds. (The captured step's memset nodes,
+            # which the runtime executes only partially from a graph's second launch on, are
+            # rewritten as fill kernels by GraphedStep: profiles/r5_graph_memset.md)
             ab = {"eager": [], "graph": []}
             for _ in range(max(3, a.warmup)):
                 eager()

@@ -41,7 +41,12 @@ def _like(t: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
     """t in x's memory layout (autograd hands back whatever the consumer produced)."""
     if t.stride() == x.stride():
         return t
-    return t.contiguous(memory_format=torch.channels_last) if x.dim() == 4 else t.contiguous()
+    out = t.contiguous(memory_format=torch.channels_last) if x.dim() == 4 else t.contiguous()
+    if out.stride() != x.stride():
+        # size-1 dims (e.g. [B, C, 1, 1] after layer4 of a small-image ResNet) make several stride
+        # tuples "contiguous" for one layout, and .contiguous() keeps t's: copy into x's exact strides
+        out = torch.empty_strided(x.shape, x.stride(), dtype=t.dtype, device=t.device).copy_(t)
+    return out
 
 
 class ResidualLink:

@@ -68,6 +68,10 @@ for s in "$@"; do
     tests:*)   tstep pytest_sel 600 python3 -u -m pytest -q -rf --timeout 120 --timeout-method thread ${s#tests:} ;;
     smoke)     step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" ;;
     driver)    for i in 1 2 3; do jstep bench_driver 300 python3 bench.py --gpus 1 --steps 20 --warmup 5; done ;;
+    rehab)     # A/B of the warm-up split (PTDT_BENCH_REHEARSALS), interleaved, headline only
+               for i in 1 2 3; do for r in 1 2 3; do
+                 jstep rehab 120 env PTDT_BENCH_REHEARSALS=$r python3 bench.py --steps 20 --warmup 5 --no_ref --no_mlp_side
+               done; done ;;
     default)   jstep bench_default 300 python3 bench.py ;;
     stamps)    jstep stamps 300 python3 bench.py --steps 20000 --warmup 2000 --stamps --no_mlp_side
                jstep stamps 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --stamps ;;

@@ -273,16 +273,71 @@ def test_graph_replay_with_miopen_memset_nodes_tracks_eager(pg, dev):
         snap = [t.detach().clone() for t in live]
         rl = [float(gs()) for _ in range(4)]
         torch.cuda.synchronize(dev)
-        pa = [p.detach().float().clone() for p in model.parameters()]
         with torch.no_grad():
             for t, s in zip(live, snap):
                 t.copy_(s)
         el = [float(step()) for _ in range(4)]
         torch.cuda.synchronize(dev)
-        pb = [p.detach().float().clone() for p in model.parameters()]
+        with torch.no_grad():
+            for t, s in zip(live, snap):
+                t.copy_(s)
+        el2 = [float(step()) for _ in range(4)]  # eager again: the atomic solvers' run-to-run floor
+        torch.cuda.synchronize(dev)
     finally:
         torch.backends.cudnn.deterministic, torch.backends.cudnn.benchmark = old
-    assert all(torch.isfinite(torch.tensor(rl)))
-    torch.testing.assert_close(torch.tensor(rl), torch.tensor(el), rtol=2e-3, atol=2e-3)
-    for a, b in zip(pa, pb):
-        torch.testing.assert_close(a, b, rtol=2e-3, atol=2e-3)
+    rl, el, el2 = torch.tensor(rl), torch.tensor(el), torch.tensor(el2)
+    assert bool(torch.isfinite(rl).all())
+    gap = ((rl - el).abs() / el.abs()).max().item()
+    floor = ((el2 - el).abs() / el.abs()).max().item()
+    print(f"replay vs eager {gap:.2e}, eager vs eager {floor:.2e}, memset nodes {gs.memset_nodes}")
+    # the first replay's forward runs the snapshot's weights: same loss as the eager step's
+    assert abs(rl[0] - el[0]) <= 1e-3 * abs(el[0])
+    # then within 2e-3, or within the noise two eager runs show (without the rewrite: ~1e19)
+    assert gap <= max(2e-3, 3 * floor), (gap, floor)
+
+
+# the memset nodes of the captured ResNet-50 step (benchmarks/graph_memset_probe.py): value 0, byte
+# elements, (width, dst offset mod 4 KiB)
+_RESNET_MEMSETS = [(131072, 3584)] * 4 + [(131072, 0)] * 3 + [(65536, 0), (32768, 3584), (32768, 3584), (8192, 3584)]
+
+
+def test_graph_memset_nodes_fail_from_the_second_replay_and_the_rewrite_fixes_it(dev, native):
+    """Root cause of the replay divergence (profiles/r5_graph_memset.md): a graph holding the captured
+    step's memset shapes -- hipMemsetAsync calls only, no MIOpen, no eager work in between -- zeroes
+    every buffer on its first launch, but from the second launch on the runtime leaves thousands of
+    bytes of several memset nodes unset. The same graph with the nodes rewritten as fill kernels
+    (graph_replace_memsets, what GraphedStep does) is correct on every launch."""
+    views, bufs = [], []
+    for width, align in _RESNET_MEMSETS:
+        b = torch.empty(width + 8192, dtype=torch.uint8, device=dev)
+        off = (align - b.data_ptr()) % 4096
+        bufs.append(b)
+        views.append(b[off:off + width])
+    other = torch.empty(3 * 4096 + 100, dtype=torch.uint8, device=dev)
+
+    def run(rewrite: bool):
+        side = torch.cuda.Stream(dev)
+        g = torch.cuda.CUDAGraph(keep_graph=True)
+        with torch.cuda.graph(g, stream=side):
+            for v in views:
+                native.memset_async_(v, 0)
+            native.memset_async_(other, 0x3F)
+        raw = g.raw_cuda_graph()
+        if rewrite:
+            assert native.graph_replace_memsets(raw) == len(views) + 1
+        g.instantiate()
+        bad = []
+        for _ in range(4):
+            for v in views:
+                v.fill_(0xAB)
+            other.fill_(0)
+            torch.cuda.synchronize(dev)
+            g.replay()
+            torch.cuda.synchronize(dev)
+            bad.append(sum(int((v != 0).sum()) for v in views) + int((other != 0x3F).sum()))
+        return bad
+
+    fixed = run(True)
+    assert fixed == [0, 0, 0, 0]
+    raw = run(False)  # the runtime's own memset nodes: reported, not asserted (a fixed runtime passes too)
+    print("unset bytes per launch, memset nodes kept:", raw, "rewritten:", fixed)
