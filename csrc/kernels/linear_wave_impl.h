@@ -1005,12 +1005,15 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   if (wave != 0) {
     const int ht = (int)threadIdx.x - 64, hn = kThreads - 64;
     int64_t lo = pos0;
-    auto reduce_losses = [&](int64_t hi) {  // positions [lo, hi): sum the 64 shares in lane order
-      for (int64_t P = lo + ht; P < hi; P += hn) {
-        const float* sh = lring + (int)((P - pos0) % ring) * 64;
-        float acc = 0.f;
-        for (int l = 0; l < 64; ++l) acc += sh[l];
-        pa.losses[P - pos0] = acc;
+    // positions [lo, hi): 16 lanes per position (a DPP row), 4 shares per lane (one 16-B LDS read),
+    // then a fixed-order 16-lane tree -- the final call runs after the last step, in the launch's tail
+    auto reduce_losses = [&](int64_t hi) {
+      const int grp = ht >> 4, sub = ht & 15, ngrp = hn >> 4;
+      for (int64_t P = lo + grp; P < hi; P += ngrp) {
+        const float* sh = lring + ((int)(P - pos0) % ring) * 64;
+        const float4 v = *reinterpret_cast<const float4*>(sh + 4 * sub);
+        const float acc = group_sum<16>((v.x + v.y) + (v.z + v.w));
+        if (sub == 0) pa.losses[P - pos0] = acc;
       }
       lo = hi > lo ? hi : lo;
     };
@@ -1373,13 +1376,8 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     if (ring) run(std::false_type{}, std::true_type{});
     else run(std::false_type{}, std::false_type{});
   }
-  while (barriers < T) {
-    __syncthreads();
-    ++barriers;
-  }
-  if (ring) __syncthreads();  // final barrier: the helpers reduce the remaining losses
   tl_mark(pa.tl, 2);
-
+  // final stores first, then the remaining barriers: their latency overlaps the helpers' tail
   if (i == 0) {
     const auto Pw = gptr_w(a.P);
     const auto Gw = gptr_w(a.G);
@@ -1418,6 +1416,11 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
       }
     }
   }
+  while (barriers < T) {
+    __syncthreads();
+    ++barriers;
+  }
+  if (ring) __syncthreads();  // final barrier: the helpers reduce the remaining losses
   if (pa.tl != nullptr) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the final stores issued above are done
     tl_mark(pa.tl, 3);

@@ -43,6 +43,7 @@ namespace {
 
 constexpr int kTpThreadsMax = 320;  // up to 4 compute waves + the helper wave
 using f4 = __attribute__((ext_vector_type(4))) float;
+using f2 = __attribute__((ext_vector_type(2))) float;
 
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
 
@@ -199,6 +200,7 @@ struct TpStage {
 };
 constexpr int kTpLD2 = 20;  // W2 slice (classes x 16 units), b128 rows
 constexpr int kTpLDT = 36;  // per-wave transposes: 16 (class / unit) x 32 rows
+constexpr int kTpLDZ = 20;  // shared dZ, row-major: 32 rows x 16 classes, b128 rows
 constexpr int kTpLossRing = 32;  // loss-ring slots (power of two)
 constexpr int kTpLossFlush = 16; // steps per flush: the slots being added are never the one written meanwhile
 __host__ __device__ __forceinline__ int tp_wave_floats() { return 16 * kTpLD2 + 2 * 16 * kTpLDT + 16; }
@@ -254,6 +256,10 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   // scaled loss share per step; every kTpLossFlush steps all waves add the shares of the
   // past kTpLossFlush slots in lane order
   float* const lring = lds + al4((int)(reinterpret_cast<float*>(fkeys) - lds) + 48);
+  // shared dZ of the step (written by the row slices' owners before the second barrier):
+  // row-major [32][kTpLDZ] and transposed [16 classes][LDT] with interleaved tiles
+  float* const dZr = lring + kTpLossRing * 64;
+  float* const dZt = dZr + 32 * kTpLDZ;
   auto flush_losses = [&](int lo, int hi) {  // steps [lo, hi), hi - lo <= kTpLossFlush (helper wave)
     const int j = l;
     if (j < hi - lo) {
@@ -371,6 +377,8 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   // arithmetic of a one-pass fill cost ~1-2 us of every launch's prologue)
   static_assert(St::FLOATS % 4 == 0, "float4 fill");
   for (int e = tid; e < 3 * St::FLOATS / 4; e += T) reinterpret_cast<f4*>(stage0)[e] = f4{0.f, 0.f, 0.f, 0.f};
+  // loss ring: each step writes its 32 row losses into entries 0..31 of its slot; 32..63 stay 0
+  for (int e = tid; e < kTpLossRing * 64; e += T) lring[e] = 0.f;
   __syncthreads();
   if (hb) {
     for (int e = tid; e < 3 * 64; e += T) {  // per slot: X[row][Din] and X^T[Din][row], rows 0..31
@@ -533,7 +541,8 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       // shares of steps [k-17, k-1): written by wave 0 before barrier k-1
       if (k > 1 && ((k - 1) & (kTpLossFlush - 1)) == 0) flush_losses(k - 1 - kTpLossFlush, k - 1);
       stage_write(sn);
-      __syncthreads();  // barrier of step k
+      __syncthreads();  // barrier 1 of step k (partial logits)
+      __syncthreads();  // barrier 2 of step k (dZ slices)
       ce = ne;
       cj = nj;
       sc = sn;
@@ -583,55 +592,71 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     const float* const st = stage(sc);
 
     // ---------------- fwd1: HT = W1aug . Xaug^T (this wave's 16 units x 32 rows), ReLU
-    // four independent accumulation chains (tile x K-step parity) instead of two: a dependent
-    // v_mfma_f32_16x16x4_f32 waits for its predecessor's result, independent ones pipeline
-    f4 h[2][2] = {{{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}};
+    f4 h[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
+    for (int t = 0; t < 2; ++t) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int mt = 0; mt < MT; ++mt) {
         const f4 xb = *reinterpret_cast<const f4*>(st + (16 * t + c) * LDX + 16 * mt + 4 * q);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) h[t][s & 1] = mfma4(w1r[mt][s], xb[s], h[t][s & 1]);
+        for (int s = 0; s < 4; ++s) h[t] = mfma4(w1r[mt][s], xb[s], h[t]);
       }
     }
     float ht[2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ht[t][i] = fmaxf(h[t][0][i] + h[t][1][i], 0.f);
+      for (int i = 0; i < 4; ++i) ht[t][i] = fmaxf(h[t][i], 0.f);
 
     // ---------------- fwd2 partial: ZT_w = W2[:, slice] . HT (K steps permuted: unit 4q + s)
     const f4 a2 = *reinterpret_cast<const f4*>(W2m + c * LD2 + 4 * q);
-    f4 zz[2][2] = {{{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}};
+    f4 z[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      zz[0][s & 1] = mfma4(a2[s], ht[0][s], zz[0][s & 1]);
-      zz[1][s & 1] = mfma4(a2[s], ht[1][s], zz[1][s & 1]);
+      z[0] = mfma4(a2[s], ht[0][s], z[0]);
+      z[1] = mfma4(a2[s], ht[1][s], z[1]);
     }
-    const f4 z[2] = {zz[0][0] + zz[0][1], zz[1][0] + zz[1][1]};
     {
       // tile-major planes: consecutive lanes read consecutive 16 B (no bank conflicts)
       f4* dst = reinterpret_cast<f4*>(xbuf + (par * NW + w) * 512 + l * 4);
       dst[0] = z[0];
       dst[64] = z[1];
     }
-    // H^T of the slice for the backward's transposed reads (wave-private)
+    // H^T of the slice for the backward's transposed reads (wave-private). Rows of the two tiles
+    // interleave (batch row 16 t + c at position 2 c + t): one 8-B store per unit instead of two
+    // 4-B stores, and the readers still fetch 8 consecutive positions with two 16-B loads
 #pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) Th[(4 * q + i) * LDT + 16 * t + c] = ht[t][i];
-    // wave-private or previous-step data the loss needs, read before the barrier so
-    // that only the partial logits are waited for after it: b2 (this wave's mirror)
-    // and the current batch's targets (staged in slot sc before the last barrier)
-    const f4 b2v = *reinterpret_cast<const f4*>(B2m + 4 * q);
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<f2*>(Th + (4 * q + i) * LDT + 2 * c) = f2{ht[0][i], ht[1][i]};
+    // ---- the loss is split by rows: wave w owns the 8-row slices sl = w, w + NW, .. (lane: row
+    // lrow = l >> 3 of the slice, classes 2 lk, 2 lk + 1 with lk = l & 7), so the softmax is computed
+    // once per element instead of once per wave; the dZ slices meet in LDS at a second barrier.
+    // Everything the loss reads besides the partial logits is read before the first barrier: b2
+    // (this wave's mirror) and the current batch's targets (staged in slot sc before the last barrier).
     const float* const ys = st + St::Y_OFF;
-    int yl[2];
-    f4 yf[2];
+    const int lrow = l >> 3, lk = l & 7, cls0 = 2 * lk;  // (lr is the learning rate)
+    constexpr int NSL = 4;  // 8-row slices of the 32-row tile pair
+    const f2 b2v = *reinterpret_cast<const f2*>(B2m + cls0);
+    int ylab[NSL];
+    f2 ytg[NSL];
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      if constexpr (LOSS == kLossCEIndex) yl[t] = reinterpret_cast<const int*>(ys)[16 * t + c];
-      else yf[t] = *reinterpret_cast<const f4*>(ys + (16 * t + c) * 16 + 4 * q);
+    for (int u = 0; u < NSL; ++u) {
+      const int sl = w + u * NW;
+      if (sl < NSL) {
+        const int R = 8 * sl + lrow;
+        if constexpr (LOSS == kLossCEIndex) ylab[u] = reinterpret_cast<const int*>(ys)[R];
+        else ytg[u] = *reinterpret_cast<const f2*>(ys + R * 16 + cls0);
+      }
+    }
+    // rows that take part (CE index: label not ignored), counted by every wave over all 32 rows
+    float inv;
+    bool none = false;
+    if constexpr (LOSS == kLossCEIndex) {
+      const int y32 = reinterpret_cast<const int*>(ys)[l & 31];
+      const int cnt = __popcll(__ballot(l < 32 && l < nb && y32 != a.ignore_index));
+      inv = cnt == B ? inv_full : 1.f / (float)(cnt > 0 ? cnt : 1);
+      none = cnt == 0;
+    } else {
+      inv = nb == B ? inv_full : 1.f / (float)(LOSS == kLossMSE ? nb * Dout : nb);
     }
     tick(1);
     __syncthreads();
@@ -640,118 +665,75 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       acc_bar += t - tmark;
       tmark = t;
     }
-    float zf[2][4];
-    // all partial reads in flight before the first add (a runtime-count loop waited on each)
-    f4 pz[4][2];
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      if (v < NW) {
-        const f4* src = reinterpret_cast<const f4*>(xbuf + (par * NW + v) * 512 + l * 4);
-        pz[v][0] = src[0];
-        pz[v][1] = src[64];
+    for (int u = 0; u < NSL; ++u) {
+      const int sl = w + u * NW;  // uniform
+      if (sl >= NSL) break;
+      const int R = 8 * sl + lrow, tr = R >> 4, cr = R & 15;
+      // logits: b2 + the NW partials in wave order (partials: lane (c', q') of tile tr holds
+      // classes 4q'..4q'+3 of row c'); all reads in flight before the first add
+      f2 pz[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        if (v < NW)
+          pz[v] = *reinterpret_cast<const f2*>(xbuf + (par * NW + v) * 512 + tr * 256 + ((lk >> 1) * 16 + cr) * 4 +
+                                                2 * (lk & 1));
+      f2 z = b2v;
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        if (v < NW) z += pz[v];
+      const bool rv = R < nb, ok0 = cls0 < Dout, ok1 = cls0 + 1 < Dout;
+      float g0, g1, ls;
+      if constexpr (LOSS == kLossMSE) {
+        const f2 y = ytg[u];
+        const float d0 = z[0] - y[0], d1 = z[1] - y[1];
+        g0 = (rv && ok0) ? 2.f * d0 : 0.f;
+        g1 = (rv && ok1) ? 2.f * d1 : 0.f;
+        ls = ((rv && ok0) ? d0 * d0 : 0.f) + ((rv && ok1) ? d1 * d1 : 0.f);
+      } else {
+        float m = fmaxf(ok0 ? z[0] : -INFINITY, ok1 ? z[1] : -INFINITY);
+        m = fmaxf(m, dpp_f<kDppXor1>(m));
+        m = fmaxf(m, dpp_f<kDppXor2>(m));
+        m = fmaxf(m, dpp_f<kDppHalfMirror>(m));
+        const float e0 = ok0 ? __builtin_amdgcn_exp2f((z[0] - m) * 1.4426950408889634f) : 0.f;
+        const float e1 = ok1 ? __builtin_amdgcn_exp2f((z[1] - m) * 1.4426950408889634f) : 0.f;
+        const float se = group_sum<8>(e0 + e1);
+        const float rse = __builtin_amdgcn_rcpf(se);  // softmax = e / se (v_rcp_f32); the log only feeds the loss
+        const float lse = m + __builtin_amdgcn_logf(se) * 0.6931471805599453f;
+        if constexpr (LOSS == kLossCEIndex) {
+          const int y = ylab[u];
+          const bool use = rv && y != a.ignore_index;
+          g0 = (use && ok0) ? e0 * rse - (cls0 == y ? 1.f : 0.f) : 0.f;
+          g1 = (use && ok1) ? e1 * rse - (cls0 + 1 == y ? 1.f : 0.f) : 0.f;
+          ls = (use && cls0 == y) ? lse - z[0] : ((use && cls0 + 1 == y) ? lse - z[1] : 0.f);
+        } else {  // soft targets: -(t . log_softmax(z)), grad = softmax * sum(t) - t
+          const f2 y = ytg[u];  // classes >= Dout stage as 0
+          const float sc = group_sum<8>(y[0] + y[1]) * rse;
+          g0 = (rv && ok0) ? e0 * sc - y[0] : 0.f;
+          g1 = (rv && ok1) ? e1 * sc - y[1] : 0.f;
+          ls = rv ? ((ok0 ? -y[0] * (z[0] - lse) : 0.f) + (ok1 ? -y[1] * (z[1] - lse) : 0.f)) : 0.f;
+        }
       }
-    }
-    f4 zs[2] = {b2v, b2v};
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {  // wave order: identical sums in every wave (vector adds: v_pk_add_f32)
-      if (v < NW) {
-        zs[0] += pz[v][0];
-        zs[1] += pz[v][1];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      zf[0][i] = zs[0][i];
-      zf[1][i] = zs[1][i];
+      g0 *= inv;
+      g1 *= inv;
+      // the row's loss (its 8 lanes' parts) into the loss ring: entry R of the step's 64 (32..63 stay 0)
+      ls = group_sum<8>(ls);
+      if (lk == 0) lring[(k & (kTpLossRing - 1)) * 64 + R] = (LOSS == kLossCEIndex && none) ? NAN : ls * inv;
+      // dZ for every wave: row-major (dH's A operand) and transposed with interleaved tiles (row
+      // 16 t + c at position 2 c + t; dW2's A operand and db2)
+      *reinterpret_cast<f2*>(dZr + R * kTpLDZ + cls0) = f2{g0, g1};
+      dZt[cls0 * LDT + 2 * cr + tr] = g0;
+      dZt[(cls0 + 1) * LDT + 2 * cr + tr] = g1;
     }
     tick(2);
-
-    // ---------------- loss and dL/dZ (classes 4q + i across lane groups, rows 16t + c)
+    __syncthreads();  // barrier 2: every slice of dZ is in LDS
     float g[2][4];
-    float lsum = 0.f;
-    int cnt = 0;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int row = 16 * t + c;
-      const bool rv = row < nb;
-      if constexpr (LOSS == kLossMSE) {
-        const f4 y = yf[t];
+      const f4 gg = *reinterpret_cast<const f4*>(dZr + (16 * t + c) * kTpLDZ + 4 * q);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const bool ok = rv && 4 * q + i < Dout;
-          const float df = zf[t][i] - y[i];
-          lsum += ok ? df * df : 0.f;
-          g[t][i] = ok ? 2.f * df : 0.f;
-        }
-      } else {
-        float m = -INFINITY;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) m = (4 * q + i < Dout) ? fmaxf(m, zf[t][i]) : m;
-        m = rows4_max(m);
-        float se = 0.f, e[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          e[i] = (4 * q + i < Dout) ? __builtin_amdgcn_exp2f((zf[t][i] - m) * 1.4426950408889634f) : 0.f;
-          se += e[i];
-        }
-        se = rows4_sum(se);
-        const float rse = __builtin_amdgcn_rcpf(se);  // softmax = e / se (v_rcp_f32); the log only feeds the loss
-        if constexpr (LOSS == kLossCEIndex) {
-          const int y = yl[t];
-          const bool use = rv && y != a.ignore_index;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int cls = 4 * q + i;
-            g[t][i] = (use && cls < Dout) ? e[i] * rse - (cls == y ? 1.f : 0.f) : 0.f;
-          }
-          if (w == 0) {
-            const float lse = m + __builtin_amdgcn_logf(se) * 0.6931471805599453f;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) lsum += (use && 4 * q + i == y) ? lse - zf[t][i] : 0.f;
-          }
-          cnt += __popcll(__ballot(use && q == 0));
-        } else {  // soft targets: -(t . log_softmax(z)), grad = softmax * sum(t) - t
-          const f4 y = yf[t];
-          float ts = 0.f;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) ts += y[i];  // classes >= Dout stage as 0
-          ts = rows4_sum(ts);
-          const float sc = ts * rse;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const bool ok = rv && 4 * q + i < Dout;
-            g[t][i] = ok ? e[i] * sc - y[i] : 0.f;
-          }
-          if (w == 0) {
-            const float lse = m + __builtin_amdgcn_logf(se) * 0.6931471805599453f;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) lsum += (rv && 4 * q + i < Dout) ? -y[i] * (zf[t][i] - lse) : 0.f;
-          }
-        }
-      }
+      for (int i = 0; i < 4; ++i) g[t][i] = gg[i];
     }
-    // 1 / count: the full batch's value precomputed (uniform branch; the IEEE division
-    // only for a short batch or ignored targets)
-    float inv;
-    if constexpr (LOSS == kLossCEIndex) {
-      cnt = __builtin_amdgcn_readfirstlane(cnt);
-      if (cnt == B) inv = inv_full;
-      else inv = 1.f / (float)(cnt > 0 ? cnt : 1);
-    } else {
-      if (nb == B) inv = inv_full;
-      else inv = 1.f / (float)(LOSS == kLossMSE ? nb * Dout : nb);
-    }
-    if (w == 0)  // this lane's share of the step's loss (added up by flush_losses, off the critical path)
-      lring[(k & (kTpLossRing - 1)) * 64 + l] = (LOSS == kLossCEIndex && cnt == 0) ? NAN : lsum * inv;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      g[0][i] *= inv;
-      g[1][i] *= inv;
-    }
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) Tdz[(4 * q + i) * LDT + 16 * t + c] = g[t][i];
     tick(3);
 
     // ---------------- dH = dZ . W2[:, slice]: dZ's result layout is the A operand
@@ -764,20 +746,25 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
         xa[t][mt] = *reinterpret_cast<const f4*>(st + St::XT_OFF + (16 * mt + c) * LDXT + 16 * t + 4 * q);
-    f4 dhh[2][2] = {{{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}, {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}}};
+    f4 dh[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      dhh[0][s & 1] = mfma4(g[0][s], w2t[s], dhh[0][s & 1]);
-      dhh[1][s & 1] = mfma4(g[1][s], w2t[s], dhh[1][s & 1]);
+      dh[0] = mfma4(g[0][s], w2t[s], dh[0]);
+      dh[1] = mfma4(g[1][s], w2t[s], dh[1]);
     }
-    f4 dh[2] = {dhh[0][0] + dhh[0][1], dhh[1][0] + dhh[1][1]};
     // transposed reads: H[row 16t + 4q + s][unit c] (ReLU mask, dW2's B) and
-    // dZ[row 16t + 4q + s][class c] (dW2's A)
+    // dZ[row 16t + 4q + s][class c] (dW2's A); interleaved tiles: positions 8q .. 8q+7 hold
+    // rows 16t + 4q + s at 2s + t
     f4 hT[2], dzT[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      hT[t] = *reinterpret_cast<const f4*>(Th + c * LDT + 16 * t + 4 * q);
-      dzT[t] = *reinterpret_cast<const f4*>(Tdz + c * LDT + 16 * t + 4 * q);
+    {
+      const f4 h0 = *reinterpret_cast<const f4*>(Th + c * LDT + 8 * q);
+      const f4 h1 = *reinterpret_cast<const f4*>(Th + c * LDT + 8 * q + 4);
+      const f4 d0 = *reinterpret_cast<const f4*>(dZt + c * LDT + 8 * q);
+      const f4 d1 = *reinterpret_cast<const f4*>(dZt + c * LDT + 8 * q + 4);
+      hT[0] = f4{h0[0], h0[2], h1[0], h1[2]};
+      hT[1] = f4{h0[1], h0[3], h1[1], h1[3]};
+      dzT[0] = f4{d0[0], d0[2], d1[0], d1[2]};
+      dzT[1] = f4{d0[1], d0[3], d1[1], d1[3]};
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -788,27 +775,19 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     db2 = rows4_sum(db2);
 
     // ---------------- dW2 = dZ^T . H (K = rows), dW1aug^T = Xaug^T . dH (K = rows)
-    // one accumulation chain per row tile (t), added at the end: independent MFMAs pipeline
-    f4 gw2p[2], gw1p[2][MT];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      gw2p[t] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) gw1p[t][mt] = f4{0.f, 0.f, 0.f, 0.f};
-    }
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-#pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        gw2p[t] = mfma4(dzT[t][s], hT[t][s], gw2p[t]);
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) gw1p[t][mt] = mfma4(xa[t][mt][s], dh[t][s], gw1p[t][mt]);
-      }
-    }
-    const f4 gw2 = gw2p[0] + gw2p[1];
+    f4 gw2 = {0.f, 0.f, 0.f, 0.f};
     f4 gw1[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) gw1[mt] = gw1p[0][mt] + gw1p[1][mt];
+    for (int mt = 0; mt < MT; ++mt) gw1[mt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        gw2 = mfma4(dzT[t][s], hT[t][s], gw2);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) gw1[mt] = mfma4(xa[t][mt][s], dh[t][s], gw1[mt]);
+      }
+    }
     mfma_settle();  // uniform branches follow (hb, tick, the all-reduce's failed check)
     tick(4);
 
@@ -944,7 +923,8 @@ bool tp_vec_x(const FusedMlpArgs& a) {
 size_t tp_lds_bytes(const FusedMlpArgs& a, const PersistArgs& p) {
   const int NW = a.H / 16;
   const size_t fl = (size_t)3 * al4(p.num_samples) + (size_t)3 * tp_stage_floats(tp_mt(a)) +
-                    (size_t)2 * NW * 64 * 8 + (size_t)NW * tp_wave_floats() + 48 + 3 + (size_t)kTpLossRing * 64;
+                    (size_t)2 * NW * 64 * 8 + (size_t)NW * tp_wave_floats() + 48 + 3 + (size_t)kTpLossRing * 64 +
+                    (size_t)32 * kTpLDZ + (size_t)16 * kTpLDT;
   return fl * sizeof(float);
 }
 

@@ -72,6 +72,11 @@ for s in "$@"; do
                for i in 1 2 3; do for r in 1 2 3; do
                  jstep rehab 120 env PTDT_BENCH_REHEARSALS=$r python3 bench.py --steps 20 --warmup 5 --no_ref --no_mlp_side
                done; done ;;
+    pinab)     # A/B: default vs the persistent launches pinned to one CU (PTDT_BENCH_PIN_CU), interleaved
+               for i in 1 2 3 4; do
+                 jstep pinab 120 python3 bench.py --steps 20 --warmup 5 --no_ref --no_mlp_side
+                 jstep pinab 120 env PTDT_BENCH_PIN_CU=0 python3 bench.py --steps 20 --warmup 5 --no_ref --no_mlp_side
+               done ;;
     default)   jstep bench_default 300 python3 bench.py ;;
     stamps)    jstep stamps 300 python3 bench.py --steps 20000 --warmup 2000 --stamps --no_mlp_side
                jstep stamps 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --stamps ;;

@@ -292,8 +292,9 @@ def test_graph_replay_with_miopen_memset_nodes_tracks_eager(pg, dev):
     print(f"replay vs eager {gap:.2e}, eager vs eager {floor:.2e}, memset nodes {gs.memset_nodes}")
     # the first replay's forward runs the snapshot's weights: same loss as the eager step's
     assert abs(rl[0] - el[0]) <= 1e-3 * abs(el[0])
-    # then within 2e-3, or within the noise two eager runs show (without the rewrite: ~1e19)
-    assert gap <= max(2e-3, 3 * floor), (gap, floor)
+    # then within 2e-3, or within the noise two eager runs show (the atomic solvers' order differs
+    # run to run; measured 3-9e-3 after 4 steps); without the rewrite the loss is ~1e19 by replay 2
+    assert gap <= max(2e-3, 5 * floor) and gap < 0.05, (gap, floor)
 
 
 # the memset nodes of the captured ResNet-50 step (benchmarks/graph_memset_probe.py): value 0, byte

@@ -249,7 +249,8 @@ def test_native_resnet_ddp_multi_gpu_equals_accumulated_single_process(tmp_path,
     spawn(_mgpu_workers.resnet_ddp, args=(world, free_port(), str(tmp_path), True), nprocs=world)
     res = _ranks(tmp_path, world)
     assert all(r["in_sync"] for r in res)
-    assert all(r["rebuilt"] and r["buckets"] >= 2 for r in res)
+    if world > 1:  # (a one-rank reducer issues no all-reduce and keeps its first bucketing)
+        assert all(r["rebuilt"] and r["buckets"] >= 2 for r in res)
     assert res[0]["sinks"] > 0 and res[0]["deferred"]
     ref = _mgpu_workers.resnet_reference(world, gpu=True)
     torch.testing.assert_close(res[0]["params"], ref, rtol=2e-2, atol=2e-3)

@@ -133,7 +133,7 @@ def main(argv=None):
                 if r >= 2:
                     rows.append({"total_us": w_us})
                 else:
-                    first.append(w_us)
+                    first.append({"total_us": w_us})
                 continue
             if var.startswith("wait"):
                 h0, h1, waited = plan.launch_wait_at(a.steps, pos, int(var[4:]))
@@ -155,9 +155,6 @@ def main(argv=None):
             if var in ("wait3", "wait5"):  # hipExtLaunchKernel: no launcher stamps
                 l0, l1 = h0, h1
             tl = hm.read()
-            if r < 2:  # first reps of a variant: reported apart, not in the medians
-                first.append(round((h2 - h0) / 1e3, 3))
-                continue
             row = {"total_us": (h2 - h0) / 1e3, "py_to_hip_call_us": (l0 - h0) / 1e3,
                    "hipLaunchKernel_us": (l1 - l0) / 1e3, "hip_return_to_py_us": (h1 - l1) / 1e3}
             if var != "nostamp" and all(t > 0 for t in tl[:4]):
@@ -176,12 +173,15 @@ def main(argv=None):
                 if seen is not None and seen > 0:
                     row["end_store_seen_by_host_us"] = (seen - x) / 1e3
                     row["sync_after_seen_us"] = (h2 - seen) / 1e3
+            if r < 2:  # first reps of a variant: reported apart (full breakdown), not in the medians
+                first.append({k: round(v, 3) for k, v in row.items()})
+                continue
             rows.append(row)
         keys = rows[0].keys()
         med = {k: round(statistics.median(rw[k] for rw in rows if k in rw), 3) for k in keys}
         lo = {k: round(min(rw[k] for rw in rows if k in rw), 3) for k in ("total_us",)}
         lines.append({"what": "timeline", "variant": var, "steps": a.steps, "reps": len(rows), "median": med,
-                      "min_total_us": lo["total_us"], "first_reps_total_us": first})
+                      "min_total_us": lo["total_us"], "first_reps": first})
     for ln in lines:
         s = json.dumps(ln)
         print(s, flush=True)
