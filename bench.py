@@ -278,14 +278,9 @@ def run_persistent(args, rank, world, dev, comm):
         # fit, so the timed launch below is not the first of its kind in this process
         # (PTDT_BENCH_REHEARSALS: into how many such launches the W steps are split; interleaved A/B at
         # the driver's W = 5: 1 -> 28.2-30.9 us window, 2 -> 25.0-26.1, 3 -> 24.8-26.1; default 3)
-        reh = max(1, min(n_warm, int(os.environ.get("PTDT_BENCH_REHEARSALS", "3"))))
         if n_warm <= chunk:
-            p0 = 0
             with pin_ctx:
-                for r in range(reh):
-                    k = n_warm // reh + (1 if r < n_warm % reh else 0)
-                    _untimed(comm, dev, lambda k=k, p0=p0: plan.launch_at(k, p0))
-                    p0 += k
+                _rehearse(comm, dev, plan, n_warm)
         else:
             for d in range(0, n_warm, chunk):
                 plan.launch(min(chunk, n_warm - d))
@@ -385,7 +380,7 @@ def _mlp_side(args, rank, world, dev, comm, xg):
     n_w, n_t = max(args.warmup, 1), args.steps
     losses = torch.zeros(max(n_w, n_t), device=dev)
     plan = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses)
-    _untimed(comm, dev, lambda: plan.launch_at(n_w, 0))
+    _rehearse(comm, dev, plan, n_w)
     t = _timed(comm, dev, lambda: plan.launch_at(n_t, n_w), label="mlp_side")
     failed = xg is not None and _xgmi_failed(comm, dev, xg, "MLP side measurement")
     return {"mlp_us_per_step": None if failed else round(1e6 * t / n_t, 3),
@@ -569,6 +564,17 @@ def _untimed(comm, dev, fn) -> None:
         spin.wait()
     fn()
     _sync(dev)
+
+
+def _rehearse(comm, dev, plan, n_warm: int) -> None:
+    """Run exactly ``n_warm`` warm-up steps of a persistent plan (positions 0 .. n_warm-1) as
+    PTDT_BENCH_REHEARSALS launches through the timed region's own sequence (_untimed)."""
+    reh = max(1, min(n_warm, int(os.environ.get("PTDT_BENCH_REHEARSALS", "3"))))
+    p0 = 0
+    for r in range(reh):
+        k = n_warm // reh + (1 if r < n_warm % reh else 0)
+        _untimed(comm, dev, lambda k=k, p0=p0: plan.launch_at(k, p0))
+        p0 += k
 
 
 def _timed(comm, dev, fn, label: str = "headline"):

@@ -90,6 +90,14 @@ for s in "$@"; do
                share wstamps 2 --steps 20000 --warmup 2000 --stamps --no_mlp_side
                share wstamps 4 --steps 20000 --warmup 2000 --stamps --no_mlp_side
                unset PTDT_EXT_PATH ;;
+    tpab)      # A/B of this tree vs tools/bin/_C_base.so (an earlier commit's build), shared-GPU rehearsals, interleaved
+               for r in 1 2; do for W in 2 4 8; do
+                 share tpab_cur $W --model mlp --steps 2000 --warmup 200 --no_ref
+                 export PTDT_EXT_PATH=$PWD/tools/bin/_C_base.so
+                 share tpab_base $W --model mlp --steps 2000 --warmup 200 --no_ref
+                 unset PTDT_EXT_PATH
+               done; done ;;
+    linshare)  for W in 2 4 8; do share linshare $W --steps 2000 --warmup 200 --no_ref; done ;;
     share_fused) share share_fused 2 --engine fused --steps 2000 --warmup 200
                share share_fused 4 --engine fused --model mlp --steps 2000 --warmup 200 ;;
     engines)   jstep engines 300 python3 bench.py --engine fused --steps 2000 --warmup 200

@@ -1,5 +1,6 @@
 """Worker bodies for the multi-GPU tests (one process per GPU, RCCL over xGMI).
 Importable without a GPU; every function runs in a spawned process."""
+import contextlib
 import os
 
 import torch
@@ -185,11 +186,13 @@ def _init_any(rank, world, port, gpu: bool):
 RESNET_CFG = {"layers": (1, 1, 1, 1), "classes": 10, "batch": 2, "image": 32, "steps": 3, "lr": 0.05}
 
 
-def resnet_ddp(rank, world, port, out_dir, gpu=True):
+def resnet_ddp(rank, world, port, out_dir, gpu=True, accum=1, ref=False):
     """Native ResNet DDP (small Bottleneck ResNet) on cuda:rank: channels_last, bf16 autocast, FusedSGD
     with bf16 weight shadows -- so the grad sinks, the deferred bf16->fp32 gradient casts and the bucket
     rebuild after iteration 0 all run at world > 1 (VERDICT r4 #6a). Each rank trains on its B rows of
-    a shared global batch. ``gpu=False``: the same host logic on CPU / gloo (fp32, no shadows)."""
+    a shared global batch. ``gpu=False``: the same host logic on CPU / gloo (fp32, no shadows).
+    ``accum > 1`` (world 1): the reference -- the same native path, each step accumulating ``accum``
+    micro-batches of B rows under ``no_sync`` with the loss scaled by 1/accum; ``ref`` saves to ref.pt."""
     dev, comm = _init_any(rank, world, port, gpu)
     from pytorch_distributed_training_tutorials_amd.models.resnet import Bottleneck, ResNet
     from pytorch_distributed_training_tutorials_amd.ops.loss import cross_entropy
@@ -209,28 +212,33 @@ def resnet_ddp(rank, world, port, out_dir, gpu=True):
     opt = FusedSGD(model.parameters(), lr=c["lr"], momentum=0.9, weight_decay=1e-4, bf16_shadow=gpu)
     g = torch.Generator().manual_seed(0)
     B, S = c["batch"], c["steps"]
-    X = torch.randn(S, B * world, 3, c["image"], c["image"], generator=g)
-    Y = torch.randint(0, c["classes"], (S, B * world), generator=g)
+    G = world * accum
+    X = torch.randn(S, B * G, 3, c["image"], c["image"], generator=g)
+    Y = torch.randint(0, c["classes"], (S, B * G), generator=g)
     losses = []
     for it in range(S):
-        xs = X[it, rank * B:(rank + 1) * B].to(dev)
-        if gpu:
-            xs = xs.contiguous(memory_format=torch.channels_last)
-        ys = Y[it, rank * B:(rank + 1) * B].to(dev)
         ddp.zero_grad()
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=gpu, cache_enabled=False):
-            out = ddp(xs)
-        loss = cross_entropy(out.float(), ys)
-        loss.backward()
+        for a in range(accum):
+            r = rank * accum + a
+            xs = X[it, r * B:(r + 1) * B].to(dev)
+            if gpu:
+                xs = xs.contiguous(memory_format=torch.channels_last)
+            ys = Y[it, r * B:(r + 1) * B].to(dev)
+            sync = ddp.no_sync() if a + 1 < accum else contextlib.nullcontext()
+            with sync:
+                with torch.autocast("cuda", dtype=torch.bfloat16, enabled=gpu, cache_enabled=False):
+                    out = ddp(xs)
+                loss = cross_entropy(out.float(), ys) / accum
+                loss.backward()
         opt.step()
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
     if gpu:
         torch.cuda.synchronize()
     flat = torch.cat([p.detach().float().reshape(-1) for p in model.parameters()])
     torch.save({"params": flat.cpu(), "in_sync": _digest_equal(comm, flat), "losses": losses,
                 "buckets": len(ddp.bucket_sizes_bytes()), "rebuilt": bool(ddp._rebuilt),
                 "sinks": len(getattr(ddp, "_sink_params", [])), "deferred": bool(getattr(ddp, "_defer", False))},
-               os.path.join(out_dir, f"r{rank}.pt"))
+               os.path.join(out_dir, "ref.pt" if ref else f"r{rank}.pt"))
     destroy_process_group()
 
 

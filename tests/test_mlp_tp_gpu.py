@@ -101,10 +101,12 @@ def test_tp_engine_matches_torch_fp32(dev, B, Din, H, Dout, loss, bias):
     torch.testing.assert_close(eng.G, gref, rtol=1e-3, atol=1e-5)
 
 
-@pytest.mark.parametrize("N,B", [(32, 32), (40, 32), (300, 16)])
-def test_tp_engine_short_epochs_and_plan_splits(dev, N, B):
+@pytest.mark.parametrize("N,B,H", [(32, 32, 64), (40, 32, 64), (300, 16, 64), (32, 32, 16), (40, 32, 16)])
+def test_tp_engine_short_epochs_and_plan_splits(dev, N, B, H):
     """One or two steps per epoch (list entries produced S+1 steps ahead), cached
-    epoch lists across launches: equals one long launch."""
+    epoch lists across launches: equals one long launch. H = 16 runs one compute wave
+    + the helper (two waves: the prologue's Feistel keys must not depend on the wave
+    count), after launches of other sample counts on the same device (stale LDS key tags)."""
     from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
     from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP
     from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
@@ -113,7 +115,7 @@ def test_tp_engine_short_epochs_and_plan_splits(dev, N, B):
     out = []
     for splits in ((37,), (1, 2, 3, 5, 26)):
         torch.manual_seed(1)
-        eng = FusedMLPStep(ToyMLP(20, 64, 10).to(dev), loss="ce_index", lr=0.05, momentum=0.9)
+        eng = FusedMLPStep(ToyMLP(20, H, 10).to(dev), loss="ce_index", lr=0.05, momentum=0.9)
         sampler = DeviceDistributedSampler(N, 1, 0, seed=4, device=dev)
         cursor = torch.zeros(2, dtype=torch.int32, device=dev)
         losses = torch.zeros(37, device=dev)

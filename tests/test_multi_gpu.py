@@ -252,8 +252,12 @@ def test_native_resnet_ddp_multi_gpu_equals_accumulated_single_process(tmp_path,
     if world > 1:  # (a one-rank reducer issues no all-reduce and keeps its first bucketing)
         assert all(r["rebuilt"] and r["buckets"] >= 2 for r in res)
     assert res[0]["sinks"] > 0 and res[0]["deferred"]
-    ref = _mgpu_workers.resnet_reference(world, gpu=True)
-    torch.testing.assert_close(res[0]["params"], ref, rtol=2e-2, atol=2e-3)
+    # reference: the same native bf16 path in ONE process, accumulating the ranks' micro-batches
+    # under no_sync (BatchNorm sees the same rows as on each rank); the CPU dry run of this case
+    # (tests/test_ddp_cpu.py) checks the host logic against a plain fp32 torch loop instead
+    spawn(_mgpu_workers.resnet_ddp, args=(1, free_port(), str(tmp_path), True, world, True), nprocs=1)
+    ref = torch.load(os.path.join(tmp_path, "ref.pt"), weights_only=True)
+    torch.testing.assert_close(res[0]["params"], ref["params"], rtol=2e-2, atol=5e-3)
 
 
 @pytest.mark.parametrize("world", [1, 2, 4])
