@@ -118,11 +118,7 @@ __device__ __forceinline__ float sgd1(float& w, float& m, float g, bool first, f
 // every lane re-polls its whole set), contributions are summed in rank order (own value
 // from the register): bit-identical replicas. Padded values (zero gradients) travel too.
 template <int NV, int G>
-__device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq, float (&v)[NV], int wave, int lane,
-                                                uint32_t live, int last_src) {
-  // live: bit k set when value k of this lane is a real gradient (padded inputs / classes are zero
-  // on every rank: neither pushed nor polled); value NV-1 (db2, identical in every wave and lane
-  // group) is pushed by one source slot per class and read by every lane from `last_src`
+__device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq, float (&v)[NV], int wave, int lane) {
   const int parity = (int)(seq & 1u);
   const uint64_t hi = (uint64_t)seq << 32;
   const bool drop = x.drop_push != 0u && seq >= x.drop_push;
@@ -133,14 +129,9 @@ __device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq,
         (uint64_t PTDT_GLOBAL*)x.peers[p] + (int64_t)(parity * x.world + x.rank) * x.max_elems + base;
 #pragma unroll
     for (int k = 0; k < NV; ++k)
-      if ((live >> k) & 1u)
-        __hip_atomic_store(dst + k * 64, hi | (uint64_t)__float_as_uint(v[k]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(dst + k * 64, hi | (uint64_t)__float_as_uint(v[k]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  // polled values: own slots for the first NV-1 (when real), the source slot for the last one; a
-  // padded value is 0 on every rank (taken as present, adds 0)
-  const uint32_t pol = (live & ((1u << (NV - 1)) - 1u)) | (last_src >= 0 ? 1u << (NV - 1) : 0u);
-  const int last_off = last_src >= 0 ? last_src : base;
   float acc[NV];
 #pragma unroll
   for (int k = 0; k < NV; ++k) acc[k] = 0.f;
@@ -155,13 +146,10 @@ __device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq,
       for (int g = 0; g < G; ++g) {
         const bool real = i0 + g < np;  // uniform
         const uint64_t PTDT_GLOBAL* src =
-            (const uint64_t PTDT_GLOBAL*)x.local + (int64_t)(parity * x.world + (real ? peer(i0 + g) : 0)) * x.max_elems;
+            (const uint64_t PTDT_GLOBAL*)x.local + (int64_t)(parity * x.world + (real ? peer(i0 + g) : 0)) * x.max_elems + base;
 #pragma unroll
         for (int k = 0; k < NV; ++k)
-          w[g][k] = (real && ((pol >> k) & 1u))
-                        ? __hip_atomic_load(src + (k + 1 < NV ? base + k * 64 : last_off), __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_SYSTEM)
-                        : hi;
+          w[g][k] = real ? __hip_atomic_load(src + k * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : hi;
       }
     };
     issue();
@@ -829,22 +817,8 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
           for (int mt = 0; mt < MT; ++mt) v[mt * 4 + i] = gv1[mt][i];
           v[4 * MT + i] = gv2[i];
         }
-        v[4 * MT + 4] = db2;  // b2[class c]: the same value in every wave and lane group
-        // real values only: dW1aug inputs < Din (+ the bias column), dW2 / db2 classes < Dout; db2
-        // travels once per class (wave 0, lane group 0) and every lane reads that slot
-        uint32_t live = 0u;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const int in = 16 * mt + 4 * q + i;
-            if (in < Din + (hb ? 1 : 0)) live |= 1u << (mt * 4 + i);
-          }
-          if (4 * q + i < Dout) live |= 1u << (4 * MT + i);
-        }
-        if (w == 0 && q == 0 && c < Dout) live |= 1u << (4 * MT + 4);
-        const int db2_src = c < Dout ? (4 * MT + 4) * 64 + c : -1;  // wave 0's slot of lane (c, 0)
-        failed = !tp_allreduce_lm<NV, 2>(a.ar, seq, v, w, l, live, db2_src);
+        v[4 * MT + 4] = db2;  // b2[class c]: the same value in every wave (identical loss in every wave)
+        failed = !tp_allreduce_lm<NV, (LOSS == kLossCEIndex && VX) ? 3 : 2>(a.ar, seq, v, w, l);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
 #pragma unroll
