@@ -333,8 +333,9 @@ def run_persistent(args, rank, world, dev, comm):
             phase["prologue_split_us"] = [round(v[k] * 0.01 / nl, 2) for k in (11, 12, 13)]
         if which.startswith("tp"):  # each wave's barrier + logit-sum phase (load balance)
             nl = math.ceil(args.steps / chunk)
-            # kernel entry -> lists/init done, -> past the barrier, -> step 0 staged (10 ns ticks, per launch)
-            phase["prologue_split_us"] = [round(v[k] * 0.01 / nl, 2) for k in (17, 18, 19)]
+            # kernel entry -> resident state loaded, -> list e0, -> list e0+1 + keys, -> lists/init done,
+            # -> past the barrier, -> step 0 staged (10 ns ticks, per launch; waits forced at each mark)
+            phase["prologue_split_us"] = [round(v[k] * 0.01 / nl, 2) for k in (20, 21, 22, 17, 18, 19)]
             nw = int(which.split(":")[1].split("w")[0])
             phase["logits_loss_per_wave"] = [round(x / args.steps, 1) for x in v[9:9 + nw]]
             phase["barrier_wait_per_wave"] = [round(x / args.steps, 1) for x in v[9 + nw:9 + 2 * nw]]

@@ -39,7 +39,7 @@ struct XgmiArgs {
   uint32_t max_polls;                    // poll budget per slot (kXgmiMaxPolls; PTDT_XGMI_MAX_POLLS)
   uint32_t drop_push;                    // fault injection: from collective seq drop_push on (0: never) skip
                                          // pushes to other ranks (PTDT_FAULT_XGMI_DROP_RANK / _SEQ)
-  uint32_t flags;                        // kXgmiPair: the single-wave engine's packed exchange at world 2
+  uint32_t flags;                        // kXgmiPair: the single-wave engine's packed-words exchange (world 2..8)
 };
 constexpr uint32_t kXgmiPair = 1u;  // PTDT_XGMI_PAIR=0 clears it (A/B against the chunked exchange)
 

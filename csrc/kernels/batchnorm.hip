@@ -213,43 +213,64 @@ __device__ __forceinline__ float ld_sc1(const float* p, bool fence = false) {
   return __hip_atomic_load((gfloat_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Last block of a channel tile: sum the gx row-block partials (two [gx][C] slabs)
-// of the tile's `width` channels with ALL threads -- thread (part, ch) adds
-// partials part, part + P, ... with 4 loads in flight, then the P part-sums are
-// added in part order through LDS (deterministic). Result in threads t < width.
+// Last block of a channel tile: sum the gx row-block partials (two [gx][C] slabs) of the tile's
+// `width` channels with ALL threads. Thread (part, quad) adds rows part, part + P, ... of 4
+// consecutive channels (P = kRed / (width / 4) parts), kCombineRows rows x 2 slabs of 16-B loads in
+// flight per thread, so the whole combine is ceil(gx / (P kCombineRows)) round trips -- one for
+// every ResNet-50 shape. (Round 4's form, one channel per thread and 4 rows in flight, took up to
+// 32 dependent round trips on the wide layer-1 tiles: gx = 256 row blocks, 256 channels.) The P
+// part-sums are then added in part order through LDS (deterministic). Result in threads t < width.
+constexpr int kCombineRows = 4;
+constexpr size_t kCombineLds = (size_t)2 * kRed * 4 * sizeof(double);  // 2 slabs x P x width doubles
+__device__ __forceinline__ void ld2_sc1(const float* p, float& x, float& y, bool fence) {
+  uint64_t u;
+  if (fence) u = *reinterpret_cast<const uint64_t*>(p);
+  else u = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  x = __uint_as_float((uint32_t)u);
+  y = __uint_as_float((uint32_t)(u >> 32));
+}
 __device__ __forceinline__ void combine_partials(const float* ws, int gx, int C, int cbase, int width, float* sh,
                                                  double& s0, double& s1, bool fence) {
-  const int P = kRed / width;
-  const int t = threadIdx.x, ch = t % width, part = t / width;
-  const int c = cbase + ch;
-  double a0 = 0.0, a1 = 0.0;
-  const float* w0 = ws;
-  const float* w1 = ws + (int64_t)gx * C;
+  const int nq = width >> 2;
+  const int P = kRed / nq;
+  const int t = threadIdx.x, qd = t % nq, part = t / nq;
+  const int c = cbase + 4 * qd;
+  double a0[4] = {0.0, 0.0, 0.0, 0.0}, a1[4] = {0.0, 0.0, 0.0, 0.0};
   if (part < P && c < C) {
-    int b = part;
-    for (; b + 3 * P < gx; b += 4 * P) {
-      float u[4], v[4];
+    const float* w0 = ws + c;
+    const float* w1 = ws + (int64_t)gx * C + c;
+    for (int b = part; b < gx; b += kCombineRows * P) {
+      float u[kCombineRows][4], v[kCombineRows][4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        u[k] = ld_sc1(w0 + (int64_t)(b + k * P) * C + c, fence);
-        v[k] = ld_sc1(w1 + (int64_t)(b + k * P) * C + c, fence);
+      for (int k = 0; k < kCombineRows; ++k) {
+        const int r = b + k * P;
+        if (r < gx) {
+          ld2_sc1(w0 + (int64_t)r * C, u[k][0], u[k][1], fence);
+          ld2_sc1(w0 + (int64_t)r * C + 2, u[k][2], u[k][3], fence);
+          ld2_sc1(w1 + (int64_t)r * C, v[k][0], v[k][1], fence);
+          ld2_sc1(w1 + (int64_t)r * C + 2, v[k][2], v[k][3], fence);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) u[k][i] = v[k][i] = 0.f;
+        }
       }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        a0 += (double)u[k];
-        a1 += (double)v[k];
-      }
-    }
-    for (; b < gx; b += P) {
-      a0 += (double)ld_sc1(w0 + (int64_t)b * C + c, fence);
-      a1 += (double)ld_sc1(w1 + (int64_t)b * C + c, fence);
+      for (int k = 0; k < kCombineRows; ++k)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          a0[i] += (double)u[k][i];
+          a1[i] += (double)v[k][i];
+        }
     }
   }
   __syncthreads();  // the reduction slots in sh are free again
   double* d = reinterpret_cast<double*>(sh);
   if (part < P) {
-    d[part * width + ch] = a0;
-    d[(P + part) * width + ch] = a1;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      d[part * width + 4 * qd + i] = a0[i];
+      d[(P + part) * width + 4 * qd + i] = a1[i];
+    }
   }
   __syncthreads();
   s0 = s1 = 0.0;
@@ -659,6 +680,14 @@ __global__ void __launch_bounds__(kThreads) bn_bwd_apply_kernel(const T* __restr
   }
 }
 
+// LDS of a reduction launch: the row-sum slots (2 x kRed x V floats, then the last-block flag)
+// and the combine's part sums (kCombineLds) share one array
+template <typename T>
+size_t red_lds() {
+  const size_t rows = (size_t)2 * kRed * VecIO<T>::V * sizeof(float) + 16;
+  return rows > kCombineLds ? rows : kCombineLds;
+}
+
 int apply_grid(int64_t nvec) {
   const int au = apply_unroll(), cap = apply_block_cap();
   int64_t per = (int64_t)kThreads * (cap > 0 ? 4 : au);  // >= 4 vectors per thread when capped
@@ -693,7 +722,7 @@ hipError_t fwd_impl(const BnFwdArgs& a, hipStream_t s) {
   constexpr int V = VecIO<T>::V;
   if (a.C % V != 0) return hipErrorInvalidValue;
   const Geom g = geom<T>(a.M, a.C);
-  const size_t sh_red = (size_t)2 * kRed * V * sizeof(float) + 16;
+  const size_t sh_red = red_lds<T>();
   if (!a.stats_ready) {
     hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(g.gx, g.gy), dim3(kRed), sh_red, s, static_cast<const T*>(a.x),
                        a.M, a.C, g.TC, g.RPI, g.rows_per_block, interleave_rows() | (dir(1) << 1), a.workspace,
@@ -749,7 +778,7 @@ hipError_t apply_impl(const void* x, const void* res, void* y, const float* scal
 template <typename T, int MASK, bool ADD2>
 hipError_t bwd_launch(const BnBwdArgs& a, const Geom& g, hipStream_t s) {
   constexpr int V = VecIO<T>::V;
-  const size_t sh_red = (size_t)2 * kRed * V * sizeof(float) + 16;
+  const size_t sh_red = red_lds<T>();
   const T* dy = static_cast<const T*>(a.dy);
   const T* dy2 = static_cast<const T*>(a.dy2);
   const T* x = static_cast<const T*>(a.x);

@@ -222,7 +222,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   const TpDims d = tp_dims(a, pa);
   // diagnostic (ST): kernel entry and three prologue marks (10 ns ticks; waits forced at each mark)
   const int64_t r_entry = ST ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
-  int64_t r_pro[3] = {0, 0, 0};
+  int64_t r_pro[6] = {0, 0, 0, 0, 0, 0};
   auto pstamp = [&](int k) {
     if constexpr (ST) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
@@ -317,6 +317,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     failed = AR && *a.ar.err != 0;
   };
   if (w < NW) load_state();
+  pstamp(0);  // resident state loaded
 
   // ---- sampler lists: epoch e0 whole, epoch e0+1 up to batch j0 (entries of later
   // positions are produced S+1 steps ahead inside the loop)
@@ -333,6 +334,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     return pos;
   };
   rank_epoch_indices_or(given_list(pa, e0), list(e0), Nn, pa.W, pa.rank, ns, pa.seed, e0, pa.shuffle, tid, T, lc);
+  pstamp(1);  // epoch e0's list in LDS
   {
     const int upto = min((j0 + 1) * B, ns);
     const int32_t* g1 = given_list(pa, e0 + 1);
@@ -378,6 +380,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     if (tid < 3) keys_store(e0 + 1 + tid);
     else fkeys[(e0 & 3) * 12 + 8] = -0x7fffffff - 1;
   }
+  pstamp(2);  // epoch e0+1's list up to the cursor, Feistel keys
   // staged batch slots: zeros, and the constant-1 input column (b1 rides in W1's
   // column Din) in X and X^T; the per-step writes only touch columns < Din
   // (16-B zero stores, then the constant-1 entries after a barrier: the per-element index
@@ -395,9 +398,9 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       else st[St::XT_OFF + Din * LDXT + r] = 1.f;
     }
   }
-  pstamp(0);  // lists, keys, staging-slot init (and the compute waves' state loads) done
+  pstamp(3);  // lists, keys, staging-slot init (and the compute waves' state loads) done
   __syncthreads();
-  pstamp(1);
+  pstamp(4);
   if (tid == 0 && pa.idx == nullptr) list_cache_publish(lc, e0);
 
   // Helper wave (w == NW): owns the sampler lists and the batch staging, so the NW compute
@@ -527,7 +530,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     stage_write(0);
   }
   __syncthreads();
-  pstamp(2);  // step 0's batch staged: the loop starts
+  pstamp(5);  // step 0's batch staged: the loop starts
 
   const float inv_full = 1.f / (float)(LOSS == kLossMSE ? B * Dout : B);
   const int ce0 = e0, cj0 = j0;
@@ -895,8 +898,13 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       for (int k = 0; k < 7; ++k) pa.stamps[k] += acc_t[k];
       pa.stamps[7] += (int64_t)__builtin_amdgcn_s_memtime() - t_begin;
       pa.stamps[8] += (int64_t)__builtin_amdgcn_s_memrealtime() - r_begin;
-      if (pa.stamps_n >= 20)  // prologue marks relative to kernel entry: [17] lists/init [18] barrier [19] staged
-        for (int k = 0; k < 3; ++k) pa.stamps[17 + k] += r_pro[k] - r_entry;
+      // prologue marks relative to kernel entry: [17] lists/init [18] barrier [19] staged, [20] state
+      // loaded [21] list e0 [22] list e0+1 + keys
+      if (pa.stamps_n >= 23)
+        for (int k = 0; k < 3; ++k) {
+          pa.stamps[17 + k] += r_pro[3 + k] - r_entry;
+          pa.stamps[20 + k] += r_pro[k] - r_entry;
+        }
     }
     if (a.opt_step) *a.opt_step = opt_step;
     if (AR) *a.ar.seq = seq;

@@ -97,6 +97,22 @@ for s in "$@"; do
                  share tpab_base $W --model mlp --steps 2000 --warmup 200 --no_ref
                  unset PTDT_EXT_PATH
                done; done ;;
+    bnab)      # BN kernels + ResNet-50 step: this tree vs tools/bin/_C_base.so, interleaved
+               for r in 1 2; do
+                 jstep bnab_cur 180 python3 benchmarks/bn_kernel_bench.py
+                 jstep bnab_base 180 env PTDT_EXT_PATH=$PWD/tools/bin/_C_base.so python3 benchmarks/bn_kernel_bench.py
+               done ;;
+    resab)     for r in 1 2; do
+                 jstep resab_cur 600 python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5
+                 jstep resab_base 600 env PTDT_EXT_PATH=$PWD/tools/bin/_C_base.so python3 benchmarks/resnet_ddp.py --steps 20 --warmup 5
+               done ;;
+    linab)     # single-wave engine exchange: this tree vs tools/bin/_C_base.so, shared-GPU rehearsals, interleaved
+               for r in 1 2; do for W in 2 4 8; do
+                 share linab_cur $W --steps 2000 --warmup 200 --no_ref --no_mlp_side
+                 export PTDT_EXT_PATH=$PWD/tools/bin/_C_base.so
+                 share linab_base $W --steps 2000 --warmup 200 --no_ref --no_mlp_side
+                 unset PTDT_EXT_PATH
+               done; done ;;
     linshare)  for W in 2 4 8; do share linshare $W --steps 2000 --warmup 200 --no_ref; done ;;
     share_fused) share share_fused 2 --engine fused --steps 2000 --warmup 200
                share share_fused 4 --engine fused --model mlp --steps 2000 --warmup 200 ;;

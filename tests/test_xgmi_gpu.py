@@ -305,14 +305,18 @@ def test_mfma_mlp_engine_matches_workgroup_engine(dev, B, Din, H, Dout, loss):
     torch.testing.assert_close(out["mfma"][0], out["workgroup"][0], rtol=1e-4, atol=1e-5)
 
 
-def test_wave_engine_pair_exchange_equals_chunked(tmp_path):
-    """World 2: the single-wave engine's packed pair exchange (one store + one poll per step) and the
-    chunked per-row-slot exchange (PTDT_XGMI_PAIR=0) train to the same parameters (x0 + x1 either way)."""
-    world = 2
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_wave_engine_pair_exchange_equals_chunked(tmp_path, world):
+    """W ranks sharing the GPU: the single-wave engine's packed-words exchange (one store + one poll per
+    peer and step) and the chunked per-row-slot exchange (PTDT_XGMI_PAIR=0) train to the same bits (the
+    packed path sums the ranks in row16_sum's tree order), replicas in sync, per-step reference close."""
     got = {}
     for kind in ("linear", "linear_nopair"):
         d = tmp_path / kind
         d.mkdir()
         spawn(_workers.persistent_two_procs_one_gpu, args=(world, free_port(), str(d), kind), nprocs=world)
-        got[kind] = torch.load(os.path.join(d, "r0.pt"), weights_only=True)["persistent"]
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+        assert all(torch.equal(r["persistent"], res[0]["persistent"]) for r in res)
+        torch.testing.assert_close(res[0]["persistent"], res[0]["per_step"], rtol=1e-5, atol=1e-5)
+        got[kind] = res[0]["persistent"]
     assert torch.equal(got["linear"], got["linear_nopair"])
