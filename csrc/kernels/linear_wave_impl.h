@@ -382,20 +382,17 @@ __device__ __forceinline__ bool ll_exchange_packed(const PackPlan<NT>& pp, const
   return ok;
 }
 
-// Packed-words exchange of layout F at 2 <= world <= 8 (round 4's world-2 pair exchange, tools/
-// exchange_bench.hip variant 4, generalised): the rank's npw <= 64 values (DOUT*Din weights, then the
-// biases) are staged in LDS and travel as npw consecutive LL words in ONE store instruction per peer
-// (lane = word: 168 B = 2 cache lines per peer for Linear(20,1)), and come back with ONE poll
-// instruction per peer, every peer's poll in flight together -- against the chunked exchange's
-// per-row-slot stores and polls (W = 2 rehearsal: 1,799 vs 2,369 cycles, profiles/r3_allreduce.md).
-// The sum over ranks is row16_sum's tree with the rank values in slots 0..7 (slots 8..15 zero):
-// ((v0 + v4) + (v2 + v6)) + ((v1 + v5) + (v3 + v7)) after v_j + 0 -- the chunked path's bits, on
-// every rank. xs: LDS [128] (staging, then the averages).
+// Pair exchange of layout F at world 2 (tools/exchange_bench.hip variant 4): the rank's npw <= 64
+// values (DOUT*Din weights, then the biases) are staged in LDS and travel as npw consecutive LL
+// words in ONE store instruction to the peer, and come back with ONE poll instruction -- against
+// the chunked exchange's per-row-slot stores and polls (W = 2 rehearsal: 1,799 vs 2,369 cycles,
+// profiles/r3_allreduce.md). The two-term sum x0 + x1 is the chunked path's row sum over
+// {x0, x1, 0, ...} (adding zeros is exact), so both ranks -- and both paths -- get the same values
+// (up to the sign of an exact zero). xs: LDS [128] (staging, then the averages).
 template <int KP, int DOUT>
 __device__ __forceinline__ bool ll_exchange_pair(const XgmiArgs& x, uint32_t seq, int q, int i, int lane, int Din,
                                                  float (&gW)[DOUT][KP], float (&gb)[DOUT], float* xs, float inv_w,
                                                  bool drop) {
-#pragma clang fp contract(off)
   const int k0 = q * KP, nW = DOUT * Din, npw = nW + DOUT;
   if (i == 0) {
 #pragma unroll
@@ -409,47 +406,30 @@ __device__ __forceinline__ bool ll_exchange_pair(const XgmiArgs& x, uint32_t seq
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // one wave: its LDS ops complete in order
   const bool on = lane < npw;
   const float mine = on ? xs[lane] : 0.f;
-  const int W = x.world, me = x.rank, parity = (int)(seq & 1u);
+  const int parity = (int)(seq & 1u), peer = 1 - x.rank;
   const uint64_t hi = (uint64_t)seq << 32;
   if (!drop && on) {
+    uint64_t PTDT_GLOBAL* base = nullptr;  // uniform selects, no scratch copy of peers[]
 #pragma unroll
-    for (int r = 0; r < kXgmiMaxRanks; ++r)  // constant indices into peers[]: no scratch copy
-      if (r < W && r != me)
-        __hip_atomic_store((uint64_t PTDT_GLOBAL*)x.peers[r] + (int64_t)(parity * W + me) * x.max_elems + lane,
-                           hi | __float_as_uint(mine), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int r = 0; r < 2; ++r)
+      if (peer == r) base = (uint64_t PTDT_GLOBAL*)x.peers[r];
+    __hip_atomic_store(base + (int64_t)(parity * 2 + x.rank) * x.max_elems + lane, hi | __float_as_uint(mine),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  const uint64_t PTDT_GLOBAL* const src = (const uint64_t PTDT_GLOBAL*)x.local + (on ? lane : 0);
-  uint64_t w[kXgmiMaxRanks];
-  auto issue = [&]() {
-#pragma unroll
-    for (int r = 0; r < kXgmiMaxRanks; ++r)
-      w[r] = (r < W && r != me)
-                 ? __hip_atomic_load(src + (int64_t)(parity * W + r) * x.max_elems, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_SYSTEM)
-                 : hi;
-  };
-  issue();
+  const uint64_t PTDT_GLOBAL* const src =
+      (const uint64_t PTDT_GLOBAL*)x.local + (int64_t)(parity * 2 + peer) * x.max_elems + (on ? lane : 0);
+  uint64_t w = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   bool ok = true;
-  for (uint32_t polls = 0;; ++polls) {
-    bool m = false;
-#pragma unroll
-    for (int r = 0; r < kXgmiMaxRanks; ++r) m |= (uint32_t)(w[r] >> 32) != seq;
-    if (__builtin_amdgcn_ballot_w64(on && m) == 0) break;
-    if (polls >= x.max_polls) {  // a peer is gone: fail loudly, never hang
+  for (uint32_t polls = 0; __builtin_amdgcn_ballot_w64(on && (uint32_t)(w >> 32) != seq) != 0; ++polls) {
+    if (polls >= x.max_polls) {  // the peer is gone: fail loudly, never hang
       __hip_atomic_store((int PTDT_GLOBAL*)x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       ok = false;
       break;
     }
-    issue();
+    w = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  float v[kXgmiMaxRanks];
-#pragma unroll
-  for (int r = 0; r < kXgmiMaxRanks; ++r) v[r] = r == me ? mine : (r < W ? __uint_as_float((uint32_t)w[r]) : 0.f);
-  float a8[kXgmiMaxRanks];
-#pragma unroll
-  for (int r = 0; r < kXgmiMaxRanks; ++r) a8[r] = v[r] + 0.f;  // + slot r + 8 (zero), as row16_sum adds it
-  const float tot = ((a8[0] + a8[4]) + (a8[2] + a8[6])) + ((a8[1] + a8[5]) + (a8[3] + a8[7]));
-  xs[64 + lane] = tot * inv_w;
+  const float other = __uint_as_float((uint32_t)w);
+  xs[64 + lane] = (x.rank == 0 ? mine + other : other + mine) * inv_w;  // rank order
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
   for (int c = 0; c < DOUT; ++c) {
@@ -1076,9 +1056,9 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   uint32_t seq = AR ? *ar.seq : 0u;
   bool failed = AR && *ar.err != 0;
   const float inv_w = 1.f / (float)world;
-  // one packed store + one poll per peer and step (ll_exchange_pair), staged through 128 LDS floats
+  // world 2: one packed store + one poll per step (ll_exchange_pair), staged through 128 LDS floats
   __shared__ float xpair[AR ? 128 : 1];
-  const bool pair = AR && world >= 2 && (ar.flags & kXgmiPair) != 0u && DOUT * (Din + 1) <= 64;
+  const bool pair = AR && world == 2 && (ar.flags & kXgmiPair) != 0u && DOUT * (Din + 1) <= 64;
 
   int ie = e0, ij = j0, barriers = 0;
   int sel_next[R], sel_y_next = 0, nb_next = 0;
@@ -1307,8 +1287,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
         for (int k = 0; k < KP; ++k) v[c][k] = i == my_rank ? gW[c][k] : 0.f;
       }
       // (ll_exchange_u / ll_exchange_packed / a separate pusher or poller wave measured no faster at
-      //  W = 8: tools/exchange_bench.hip, profiles/r3_exchange_bench*.jsonl; shapes with npw <= 64
-      //  take the packed-words path above)
+      //  W = 8: tools/exchange_bench.hip, profiles/r3_exchange_bench*.jsonl; W = 2 takes the pair path)
       const bool ok = ll_exchange<KP, DOUT>(i < world && i != my_rank, push_dst, poll_src, my_rank, i, world,
                                             max_elems, seq, k0, Din, hb, q == 0, 4 * KP != Din, gW, gb, v, vb,
                                             ar.err, ar.max_polls, ar.drop_push != 0u && seq >= ar.drop_push);

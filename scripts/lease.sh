@@ -113,6 +113,14 @@ for s in "$@"; do
                  share linab_base $W --steps 2000 --warmup 200 --no_ref --no_mlp_side
                  unset PTDT_EXT_PATH
                done; done ;;
+    wsab)      # single-wave engine phase split (stamps builds): this tree vs tools/bin/_C_stamps_base.so, W = 2, 4
+               for W in 2 4; do
+                 export PTDT_EXT_PATH=$PWD/tools/bin/_C_stamps.so
+                 share wsab_cur $W --steps 2000 --warmup 200 --stamps --no_mlp_side
+                 export PTDT_EXT_PATH=$PWD/tools/bin/_C_stamps_base.so
+                 share wsab_base $W --steps 2000 --warmup 200 --stamps --no_mlp_side
+                 unset PTDT_EXT_PATH
+               done ;;
     linshare)  for W in 2 4 8; do share linshare $W --steps 2000 --warmup 200 --no_ref; done ;;
     share_fused) share share_fused 2 --engine fused --steps 2000 --warmup 200
                share share_fused 4 --engine fused --model mlp --steps 2000 --warmup 200 ;;

@@ -307,9 +307,10 @@ def test_mfma_mlp_engine_matches_workgroup_engine(dev, B, Din, H, Dout, loss):
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_wave_engine_pair_exchange_equals_chunked(tmp_path, world):
-    """W ranks sharing the GPU: the single-wave engine's packed-words exchange (one store + one poll per
-    peer and step) and the chunked per-row-slot exchange (PTDT_XGMI_PAIR=0) train to the same bits (the
-    packed path sums the ranks in row16_sum's tree order), replicas in sync, per-step reference close."""
+    """W ranks sharing the GPU: at W = 2 the single-wave engine's packed pair exchange (one store + one
+    poll per step) and the chunked per-row-slot exchange (PTDT_XGMI_PAIR=0) train to the same bits
+    (x0 + x1 either way); at W = 4 / 8 both runs take the chunked exchange. Replicas in sync and close
+    to the per-step reference at every W."""
     got = {}
     for kind in ("linear", "linear_nopair"):
         d = tmp_path / kind
