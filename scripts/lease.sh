@@ -150,6 +150,22 @@ for s in "$@"; do
     mlpstamps) jstep mlpstamps 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --stamps --no_ref ;;
     prof)      prof driver 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
                prof reference 300 python3 bench.py --engine reference --steps 200 --warmup 20 ;;
+    tppmcab)   # TP engine PMC per step: this tree vs tools/bin/_C_r4.so (round-4 build), two passes each
+               for side in cur r4; do
+                 [ $side = r4 ] && export PTDT_EXT_PATH=$PWD/tools/bin/_C_r4.so
+                 pmc tp_${side}_1 "$P1" python3 bench.py --model mlp --steps 20000 --warmup 1 --no_mlp_side --no_ref
+                 pmc tp_${side}_2 "$P2" python3 bench.py --model mlp --steps 20000 --warmup 1 --no_mlp_side --no_ref
+                 unset PTDT_EXT_PATH
+               done
+               python3 tools/pmc_table.py --steps 20000 cur=$O/pmc_${T}_tp_cur_1,$O/pmc_${T}_tp_cur_2 \
+                 r4=$O/pmc_${T}_tp_r4_1,$O/pmc_${T}_tp_r4_2 > $O/${T}_tppmc.txt 2>&1
+               cat $O/${T}_tppmc.txt
+               rm -rf $O/pmc_${T}_tp_* ;;
+    tpw1ab)    # TP engine at W = 1, this tree vs the round-4 build, interleaved
+               for r in 1 2; do
+                 jstep tpw1_cur 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref
+                 jstep tpw1_r4 300 env PTDT_EXT_PATH=$PWD/tools/bin/_C_r4.so python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref
+               done ;;
     pmc_tp)    pmc tp1 "$P1" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side
                pmc tp2 "$P2" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side ;;
     pmc_wave)  pmc wave1 "$P1" python3 bench.py --steps 20000 --warmup 1 --no_mlp_side
