@@ -937,14 +937,35 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   constexpr bool SCATTER = DOUT == 1 && R > 1;
   constexpr int RY = SCATTER ? 1 : R;  // target rows a lane loads / computes the loss of
   extern __shared__ int elist[];
+  // The kernel arguments the prologue reads are loaded here in one batch, pinned by the empty asm
+  // (one wait for all), before the first branch. Left to the compiler, each scalar load followed
+  // the branch it fed (stamps, timeline, start position, momentum, ...): five dependent kernel-
+  // argument round trips before the first list load, and the start position came through a flat
+  // load of a pointer selected between the cursor and the argument (round-5 kernel-entry asm).
+  const int64_t r_now = (int64_t)__builtin_amdgcn_s_memrealtime();
+  int64_t* const stamps_p = pa.stamps;
+  int64_t* const tl_p = pa.tl;
+  const int B = a.B, Din = a.Din, ns_arg = pa.num_samples, has_start = pa.has_start, start_e = pa.start_e,
+            start_j = pa.start_j, has_bias_arg = a.has_bias, ldx_arg = a.ldx;
+  const int32_t* const cursor_p = pa.cursor;
+  const float* const P_arg = a.P;
+  const float* const mom_arg = a.mom;
+  const float* const X_arg = a.X;
+  const float momentum_arg = a.momentum;
+  asm volatile("" ::"s"(stamps_p), "s"(tl_p), "s"(B), "s"(Din), "s"(ns_arg), "s"(has_start), "s"(start_e), "s"(start_j),
+               "s"(has_bias_arg), "s"(ldx_arg), "s"(cursor_p), "s"(P_arg), "s"(mom_arg), "s"(X_arg), "s"(momentum_arg));
   // diagnostic (stamps): kernel entry, for the prologue share of a launch (stamps[10], 10 ns ticks)
-  const int64_t r_entry = pa.stamps != nullptr ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
-  tl_mark(pa.tl, 0);
+  const int64_t r_entry = stamps_p != nullptr ? r_now : 0;
+  if (tl_p != nullptr && threadIdx.x == 0)  // tl_mark(tl, 0) with the entry time taken above
+    __hip_atomic_store(tl_p, r_now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int B = a.B, Din = a.Din;
-  const int estride = al4(pa.num_samples);
-  const int S = (pa.num_samples + B - 1) / B;
-  const int e0 = pa.has_start ? pa.start_e : pa.cursor[0], j0 = pa.has_start ? pa.start_j : pa.cursor[1];
+  const int estride = al4(ns_arg);
+  const int S = (ns_arg + B - 1) / B;
+  int e0 = start_e, j0 = start_j;
+  if (!has_start) {  // the device cursor (plain launch): a load only on this path
+    e0 = cursor_p[0];
+    j0 = cursor_p[1];
+  }
   const int64_t pos0 = (int64_t)e0 * S + j0;
   const int n = pa.n_steps;
   const int T = (j0 + n - 1) / S;  // epoch barriers crossed (j0 < S)
@@ -952,7 +973,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   // diagnostic prologue split (stamps[11..13], 10 ns ticks): position known, list in LDS, after the barrier
   int64_t r_pro[3] = {0, 0, 0};
   auto pstamp = [&](int k) {
-    if (pa.stamps != nullptr) {
+    if (stamps_p != nullptr) {
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       r_pro[k] = (int64_t)__builtin_amdgcn_s_memrealtime();
     }
@@ -971,24 +992,48 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   const int lane = (int)threadIdx.x;
   const int q = (lane & 63) >> 4, i = lane & 15;  // feature group, row slot
   const int k0 = q * KP;
-  const bool hb = a.has_bias != 0;
-  const bool use_mom = a.mom != nullptr && a.momentum != 0.f;
+  const bool hb = has_bias_arg != 0;
+  const bool use_mom = mom_arg != nullptr && momentum_arg != 0.f;
   const int nW = DOUT * Din;
   float W[DOUT][KP], M[DOUT][KP], Wb[DOUT], Mb[DOUT];
   if (wave == 0) {
-    const auto P = gptr(a.P);
+    const auto P = gptr(P_arg);
 #pragma unroll
     for (int c = 0; c < DOUT; ++c) {
 #pragma unroll
       for (int k = 0; k < KP; ++k) {
         const bool in = k0 + k < Din;
         W[c][k] = in ? P[c * Din + k0 + k] : 0.f;
-        M[c][k] = (in && use_mom) ? gptr(a.mom)[c * Din + k0 + k] : 0.f;
+        M[c][k] = (in && use_mom) ? gptr(mom_arg)[c * Din + k0 + k] : 0.f;
       }
       Wb[c] = hb ? P[nW + c] : 0.f;
-      Mb[c] = (hb && use_mom) ? gptr(a.mom)[nW + c] : 0.f;
+      Mb[c] = (hb && use_mom) ? gptr(mom_arg)[nW + c] : 0.f;
     }
   }
+  // batch loads: x rows of this lane's feature group, the targets of its loss rows
+  const int rho_own = SCATTER ? (q & (R - 1)) : 0;  // the row whose loss this lane computes
+  const auto X = gptr(X_arg);
+  const int ldx = ldx_arg > 0 ? ldx_arg : Din;  // feature slots past Din read X's zero padding
+  auto load_batch = [&](Batch<R, KP, DOUT, RY>& f, const int (&sel)[R], int sel_y, int nb) {
+    f.nb = nb;
+#pragma unroll
+    for (int rho = 0; rho < R; ++rho) {
+      const auto xr = X + ((uint32_t)sel[rho] * (uint32_t)ldx + (uint32_t)k0);  // 32-bit offset (host-checked)
+#pragma unroll
+      for (int k = 0; k < KP; ++k) f.x[rho][k] = xr[k];
+    }
+#pragma unroll
+    for (int ry = 0; ry < RY; ++ry) {
+      const int s = SCATTER ? sel_y : sel[ry];
+      if constexpr (LOSS == kLossCEIndex) {
+        f.yi[ry] = reinterpret_cast<const int*>(a.Yi)[2 * (int64_t)s];  // low dword (see mlp_tp.hip)
+      } else {
+#pragma unroll
+        for (int c = 0; c < DOUT; ++c) f.y[ry][c] = gptr(a.Yf)[(int64_t)s * DOUT + c];
+      }
+    }
+  };
+  Batch<R, KP, DOUT, RY> buf[kNB];
   const ListCache lc{pa.lcache, pa.ltag, estride};
   rank_epoch_indices_or(given_list(pa, e0), list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
                      (int)threadIdx.x, kThreads, lc);
@@ -1037,11 +1082,8 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     return;
   }
 
-  const int rho_own = SCATTER ? (q & (R - 1)) : 0;  // the row whose loss this lane computes
   const float lr = a.lr, mu = a.momentum, damp = a.dampening, wd = a.weight_decay;
   const int nesterov = a.nesterov;
-  const auto X = gptr(a.X);
-  const int ldx = a.ldx > 0 ? a.ldx : Din;  // feature slots past Din read X's zero padding
 
   int opt_step = a.opt_step ? *a.opt_step : 0;
   const XgmiArgs& ar = a.ar;
@@ -1078,23 +1120,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     }
   };
   auto fetch = [&](Batch<R, KP, DOUT, RY>& f) {
-    f.nb = nb_next;
-#pragma unroll
-    for (int rho = 0; rho < R; ++rho) {
-      const auto xr = X + ((uint32_t)sel_next[rho] * (uint32_t)ldx + (uint32_t)k0);  // 32-bit offset (host-checked)
-#pragma unroll
-      for (int k = 0; k < KP; ++k) f.x[rho][k] = xr[k];
-    }
-#pragma unroll
-    for (int ry = 0; ry < RY; ++ry) {
-      const int sel = SCATTER ? sel_y_next : sel_next[ry];
-      if constexpr (LOSS == kLossCEIndex) {
-        f.yi[ry] = reinterpret_cast<const int*>(a.Yi)[2 * (int64_t)sel];  // low dword (see mlp_tp.hip)
-      } else {
-#pragma unroll
-        for (int c = 0; c < DOUT; ++c) f.y[ry][c] = gptr(a.Yf)[(int64_t)sel * DOUT + c];
-      }
-    }
+    load_batch(f, sel_next, sel_y_next, nb_next);
     read_index();
   };
 
@@ -1342,7 +1368,6 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     tk.tick(5);
   };
 
-  Batch<R, KP, DOUT, RY> buf[kNB];
   tk.start();
   read_index();
 #pragma unroll

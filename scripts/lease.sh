@@ -121,6 +121,11 @@ for s in "$@"; do
                  share wsab_base $W --steps 2000 --warmup 200 --stamps --no_mlp_side
                  unset PTDT_EXT_PATH
                done ;;
+    firstab)   # driver command with / without the host-planned first rows (PTDT_NO_FIRST_ROWS), interleaved
+               for r in 1 2 3; do
+                 jstep first_on 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
+                 jstep first_off 300 env PTDT_NO_FIRST_ROWS=1 python3 bench.py --gpus 1 --steps 20 --warmup 5
+               done ;;
     linshare)  for W in 2 4 8; do share linshare $W --steps 2000 --warmup 200 --no_ref; done ;;
     share_fused) share share_fused 2 --engine fused --steps 2000 --warmup 200
                share share_fused 4 --engine fused --model mlp --steps 2000 --warmup 200 ;;
