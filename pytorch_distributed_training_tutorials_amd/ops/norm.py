@@ -60,12 +60,45 @@ class ResidualLink:
     Ordering is autograd's own: the producer's backward runs only after every
     consumer of its output, the linking BN included, has run its backward. Each
     backward pass (a retained graph may run several) re-delivers: the consumer
-    stores, the producer takes and clears; None means the consumer did not run."""
+    stores, the producer takes and clears; None means the consumer did not run.
 
-    __slots__ = ("dres",)
+    Streams: autograd runs each backward on its forward's stream and synchronises the
+    gradients it passes along graph edges, but not this side channel. A link can span two
+    streams (a pipeline's stage streams on one device, where the stage hop ``a.to(dev)`` is
+    the same tensor and keeps its link), so the delivering stream is recorded and the taker
+    waits for it when it runs elsewhere (``take``)."""
+
+    __slots__ = ("dres", "stream")
 
     def __init__(self):
         self.dres = None
+        self.stream = None
+
+    def put(self, g):
+        """Store (or, when already delivered, add) a consumer's residual gradient."""
+        if self.dres is None:
+            self.dres = g
+            self.stream = torch.cuda.current_stream(g.device) if g.is_cuda else None
+        else:
+            self._sync(g.device)
+            self.dres = self.dres + g
+
+    def take(self, device):
+        """The delivered gradient (None if no consumer ran), ordered after its producer's stream."""
+        g, self.dres = self.dres, None
+        if g is not None:
+            self._sync(device, g)
+        self.stream = None
+        return g
+
+    def _sync(self, device, g=None):
+        if self.stream is None or device.type != "cuda":
+            return
+        cur = torch.cuda.current_stream(device)
+        if cur != self.stream:
+            cur.wait_stream(self.stream)
+            t = g if g is not None else self.dres
+            t.record_stream(cur)
 
 
 class _BatchNormActFn(torch.autograd.Function):
@@ -102,7 +135,7 @@ class _BatchNormActFn(torch.autograd.Function):
         dy2 = None
         if link_out is not None:  # a later block's residual gradient of our output
             # (None: that block's backward did not run -- its output does not reach the loss)
-            dy2, link_out.dres = link_out.dres, None
+            dy2 = link_out.take(dy.device)
             if dy2 is not None and dy2.stride() != dy.stride():
                 dy, dy2 = dy + dy2, None
         sinks = [None, None]
@@ -122,9 +155,10 @@ class _BatchNormActFn(torch.autograd.Function):
                                                ctx.tickets, sinks[0], sinks[1], dy2, mask)
         if link_in is not None and dres is not None:  # delivered to the residual's producer instead of autograd
             if link_in.dres is None:
-                link_in.dres, dres = dres, None
+                link_in.put(dres)
+                dres = None
             elif not ctx.needs_input_grad[3]:  # the link is taken (another consumer delivered): sum into it
-                link_in.dres = link_in.dres + dres
+                link_in.put(dres)
                 dres = None
             # else: autograd adds this one (returned below), as _GradLinkFn does
         return (dx if ctx.needs_input_grad[0] else None, dw if want_dw else None, db if want_dw else None,
@@ -144,7 +178,7 @@ class _GradLinkFn(torch.autograd.Function):
     def backward(ctx, g):
         link = ctx.link
         if link.dres is None:  # delivered: the producer adds it as dy2 inside its backward kernels
-            link.dres = g
+            link.put(g)
             return None, None
         return g, None  # the link is taken (another consumer delivered): autograd adds this one
 

@@ -126,6 +126,9 @@ for s in "$@"; do
                  jstep first_on 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
                  jstep first_off 300 env PTDT_NO_FIRST_ROWS=1 python3 bench.py --gpus 1 --steps 20 --warmup 5
                done ;;
+    sprep)     step sprep 300 python3 tools/stream_pipeline_repeat.py 25 ;;
+    sprep_r4)  step sprep_r4 300 env PTDT_EXT_PATH=$PWD/tools/bin/_C_r4.so python3 tools/stream_pipeline_repeat.py 25 ;;
+    sprep_nl)  step sprep_nl 300 env PTDT_BN_FENCE=1 python3 tools/stream_pipeline_repeat.py 10 ;;
     linshare)  for W in 2 4 8; do share linshare $W --steps 2000 --warmup 200 --no_ref; done ;;
     share_fused) share share_fused 2 --engine fused --steps 2000 --warmup 200
                share share_fused 4 --engine fused --model mlp --steps 2000 --warmup 200 ;;

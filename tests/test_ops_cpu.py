@@ -202,3 +202,20 @@ def test_conv_bn_act_falls_back_off_gpu():
     y = conv_bn_act(conv, bn, x, relu=True)
     torch.testing.assert_close(y, bn_act(bn2, conv2(x), relu=True))
     torch.testing.assert_close(bn.running_var, bn2.running_var)
+
+
+def test_residual_link_put_take_cpu():
+    """ops.norm.ResidualLink: the first consumer stores, a second one adds, the producer takes and
+    clears (CPU tensors: no stream bookkeeping); None when no consumer delivered."""
+    import torch
+
+    from pytorch_distributed_training_tutorials_amd.ops.norm import ResidualLink
+
+    link = ResidualLink()
+    assert link.take(torch.device("cpu")) is None
+    a, b = torch.ones(3), torch.full((3,), 2.0)
+    link.put(a)
+    link.put(b)
+    got = link.take(torch.device("cpu"))
+    assert torch.equal(got, torch.full((3,), 3.0))
+    assert link.dres is None and link.stream is None
