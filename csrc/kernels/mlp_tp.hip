@@ -333,14 +333,14 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     while (pos >= Nn) pos -= Nn;
     return pos;
   };
-  rank_epoch_indices_or(given_list(pa, e0), list(e0), Nn, pa.W, pa.rank, ns, pa.seed, e0, pa.shuffle, tid, T, lc);
-  pstamp(1);  // epoch e0's list in LDS
-  // epoch e0+1 whole, from the launch-to-launch cache when it holds it (its entries of positions
-  // before j0 are never produced by the helper; later ones are, with the same values): a launch
-  // that resumes where the last one stopped loads both lists instead of running the Feistel
-  // permutation for up to a whole epoch on the way to step 0 (round 4: ~1.8 us of the prologue)
-  rank_epoch_indices_or(given_list(pa, e0 + 1), list(e0 + 1), Nn, pa.W, pa.rank, ns, pa.seed, e0 + 1, pa.shuffle, tid, T,
-                        lc);
+  // epochs e0 and e0+1 whole, from the launch-to-launch cache when it holds them (both slots' loads
+  // in flight together). Epoch e0+1's entries of positions before j0 are never produced by the
+  // helper (later ones are, with the same values): a launch that resumes where the last one stopped
+  // loads both lists instead of running the Feistel permutation for up to a whole epoch on the way
+  // to step 0 (round 4: ~1.8 us of the prologue)
+  rank_epoch_indices_or2(given_list(pa, e0), list(e0), given_list(pa, e0 + 1), list(e0 + 1), Nn, pa.W, pa.rank, ns,
+                         pa.seed, e0, pa.shuffle, tid, T, lc);
+  pstamp(1);  // epochs e0 and e0+1 in LDS
   // Feistel keys of the epochs the producer will need (computed by one thread, one
   // epoch ahead of use: a produce call reads te, te + 1 and prepares te + 2)
   const bool feistel = pa.idx == nullptr && pa.shuffle;

@@ -142,6 +142,30 @@ __device__ __forceinline__ void rank_epoch_indices_or(const int32_t* given, int3
     for (int i = tid; i < num_samples; i += nt) dst[i] = out[i];
   }
 }
+// Epochs e and e + 1 into out0 / out1: rank_epoch_indices_or twice, except that with the cache
+// and no given lists both slots' entries and tags are loaded together (one round trip for two hits
+// instead of two in a row on the path to step 0).
+__device__ __forceinline__ void rank_epoch_indices_or2(const int32_t* given0, int32_t* out0, const int32_t* given1,
+                                                       int32_t* out1, uint32_t N, int W, int rank, int num_samples,
+                                                       uint64_t seed, int e, int shuffle, int tid, int nt,
+                                                       const ListCache& lc) {
+  if (given0 != nullptr || given1 != nullptr || lc.lists == nullptr || num_samples > kListSpec * nt) {
+    rank_epoch_indices_or(given0, out0, N, W, rank, num_samples, seed, e, shuffle, tid, nt, lc);
+    rank_epoch_indices_or(given1, out1, N, W, rank, num_samples, seed, e + 1, shuffle, tid, nt, lc);
+    return;
+  }
+  const int32_t* const src0 = lc.lists + (e & 1) * lc.stride;
+  const int32_t* const src1 = lc.lists + ((e + 1) & 1) * lc.stride;
+  const int tag0 = lc.tag[e & 1], tag1 = lc.tag[(e + 1) & 1];
+  int32_t v0[kListSpec], v1[kListSpec];
+  list_load(src0, num_samples, tid, nt, v0);
+  list_load(src1, num_samples, tid, nt, v1);
+  const bool hit0 = __builtin_amdgcn_readfirstlane(tag0) == e, hit1 = __builtin_amdgcn_readfirstlane(tag1) == e + 1;
+  if (hit0) list_store(out0, num_samples, tid, nt, v0);
+  if (hit1) list_store(out1, num_samples, tid, nt, v1);
+  if (!hit0) rank_epoch_indices_or(nullptr, out0, N, W, rank, num_samples, seed, e, shuffle, tid, nt, lc);
+  if (!hit1) rank_epoch_indices_or(nullptr, out1, N, W, rank, num_samples, seed, e + 1, shuffle, tid, nt, lc);
+}
 // Publish `epoch` as cached (one thread, after every builder thread's writes).
 __device__ __forceinline__ void list_cache_publish(const ListCache& lc, int epoch) {
   if (lc.lists != nullptr) lc.tag[epoch & 1] = epoch;
