@@ -176,6 +176,12 @@ for s in "$@"; do
                done ;;
     pmc_tp)    pmc tp1 "$P1" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side
                pmc tp2 "$P2" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side ;;
+    wavepmc)   # single-wave engine PMC per step (two passes) + table, then the pass directories removed
+               pmc wave_1 "$P1" python3 bench.py --steps 20000 --warmup 1 --no_mlp_side --no_ref
+               pmc wave_2 "$P2" python3 bench.py --steps 20000 --warmup 1 --no_mlp_side --no_ref
+               python3 tools/pmc_table.py --steps 20000 wave=$O/pmc_${T}_wave_1,$O/pmc_${T}_wave_2 > $O/${T}_wavepmc.txt 2>&1
+               cat $O/${T}_wavepmc.txt
+               rm -rf $O/pmc_${T}_wave_* ;;
     pmc_wave)  pmc wave1 "$P1" python3 bench.py --steps 20000 --warmup 1 --no_mlp_side
                pmc wave2 "$P2" python3 bench.py --steps 20000 --warmup 1 --no_mlp_side ;;
     bnsweep)   # BN kernel geometry / sweep-direction sweep (benchmarks/bn_kernel_bench.py), one process per setting
