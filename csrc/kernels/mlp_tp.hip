@@ -209,7 +209,13 @@ __host__ __device__ __forceinline__ int tp_stage_floats(int MT) { return 32 * (1
 // MT: 16-input tiles of the augmented input (Din inputs + a constant-1 column carrying b1);
 // VX: X rows staged as float4 chunks (Din and the row stride multiples of 4, X 16-B aligned);
 // ST: phase timers compiled in (diagnostic build: uniform branches around s_memtime)
-template <int MT, int LOSS, bool AR, bool VX, bool ST>
+// LDS position of input `in` in a staged X row: the two 2-bit fields of the input's index inside
+// its 16-input tile are swapped, so the b128 read at 16 mt + 4 q hands lane group q the inputs
+// 16 mt + 4 s + q (s = 0..3) -- fwd1's K-step s then covers 4 CONSECUTIVE inputs, and the K-steps
+// of the last tile that hold only padding (inputs >= Din + bias) can be skipped (KL)
+__host__ __device__ __forceinline__ int tp_xpos(int in) { return (in & ~15) + 4 * (in & 3) + ((in >> 2) & 3); }
+
+template <int MT, int LOSS, bool AR, bool VX, bool ST, int KL = 4>
 __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, PersistArgs pa) {
   // No implicit FMA contraction: the compiler may contract differently in a peeled
   // first iteration than in the loop body, which made a run split into several
@@ -297,7 +303,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int in = 16 * mt + 4 * q + i;
+        const int in = 16 * mt + 4 * i + q;  // fwd1's K-step i of tile mt, lane group q
         const int off = in < Din ? d.oW1 + unit * Din + in : (hb && in == Din ? d.ob1 + unit : -1);
         w1r[mt][i] = off >= 0 ? P[off] : 0.f;
         m1r[mt][i] = (off >= 0 && use_mom) ? a.mom[off] : 0.f;
@@ -389,7 +395,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     for (int e = tid; e < 3 * 64; e += T) {  // per slot: X[row][Din] and X^T[Din][row], rows 0..31
       float* const st = stage0 + (e >> 6) * St::FLOATS;
       const int r = e & 31;
-      if ((e & 63) < 32) st[r * LDX + Din] = 1.f;
+      if ((e & 63) < 32) st[r * LDX + tp_xpos(Din)] = 1.f;
       else st[St::XT_OFF + Din * LDXT + r] = 1.f;
     }
   }
@@ -508,11 +514,14 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       if (k < nkx) {
         const int row = xrow[k];
         if constexpr (VX) {
-          *reinterpret_cast<f4*>(st + row * LDX + 4 * xcol[k]) = xv[k];
+          // inputs 4 xcol + i land at positions (4 xcol & ~15) + 4 i + (xcol & 3) (tp_xpos)
+          float* const xr = st + row * LDX + ((4 * xcol[k]) & ~15) + (xcol[k] & 3);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) xr[4 * i] = xv[k][i];
 #pragma unroll
           for (int i = 0; i < 4; ++i) st[St::XT_OFF + (4 * xcol[k] + i) * LDXT + row] = xv[k][i];
         } else {
-          st[row * LDX + xcol[k]] = xv[k];
+          st[row * LDX + tp_xpos(xcol[k])] = xv[k];
           st[St::XT_OFF + xcol[k] * LDXT + row] = xv[k];
         }
       }
@@ -607,7 +616,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       for (int mt = 0; mt < MT; ++mt) {
         const f4 xb = *reinterpret_cast<const f4*>(st + (16 * t + c) * LDX + 16 * mt + 4 * q);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) h[t] = mfma4(w1r[mt][s], xb[s], h[t]);
+        for (int s = 0; s < (mt == MT - 1 ? KL : 4); ++s) h[t] = mfma4(w1r[mt][s], xb[s], h[t]);
       }
     }
     float ht[2][4];
@@ -753,7 +762,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
-        xa[t][mt] = *reinterpret_cast<const f4*>(st + St::XT_OFF + (16 * mt + c) * LDXT + 16 * t + 4 * q);
+        xa[t][mt] = *reinterpret_cast<const f4*>(st + St::XT_OFF + (16 * mt + 4 * (c & 3) + (c >> 2)) * LDXT + 16 * t + 4 * q);
     f4 dh[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -864,7 +873,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const int in = 16 * mt + 4 * q + i;
+      const int in = 16 * mt + 4 * i + q;
       const int off = in < Din ? d.oW1 + unit * Din + in : (hb && in == Din ? d.ob1 + unit : -1);
       if (off >= 0) {
         Pw[off] = w1r[mt][i];
@@ -911,12 +920,17 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
 
 int tp_mt(const FusedMlpArgs& a) { return a.Din + (a.has_bias ? 1 : 0) <= 16 ? 1 : 2; }
 
+// mt 3: two input tiles whose second one holds at most 8 real inputs (Din + bias <= 24): fwd1 runs
+// 2 of that tile's 4 K-steps (kernel KL = 2)
 template <int LOSS, bool AR, bool VX>
 const void* pick_mt(int mt, bool st) {
   if (st)  // phase timers (diagnostic instantiations; the all-reduce's share shows at world > 1)
     return mt == 1 ? (const void*)mlp_tp_kernel<1, LOSS, AR, VX, true>
-                   : (const void*)mlp_tp_kernel<2, LOSS, AR, VX, true>;
-  return mt == 1 ? (const void*)mlp_tp_kernel<1, LOSS, AR, VX, false> : (const void*)mlp_tp_kernel<2, LOSS, AR, VX, false>;
+                   : (mt == 3 ? (const void*)mlp_tp_kernel<2, LOSS, AR, VX, true, 2>
+                              : (const void*)mlp_tp_kernel<2, LOSS, AR, VX, true>);
+  return mt == 1 ? (const void*)mlp_tp_kernel<1, LOSS, AR, VX, false>
+                 : (mt == 3 ? (const void*)mlp_tp_kernel<2, LOSS, AR, VX, false, 2>
+                            : (const void*)mlp_tp_kernel<2, LOSS, AR, VX, false>);
 }
 
 template <bool AR, bool VX>
@@ -957,7 +971,7 @@ bool mlp_tp_supported(const FusedMlpArgs& a, const PersistArgs& p) {
 
 hipError_t mlp_tp_prepare(const FusedMlpArgs& a, const PersistArgs& p, PersistLaunch* out) {
   if (!mlp_tp_supported(a, p)) return hipErrorInvalidValue;
-  const int mt = tp_mt(a);
+  const int mt = (tp_mt(a) == 2 && a.Din + (a.has_bias ? 1 : 0) <= 24) ? 3 : tp_mt(a);  // 3: pick_mt
   const bool vx = tp_vec_x(a);
   const bool st = p.stamps != nullptr;
   const void* fn = a.ar.world > 1

@@ -178,6 +178,11 @@ for s in "$@"; do
                  jstep tpw1_cur 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref
                  jstep tpw1_r4 300 env PTDT_EXT_PATH=$PWD/tools/bin/_C_r4.so python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref
                done ;;
+    tpw1base)  # TP engine at W = 1, this tree vs tools/bin/_C_base.so, interleaved
+               for r in 1 2 3; do
+                 jstep tpw1_cur 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref
+                 jstep tpw1_base 300 env PTDT_EXT_PATH=$PWD/tools/bin/_C_base.so python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref
+               done ;;
     pmc_tp)    pmc tp1 "$P1" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side
                pmc tp2 "$P2" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side ;;
     wavepmc)   # single-wave engine PMC per step (two passes) + table, then the pass directories removed
