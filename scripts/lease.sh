@@ -183,6 +183,15 @@ for s in "$@"; do
                  jstep tpw1_cur 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref
                  jstep tpw1_base 300 env PTDT_EXT_PATH=$PWD/tools/bin/_C_base.so python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref
                done ;;
+    drvab)     # driver command + 20,000-step headline: this tree vs tools/bin/_C_base.so, interleaved
+               for r in 1 2 3; do
+                 jstep drvab_cur 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no_ref --no_mlp_side
+                 jstep drvab_base 300 env PTDT_EXT_PATH=$PWD/tools/bin/_C_base.so python3 bench.py --gpus 1 --steps 20 --warmup 5 --no_ref --no_mlp_side
+               done
+               for r in 1 2; do
+                 jstep drvab_cur 300 python3 bench.py --steps 20000 --warmup 2000 --no_ref --no_mlp_side
+                 jstep drvab_base 300 env PTDT_EXT_PATH=$PWD/tools/bin/_C_base.so python3 bench.py --steps 20000 --warmup 2000 --no_ref --no_mlp_side
+               done ;;
     pmc_tp)    pmc tp1 "$P1" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side
                pmc tp2 "$P2" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side ;;
     wavepmc)   # single-wave engine PMC per step (two passes) + table, then the pass directories removed
