@@ -225,6 +225,19 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   using St = TpStage<MT>;
   constexpr int LDX = St::LDX, LDXT = St::LDXT, LD2 = kTpLD2, LDT = kTpLDT;
   extern __shared__ float lds[];
+  // the pointers the prologue dereferences, loaded in one batch with the dimensions (pinned): left to
+  // the compiler, four dependent kernel-argument loads led the prologue (see linear_wave_impl.h)
+  {
+    const float* const x_arg = a.X;
+    const int64_t* const yi_arg = a.Yi;
+    const float* const p_arg = a.P;
+    const int32_t* const idx_arg = pa.idx;
+    const float* const losses_arg = pa.losses;
+    const int32_t* const lcache_arg = pa.lcache;
+    const int ns_arg = pa.num_samples, b_arg = a.B, din_arg = a.Din, h_arg = a.H;
+    asm volatile("" ::"s"(x_arg), "s"(yi_arg), "s"(p_arg), "s"(idx_arg), "s"(losses_arg), "s"(lcache_arg), "s"(ns_arg),
+                 "s"(b_arg), "s"(din_arg), "s"(h_arg));
+  }
   const TpDims d = tp_dims(a, pa);
   // diagnostic (ST): kernel entry and three prologue marks (10 ns ticks; waits forced at each mark)
   const int64_t r_entry = ST ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
@@ -329,7 +342,16 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   // positions are produced S+1 steps ahead inside the loop)
   const int ns = pa.num_samples;
   const int S = (ns + B - 1) / B;
-  const int e0 = pa.has_start ? pa.start_e : pa.cursor[0], j0 = pa.has_start ? pa.start_j : pa.cursor[1];
+  // the start position: from the arguments (launch_at), or the device cursor only on the plain-launch
+  // path -- written as a value select, the compiler loaded it through a flat load of a pointer
+  // selected between the two (a dependent memory round trip on every launch; see linear_wave_impl.h)
+  const int has_start = pa.has_start, start_e = pa.start_e, start_j = pa.start_j;
+  asm volatile("" ::"s"(has_start), "s"(start_e), "s"(start_j));
+  int e0 = start_e, j0 = start_j;
+  if (!has_start) {
+    e0 = pa.cursor[0];
+    j0 = pa.cursor[1];
+  }
   const int n = pa.n_steps;
   const uint32_t Nn = (uint32_t)pa.N;
   const ListCache lc{pa.lcache, pa.ltag, d.estride};

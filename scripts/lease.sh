@@ -192,6 +192,11 @@ for s in "$@"; do
                  jstep drvab_cur 300 python3 bench.py --steps 20000 --warmup 2000 --no_ref --no_mlp_side
                  jstep drvab_base 300 env PTDT_EXT_PATH=$PWD/tools/bin/_C_base.so python3 bench.py --steps 20000 --warmup 2000 --no_ref --no_mlp_side
                done ;;
+    sideab)    # driver command incl. the toy-MLP side measurement: this tree vs tools/bin/_C_base.so
+               for r in 1 2 3 4; do
+                 jstep sideab_cur 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no_ref
+                 jstep sideab_base 300 env PTDT_EXT_PATH=$PWD/tools/bin/_C_base.so python3 bench.py --gpus 1 --steps 20 --warmup 5 --no_ref
+               done ;;
     pmc_tp)    pmc tp1 "$P1" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side
                pmc tp2 "$P2" python3 bench.py --model mlp --persist tp --steps 20000 --warmup 1 --no_mlp_side ;;
     wavepmc)   # single-wave engine PMC per step (two passes) + table, then the pass directories removed
