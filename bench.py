@@ -70,6 +70,9 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=1e-2)
     ap.add_argument("--model", default="linear", choices=["linear", "mlp"],
                     help="linear = reference Linear(20,1)+soft CE; mlp = Linear(20,64)-ReLU-Linear(64,10)+CE")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="bf16: the toy MLP (--model mlp) on the bf16 tensor-parallel engine with "
+                         "torch.autocast(bfloat16) semantics and fp32 master weights (BASELINE config 2)")
     ap.add_argument("--engine", default="persistent", choices=["persistent", "fused", "autograd", "reference"])
     ap.add_argument("--graph_steps", type=int, default=128, help="target steps per captured hipGraph")
     ap.add_argument("--allreduce", default="auto", choices=["auto", "xgmi", "rccl"],
@@ -229,7 +232,7 @@ def run_persistent(args, rank, world, dev, comm):
             print("[bench] xGMI all-reduce unavailable; falling back to --engine fused --allreduce rccl", flush=True)
             args.allreduce = "rccl"
             return run_fused(args, rank, world, dev, comm)
-    eng = FusedMLPStep(model, loss=loss, lr=args.lr, comm=comm, xgmi=xg)
+    eng = FusedMLPStep(model, loss=loss, lr=args.lr, comm=comm, xgmi=xg, dtype=args.dtype)
     if world > 1:
         comm.broadcast(eng.P, 0)  # DDP init: rank 0's parameters everywhere
     sampler = DeviceDistributedSampler(len(ds), world, rank, seed=args.seed, device=dev)
@@ -357,14 +360,16 @@ def run_persistent(args, rank, world, dev, comm):
     if phase:
         extra["phase_timers"] = phase
     if args.model == "linear" and not args.no_mlp_side:
-        extra.update(_mlp_side(args, rank, world, dev, comm, xg))
+        extra.update(_mlp_side(args, rank, world, dev, comm, xg, "fp32"))
+        extra.update(_mlp_side(args, rank, world, dev, comm, xg, "bf16"))
     return t, extra
 
 
-def _mlp_side(args, rank, world, dev, comm, xg):
+def _mlp_side(args, rank, world, dev, comm, xg, dtype):
     """Side measurement (AFTER the headline, same protocol, same K/W): the toy MLP
     Linear(20,64)-ReLU-Linear(64,10) + CE + SGD on the persistent engine -- the
-    workload BASELINE.json's north star names; reported as extra keys only."""
+    workload BASELINE.json's north star names (config 2: bf16) -- in fp32 (keys mlp_*) and
+    on bf16 operands with autocast semantics (keys mlp_bf16_*); reported as extra keys only."""
     from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
     from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
 
@@ -373,7 +378,7 @@ def _mlp_side(args, rank, world, dev, comm, xg):
     model, loss = _build_model(side, dev)
     ds = _dataset(side, dev, loss)
     X, Y = ds.tensors
-    eng = FusedMLPStep(model, loss=loss, lr=args.lr, comm=comm, xgmi=xg)
+    eng = FusedMLPStep(model, loss=loss, lr=args.lr, comm=comm, xgmi=xg, dtype=dtype)
     if world > 1:
         comm.broadcast(eng.P, 0)
     sampler = DeviceDistributedSampler(len(ds), world, rank, seed=args.seed, device=dev)
@@ -382,13 +387,16 @@ def _mlp_side(args, rank, world, dev, comm, xg):
     losses = torch.zeros(max(n_w, n_t), device=dev)
     plan = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses)
     _rehearse(comm, dev, plan, n_w)
-    t = _timed(comm, dev, lambda: plan.launch_at(n_t, n_w), label="mlp_side")
-    failed = xg is not None and _xgmi_failed(comm, dev, xg, "MLP side measurement")
-    return {"mlp_us_per_step": None if failed else round(1e6 * t / n_t, 3),
-            "mlp_samples_per_s": None if failed else round(n_t * args.batch_size * world / t, 1),
-            "mlp_engine": eng.persistent_engine(args.batch_size, sampler),
-            "mlp_replicas_in_sync": _replicas_in_sync(comm, eng.P),
-            "mlp_final_loss": float(losses[n_t - 1].item())}
+    key = "mlp" if dtype == "fp32" else "mlp_bf16"
+    t = _timed(comm, dev, lambda: plan.launch_at(n_t, n_w), label=f"{key}_side")
+    failed = xg is not None and _xgmi_failed(comm, dev, xg, f"MLP side measurement ({dtype})")
+    return {f"{key}_us_per_step": None if failed else round(1e6 * t / n_t, 3),
+            f"{key}_samples_per_s": None if failed else round(n_t * args.batch_size * world / t, 1),
+            f"{key}_dtype": dtype + (" operands (torch.autocast(bfloat16) rounding points), fp32 master weights/SGD"
+                                     if dtype == "bf16" else ""),
+            f"{key}_engine": eng.persistent_engine(args.batch_size, sampler),
+            f"{key}_replicas_in_sync": _replicas_in_sync(comm, eng.P),
+            f"{key}_final_loss": float(losses[n_t - 1].item())}
 
 
 def _xgmi_failed(comm, dev, xg, where: str) -> bool:
@@ -493,7 +501,8 @@ def run_reference(args, rank, world, dev, comm, steps=None, warmup=None, label: 
             xs, ys = batch
             xs, ys = xs.to(dev), ys.to(dev)
             opt.zero_grad()
-            l = F.cross_entropy(ddp(xs), ys)
+            with torch.autocast(dev.type, dtype=torch.bfloat16, enabled=args.dtype == "bf16"):
+                l = F.cross_entropy(ddp(xs), ys)
             l.backward()
             opt.step()
 
@@ -627,7 +636,7 @@ def _record(args, world, value, elapsed, extra):
         "scaling": "weak",
         "vs_baseline": round(value / ref, 3) if (value and ref) else None,
         "vs_cpu_probe": round(value / base, 3) if (value and base) else None,
-        "dtype": "fp32",
+        "dtype": args.dtype,
         "data": "synthetic (uniform [0,1) features/targets generated on device, 2048 samples), random-init weights",
         "config": {"model": "ddp_gpus_torchrun toy: Linear(20,1) + F.cross_entropy(soft targets) + SGD(lr=1e-2)"
                    if args.model == "linear" else "toy MLP Linear(20,64)-ReLU-Linear(64,10) + CE + SGD",
@@ -661,6 +670,10 @@ def _comparator(args, rank, world, dev, comm):
 
 def main(argv=None):
     args = parse(argv)
+    if args.dtype == "bf16" and args.model != "mlp":
+        raise SystemExit("--dtype bf16 runs the toy MLP (--model mlp); the reference Linear(20,1) job is fp32")
+    if args.dtype == "bf16" and args.engine != "persistent":
+        raise SystemExit("--dtype bf16 runs on the persistent engine (the bf16 tensor-parallel kernel)")
     cpu = args.device == "cpu" or (args.device == "auto" and not torch.cuda.is_available())
     if cpu and args.engine != "reference":
         raise SystemExit("bench.py needs a GPU (MI355X) for the framework engines; --device cpu runs "

@@ -257,8 +257,9 @@ PersistBuild build_persistent(const Tensor& X, const c10::optional<Tensor>& Yf, 
     pa.ltag = pa.lcache + 2 * stride;
   }
   const bool wave = variant != kPersistWorkgroup && variant != kPersistMfma && variant != kPersistTp &&
-                    linear_wave_supported(a, pa);
-  const bool tp = !wave && (variant == kPersistAuto || variant == kPersistTp) && H > 0 && mlp_tp_supported(a, pa);
+                    variant != kPersistTpBf16 && linear_wave_supported(a, pa);
+  const bool tp = !wave && (variant == kPersistAuto || variant == kPersistTp || variant == kPersistTpBf16) && H > 0 &&
+                  mlp_tp_supported(a, pa);
   const bool mfma = !wave && !tp && mlp_mfma_persistent_supported(a, pa);
   TORCH_CHECK(wave || mfma || tp || (variant < kPersistWave),
               "persistent: the requested engine variant does not support this configuration");
@@ -474,12 +475,13 @@ std::string persistent_engine(int64_t B, int64_t Din, int64_t H, int64_t Dout, i
   pa.num_samples = (int)num_samples;
   pa.variant = (int)variant;
   pa.N = (int)std::max<int64_t>(num_samples, 1);
-  if (variant != kPersistWorkgroup && variant != kPersistMfma && variant != kPersistTp &&
+  if (variant != kPersistWorkgroup && variant != kPersistMfma && variant != kPersistTp && variant != kPersistTpBf16 &&
       linear_wave_supported(a, pa)) {
     int L = 0, R = 0, kp = 0;
     linear_wave_layout(a, pa, &L, &R, &kp);
     return "wave:L" + std::to_string(L) + "R" + std::to_string(R) + "K" + std::to_string(kp);
   }
+  if (variant == kPersistTpBf16 && H > 0 && mlp_tp_supported(a, pa)) return "tp_bf16:" + std::to_string(H / 16) + "waves";
   if ((variant == kPersistAuto || variant == kPersistTp) && H > 0 && mlp_tp_supported(a, pa))
     return "tp:" + std::to_string(H / 16) + "waves";
   if (variant != kPersistWorkgroup && mlp_mfma_persistent_supported(a, pa)) return "workgroup:mfma";

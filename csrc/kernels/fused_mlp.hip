@@ -1018,9 +1018,10 @@ hipError_t fused_mlp_persistent_prepare(const FusedMlpArgs& a, const PersistArgs
   if (a.ar.world > 1 && (num_params(a) > a.ar.max_elems || a.ar.world != p.W || a.ar.rank != p.rank))
     return hipErrorInvalidValue;
   if (p.variant != kPersistWorkgroup && p.variant != kPersistMfma && p.variant != kPersistTp &&
-      linear_wave_supported(a, p))
+      p.variant != kPersistTpBf16 && linear_wave_supported(a, p))
     return linear_wave_prepare(a, p, out);
-  if ((p.variant == kPersistAuto || p.variant == kPersistTp) && a.H > 0 && mlp_tp_supported(a, p))
+  if ((p.variant == kPersistAuto || p.variant == kPersistTp || p.variant == kPersistTpBf16) && a.H > 0 &&
+      mlp_tp_supported(a, p))
     return mlp_tp_prepare(a, p, out);
   if (p.variant >= kPersistWave && p.variant != kPersistMfma) return hipErrorInvalidValue;
   const size_t lds = fused_mlp_persistent_lds_bytes(a.B, a.Din, a.H, a.Dout, p.num_samples, a.ar.world);

@@ -107,9 +107,12 @@ constexpr int kWavePrefetch = 3;  // batches in flight in the wave engine (regis
 // workgroup (mlp_tp.hip: each wave owns 16 hidden units, every product on
 // MFMA, one barrier per step); kPersistAuto picks it for B <= 32, Din <= 32,
 // H in 16..64 step 16, Dout <= 16.
+// kPersistTpBf16: the same engine on bf16 operands (torch.autocast(bfloat16) rounding points,
+// fp32 master weights and SGD; v_mfma_f32_16x16x32_bf16 / 16x16x16_bf16). Never picked by
+// kPersistAuto: bf16 is requested explicitly (FusedMLPStep(dtype="bf16"), bench --dtype bf16).
 enum PersistVariant : int {
   kPersistAuto = 0, kPersistWorkgroup = 1, kPersistWave = 2, kPersistWaveRows = 3, kPersistWaveF = 4,
-  kPersistMfma = 5, kPersistTp = 6
+  kPersistMfma = 5, kPersistTp = 6, kPersistTpBf16 = 7
 };
 // The caller-provided list of `epoch` (clamped into the provided range), or nullptr.
 __device__ __forceinline__ const int32_t* given_list(const PersistArgs& p, int epoch) {

@@ -46,7 +46,8 @@ def _linears(model: nn.Module):
     raise ValueError("FusedMLPStep supports Linear or Linear-ReLU-Linear models; use the autograd engine otherwise")
 
 
-_VARIANTS = {"auto": 0, "workgroup": 1, "wave": 2, "wave_rows": 3, "wave_f": 4, "mfma": 5, "tp": 6}
+_VARIANTS = {"auto": 0, "workgroup": 1, "wave": 2, "wave_rows": 3, "wave_f": 4, "mfma": 5, "tp": 6, "tp_bf16": 7}
+DTYPES = ("fp32", "bf16")
 
 
 def _variant_id(variant: str | None) -> int:
@@ -59,8 +60,17 @@ def _variant_id(variant: str | None) -> int:
 class FusedMLPStep:
     def __init__(self, model: nn.Module, *, loss: str = "ce_soft", lr: float = 1e-2, momentum: float = 0.0,
                  dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False, comm=None,
-                 reduce: bool = True, defer_update: bool = True, ignore_index: int = -100, xgmi=None):
+                 reduce: bool = True, defer_update: bool = True, ignore_index: int = -100, xgmi=None,
+                 dtype: str = "fp32"):
+        """``dtype="bf16"``: the persistent engine runs the step with torch.autocast(bfloat16)
+        semantics on bf16 MFMA operands (fp32 master weights, momentum and SGD;
+        csrc/kernels/mlp_tp_impl.h) -- Linear-ReLU-Linear models on the tensor-parallel engine only."""
         layers, relu = _linears(model)
+        if dtype not in DTYPES:
+            raise ValueError(f"dtype must be one of {DTYPES}, got {dtype!r}")
+        self.dtype = dtype
+        if dtype == "bf16" and not relu:
+            raise ValueError("FusedMLPStep(dtype='bf16') runs Linear-ReLU-Linear models (the bf16 TP engine)")
         self.model = model
         self.layers = layers
         if loss not in LOSS_KINDS:
@@ -112,6 +122,8 @@ class FusedMLPStep:
     def step(self, X: torch.Tensor, Y: torch.Tensor, idx: torch.Tensor | None, B: int,
              loss_out: torch.Tensor | None = None):
         """One DDP step on rows ``idx[:B]`` of the resident dataset ``(X, Y)``."""
+        if self.dtype != "fp32":
+            raise NotImplementedError("the per-step fused kernel is fp32; dtype='bf16' runs the persistent engine")
         lo = self.loss_buf if loss_out is None else loss_out
         if self.xgmi is not None:
             # ONE launch: fwd + loss + bwd + xGMI all-reduce + SGD update
@@ -163,7 +175,7 @@ class FusedMLPStep:
         if self.xgmi is None and self.comm is not None and self.comm.world > 1:
             raise RuntimeError("the persistent engine needs the xGMI all-reduce for world > 1")
         ce_index = self.loss_kind == LOSS_KINDS["ce_index"]
-        vid = _variant_id(variant)
+        vid = self._vid(variant)
         X, padded = self._wave_input(X, batch_size, sampler, vid)
         done = 0
         while done < n_steps:
@@ -192,7 +204,7 @@ class FusedMLPStep:
         if self.xgmi is None and self.comm is not None and self.comm.world > 1:
             raise RuntimeError("the persistent engine needs the xGMI all-reduce for world > 1")
         ce_index = self.loss_kind == LOSS_KINDS["ce_index"]
-        vid = _variant_id(variant)
+        vid = self._vid(variant)
         X, padded = self._wave_input(X, batch_size, sampler, vid)
         self._pending = False
         # launch-to-launch cache of the epoch index lists (tags -1: empty): a launch
@@ -209,6 +221,17 @@ class FusedMLPStep:
             self.xgmi.handle if self.xgmi is not None else None, sampler.num_replicas, sampler.rank,
             sampler.num_samples, sampler.shuffle, sampler.seed, cursor, losses, stamps, vid, padded, idx, lcache,
             idx_e0)
+
+    def _vid(self, variant: str | None) -> int:
+        """Engine variant id; dtype="bf16" means the bf16 TP engine (and nothing else)."""
+        if self.dtype == "bf16":
+            if (variant or "tp_bf16") not in ("tp_bf16", "auto"):
+                raise ValueError(f"dtype='bf16' runs the 'tp_bf16' persistent engine, not {variant!r}")
+            return _VARIANTS["tp_bf16"]
+        vid = _variant_id(variant)
+        if vid == _VARIANTS["tp_bf16"]:
+            raise ValueError("the 'tp_bf16' engine needs FusedMLPStep(dtype='bf16')")
+        return vid
 
     def _wave_input(self, X, batch_size, sampler, vid):
         """The wave engine reads whole lane chunks (L lanes x K features per row):
@@ -234,7 +257,7 @@ class FusedMLPStep:
         """Which persistent engine :meth:`run_persistent` runs: "workgroup" or
         "wave:L<l>R<r>K<k>" (lanes per row, rows per lane group, features per lane)."""
         return self._C.persistent_engine(batch_size, self.Din, self.H, self.Dout, self.loss_kind,
-                                         sampler.num_samples, sampler.num_replicas, _variant_id(variant),
+                                         sampler.num_samples, sampler.num_replicas, self._vid(variant),
                                          self.has_bias)
 
     # ------------------------------------------------------------ optimizer state

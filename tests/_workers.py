@@ -468,3 +468,46 @@ def tuning_agree(rank, world, port, out_dir):
     torch.save({"got": got, "choices": tuning.choices(), "outside": outside, "mismatch": mismatch},
                os.path.join(out_dir, f"r{rank}.pt"))
     destroy_process_group()
+
+
+def tp_bf16_ranks_one_gpu(rank, world, port, out_dir):
+    """bf16 TP engine at world W on one shared GPU (gloo control plane, xGMI exchange over IPC)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
+    from pytorch_distributed_training_tutorials_amd.models.toy import ToyMLP
+    from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
+    from pytorch_distributed_training_tutorials_amd.parallel.comm import Communicator
+    from pytorch_distributed_training_tutorials_amd.parallel.xgmi import XgmiAllReduce
+
+    dev = torch.device("cuda", 0)
+    ctl = Communicator(device=torch.device("cpu"))
+    xg = XgmiAllReduce(ctl, dev, max_elems=4096)
+    X = torch.randn(300, 20, generator=torch.Generator().manual_seed(9)).to(dev)
+    Y = torch.randint(0, 10, (300,), generator=torch.Generator().manual_seed(10)).to(dev)
+    torch.manual_seed(5)
+    model = ToyMLP(20, 64, 10).to(dev)
+    init = [p.detach().cpu().clone() for p in model.parameters()]
+    eng = FusedMLPStep(model, loss="ce_index", lr=0.05, momentum=0.9, xgmi=xg, dtype="bf16")
+    sampler = DeviceDistributedSampler(300, world, rank, seed=3, device=dev)
+    orders = []
+    for e in range(10):
+        sampler.set_epoch(e)
+        idx = torch.zeros(sampler.num_samples, dtype=torch.int32, device=dev)
+        sampler.generate(idx)
+        orders.append(idx.cpu())
+    sampler.set_epoch(0)
+    cursor = torch.zeros(2, dtype=torch.int32, device=dev)
+    losses = torch.zeros(7, device=dev)
+    engine = eng.persistent_engine(16, sampler)
+    eng.run_persistent(X, Y, 23, 16, sampler, cursor, losses, max_steps_per_launch=7)
+    torch.cuda.synchronize()
+    xg.check()
+    torch.save({"engine": engine, "params": eng.P.cpu(), "init": init, "orders": orders, "X": X.cpu(), "Y": Y.cpu()},
+               os.path.join(out_dir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
