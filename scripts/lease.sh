@@ -173,6 +173,22 @@ for s in "$@"; do
                  r4=$O/pmc_${T}_tp_r4_1,$O/pmc_${T}_tp_r4_2 > $O/${T}_tppmc.txt 2>&1
                cat $O/${T}_tppmc.txt
                rm -rf $O/pmc_${T}_tp_* ;;
+    tpbfpmc)   # TP engine PMC per step: bf16 operands vs exact fp32 (same tree), two passes each
+               for dt in bf16 fp32; do
+                 pmc tp_${dt}_1 "$P1" python3 bench.py --model mlp --dtype $dt --steps 20000 --warmup 1 --no_ref
+                 pmc tp_${dt}_2 "$P2" python3 bench.py --model mlp --dtype $dt --steps 20000 --warmup 1 --no_ref
+               done
+               python3 tools/pmc_table.py --steps 20000 bf16=$O/pmc_${T}_tp_bf16_1,$O/pmc_${T}_tp_bf16_2 \
+                 fp32=$O/pmc_${T}_tp_fp32_1,$O/pmc_${T}_tp_fp32_2 > $O/${T}_tpbfpmc.txt 2>&1
+               cat $O/${T}_tpbfpmc.txt
+               rm -rf $O/pmc_${T}_tp_* ;;
+    tpbfab)    # TP engine at W = 1: bf16 vs fp32 operands, interleaved, plus one phase-timer run each
+               for r in 1 2 3; do
+                 jstep tpbf_bf16 300 python3 bench.py --model mlp --dtype bf16 --steps 20000 --warmup 2000 --no_ref
+                 jstep tpbf_fp32 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref
+               done
+               jstep tpbf_stamps 300 python3 bench.py --model mlp --dtype bf16 --steps 20000 --warmup 2000 --no_ref --stamps
+               jstep tpbf_stamps 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref --stamps ;;
     tpw1ab)    # TP engine at W = 1, this tree vs the round-4 build, interleaved
                for r in 1 2; do
                  jstep tpw1_cur 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref
