@@ -96,6 +96,9 @@ def parse(argv=None):
                     help="skip the same-process stock PyTorch-ROCm comparator after the headline")
     ap.add_argument("--ref_steps", type=int, default=None,
                     help="timed steps of the comparator (default max(--steps, 256); its warmup max(--warmup, 32))")
+    ap.add_argument("--no_fallback", action="store_true",
+                    help="measure the requested engine only: no agreed fallback chain (persistent -> fused "
+                         "hipGraph -> fused eager -> native autograd -> stock torch) when it fails on a rank")
     ap.add_argument("--device", default="auto", choices=["auto", "cuda", "cpu"],
                     help="cpu: the reference engine on gloo (CPU plumbing / deadline tests)")
     ap.add_argument("--share_gpu", action="store_true",
@@ -141,24 +144,27 @@ def _dataset(args, dev, loss):
 
 
 # --------------------------------------------------------------------------- fused
-def run_fused(args, rank, world, dev, comm):
+def run_fused(args, rank, world, dev, comm, dec, graph=True, allreduce=None):
+    """Per-step fused kernel + all-reduce (in-kernel xGMI, or RCCL on the stream). ``graph``: epochs
+    captured into hipGraphs, the capture and a replay-vs-eager check agreed across ranks before
+    timing; otherwise every step is launched eagerly (the chain's last GPU resort before autograd)."""
     from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
     from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
 
+    dec.check("device", dev.type == "cuda", "the fused engine needs a GPU")
+    allreduce = allreduce or args.allreduce
     model, loss = _build_model(args, dev)
     ds = _dataset(args, dev, loss)
     X, Y = ds.tensors
     from pytorch_distributed_training_tutorials_amd.parallel.xgmi import maybe_create
 
-    xg = None if args.allreduce == "rccl" else maybe_create(comm, dev, mode="on" if args.allreduce == "xgmi" else None)
-    if args.allreduce == "xgmi" and xg is None:
-        raise SystemExit("--allreduce xgmi requested but the xGMI path is unavailable")
+    xg = None if allreduce == "rccl" else maybe_create(comm, dev, mode="on" if allreduce == "xgmi" else None)
+    if allreduce == "xgmi":
+        dec.check("xgmi_init", xg is not None, "--allreduce xgmi requested but the xGMI path is unavailable")
     eng = FusedMLPStep(model, loss=loss, lr=args.lr, comm=comm, xgmi=xg)
     if world > 1:
         comm.broadcast(eng.P, 0)  # DDP init: rank 0's parameters everywhere
     sampler = DeviceDistributedSampler(len(ds), world, rank, seed=args.seed, device=dev)
-    variant = args.persist
-    which = eng.persistent_engine(args.batch_size, sampler, variant)
     B = args.batch_size
     ns = sampler.num_samples
     S = math.ceil(ns / B)
@@ -181,12 +187,6 @@ def run_fused(args, rank, world, dev, comm):
     m = max(1, round(args.graph_steps / S))
     full = m * S
     warm_steps = math.ceil(max(args.warmup, 1) / S) * S
-    graphs = {}
-
-    def get_graph(n):
-        if n not in graphs:
-            graphs[n] = eng.graph(epochs_fn(n), extra_state=(sampler._epoch, losses))
-        return graphs[n]
 
     def schedule(n):
         out = [full] * (n // full)
@@ -194,44 +194,66 @@ def run_fused(args, rank, world, dev, comm):
             out.append(n % full)
         return out
 
-    warm = schedule(warm_steps)
-    timed = schedule(args.steps)
-    for n in set(warm + timed):
-        get_graph(n)
+    warm, timed = schedule(warm_steps), schedule(args.steps)
+    if graph:
+        graphs, why = {}, ""
+        try:
+            for n in sorted(set(warm + timed)):
+                graphs[n] = eng.graph(epochs_fn(n), extra_state=(sampler._epoch, losses))
+        except Exception as e:  # noqa: BLE001 -- agreed below: every rank leaves the graph path together
+            why = f"{type(e).__name__}: {e}"
+        dec.check("graph_capture", not why, why)
+        # one replay against the same steps run eagerly from the same state (bitwise kernels and the
+        # same RCCL reductions: anything but a near-exact match means the graph is not the step)
+        saved = [t.clone() for t in eng.state()] + [sampler._epoch.clone(), losses.clone()]
+        n0 = timed[0]
+        epochs_fn(n0)()
+        want = eng.P.clone()
+        for t, v in zip(eng.state() + [sampler._epoch, losses], saved):
+            t.copy_(v)
+        graphs[n0].replay()
+        torch.cuda.synchronize(dev)
+        got = eng.P.clone()
+        for t, v in zip(eng.state() + [sampler._epoch, losses], saved):
+            t.copy_(v)
+        dec.allclose("graph_replay_check", got, want)
+        run = lambda n: graphs[n].replay()  # noqa: E731
+    else:
+        run = lambda n: epochs_fn(n)()  # noqa: E731
     sampler.set_epoch(0)
     for n in warm:
-        get_graph(n).replay()
+        run(n)
     # timed region starts on an epoch boundary (warm_steps is a whole number of epochs)
-    t = _timed(comm, dev, lambda: [get_graph(n).replay() for n in timed])
+    t = _timed(comm, dev, lambda: [run(n) for n in timed])
     if xg is not None:
         xg.check()
     extra = {"replicas_in_sync": _replicas_in_sync(comm, eng.P),
-             "steps_per_epoch": S, "steps_per_graph": full, "warmup_steps_run": warm_steps,
+             "steps_per_epoch": S, "steps_per_graph": full if graph else None, "warmup_steps_run": warm_steps,
              "final_loss": float(losses[(args.steps - 1) % S].item()),
              "allreduce": "xgmi-oneshot (in-kernel)" if xg is not None else "rccl",
-             "kernels": ("1 launch per step: fused fwd+loss+bwd+xGMI all-reduce+SGD, hipGraph" if xg is not None
-                         else "fused_mlp_step + RCCL all-reduce per step (SGD folded into next step), hipGraph")}
+             "kernels": ("1 launch per step: fused fwd+loss+bwd+xGMI all-reduce+SGD" if xg is not None
+                         else "fused_mlp_step + RCCL all-reduce per step (SGD folded into next step)")
+             + (", hipGraph" if graph else ", eager launches")}
     return t, extra
 
 
 # --------------------------------------------------------------------------- persistent
-def run_persistent(args, rank, world, dev, comm):
+def run_persistent(args, rank, world, dev, comm, dec):
     """Persistent DDP step engine: K steps in ceil(K/8192) launches, params/momentum/sampler
-    shard resident in LDS, in-kernel xGMI all-reduce + SGD every step."""
+    shard resident in LDS, in-kernel xGMI all-reduce + SGD every step. Decision points (agreed
+    across ranks, utils/fallback.py): device, xgmi_init, xgmi_poll_warmup, xgmi_poll_timed."""
     from pytorch_distributed_training_tutorials_amd.data.device_sampler import DeviceDistributedSampler
     from pytorch_distributed_training_tutorials_amd.ops.fused_step import FusedMLPStep
     from pytorch_distributed_training_tutorials_amd.parallel.xgmi import maybe_create
 
+    dec.check("device", dev.type == "cuda", "the persistent engine needs a GPU")
     model, loss = _build_model(args, dev)
     ds = _dataset(args, dev, loss)
     X, Y = ds.tensors
     xg = None
     if world > 1:
         xg = maybe_create(comm, dev, mode="on")
-        if xg is None:  # no usable peer memory on this node: per-step engine with RCCL instead
-            print("[bench] xGMI all-reduce unavailable; falling back to --engine fused --allreduce rccl", flush=True)
-            args.allreduce = "rccl"
-            return run_fused(args, rank, world, dev, comm)
+        dec.check("xgmi_init", xg is not None, "xGMI one-shot all-reduce unavailable (peer memory / self-test)")
     eng = FusedMLPStep(model, loss=loss, lr=args.lr, comm=comm, xgmi=xg, dtype=args.dtype)
     if world > 1:
         comm.broadcast(eng.P, 0)  # DDP init: rank 0's parameters everywhere
@@ -297,13 +319,11 @@ def run_persistent(args, rank, world, dev, comm):
             for n, p in zip(launches, starts):
                 launch_at(n, p)
     torch.cuda.synchronize(dev)
-    if _xgmi_failed(comm, dev, xg, "warmup"):
-        return _rccl_fallback(args, rank, world, dev, comm)
+    dec.check("xgmi_poll_warmup", not _xgmi_error(xg), "an in-kernel xGMI poll timed out (a peer never arrived)")
 
     with pin_ctx:
         t = _timed(comm, dev, timed_steps)
-    if _xgmi_failed(comm, dev, xg, "timed run"):
-        return _rccl_fallback(args, rank, world, dev, comm)
+    dec.check("xgmi_poll_timed", not _xgmi_error(xg), "an in-kernel xGMI poll timed out (a peer never arrived)")
     in_sync = _replicas_in_sync(comm, eng.P)
     phase = None
     if args.stamps:  # diagnostic pass AFTER the timed region (timers cost a little)
@@ -360,12 +380,12 @@ def run_persistent(args, rank, world, dev, comm):
     if phase:
         extra["phase_timers"] = phase
     if args.model == "linear" and not args.no_mlp_side:
-        extra.update(_mlp_side(args, rank, world, dev, comm, xg, "fp32"))
-        extra.update(_mlp_side(args, rank, world, dev, comm, xg, "bf16"))
+        extra.update(_mlp_side(args, rank, world, dev, comm, xg, "fp32", dec))
+        extra.update(_mlp_side(args, rank, world, dev, comm, xg, "bf16", dec))
     return t, extra
 
 
-def _mlp_side(args, rank, world, dev, comm, xg, dtype):
+def _mlp_side(args, rank, world, dev, comm, xg, dtype, dec):
     """Side measurement (AFTER the headline, same protocol, same K/W): the toy MLP
     Linear(20,64)-ReLU-Linear(64,10) + CE + SGD on the persistent engine -- the
     workload BASELINE.json's north star names (config 2: bf16) -- in fp32 (keys mlp_*) and
@@ -389,7 +409,7 @@ def _mlp_side(args, rank, world, dev, comm, xg, dtype):
     _rehearse(comm, dev, plan, n_w)
     key = "mlp" if dtype == "fp32" else "mlp_bf16"
     t = _timed(comm, dev, lambda: plan.launch_at(n_t, n_w), label=f"{key}_side")
-    failed = xg is not None and _xgmi_failed(comm, dev, xg, f"MLP side measurement ({dtype})")
+    failed = bool(dec.gather("xGMI poll timeout" if _xgmi_error(xg) else None))
     return {f"{key}_us_per_step": None if failed else round(1e6 * t / n_t, 3),
             f"{key}_samples_per_s": None if failed else round(n_t * args.batch_size * world / t, 1),
             f"{key}_dtype": dtype + (" operands (torch.autocast(bfloat16) rounding points), fp32 master weights/SGD"
@@ -399,30 +419,14 @@ def _mlp_side(args, rank, world, dev, comm, xg, dtype):
             f"{key}_final_loss": float(losses[n_t - 1].item())}
 
 
-def _xgmi_failed(comm, dev, xg, where: str) -> bool:
-    """True on EVERY rank if any rank's in-kernel xGMI poll timed out (a peer never
-    arrived): the run's numbers are void and all ranks must take the same fallback."""
-    if xg is None:
-        return False
-    bad = torch.tensor([float(xg.handle.error() != 0)], device=dev)
-    comm.all_reduce(bad, "max")
-    if bad.item() == 0:
-        return False
-    if comm.rank == 0:
-        print(f"[bench] xGMI poll timeout during the {where}; re-running with --engine fused --allreduce rccl",
-              flush=True)
-    return True
-
-
-def _rccl_fallback(args, rank, world, dev, comm):
-    args.allreduce = "rccl"
-    t, extra = run_fused(args, rank, world, dev, comm)
-    extra["fallback"] = "persistent xGMI engine timed out a poll; fused engine + RCCL all-reduce measured instead"
-    return t, extra
+def _xgmi_error(xg) -> bool:
+    """This rank's in-kernel xGMI poll-timeout flag (a peer never arrived): the run's numbers are void."""
+    return xg is not None and xg.handle.error() != 0
 
 
 # --------------------------------------------------------------------------- autograd
-def run_autograd(args, rank, world, dev, comm):
+def run_autograd(args, rank, world, dev, comm, dec):
+    dec.check("device", dev.type == "cuda", "the native autograd engine needs a GPU")
     from pytorch_distributed_training_tutorials_amd.data import DeviceDataLoader, DistributedSampler
     from pytorch_distributed_training_tutorials_amd.ops.loss import cross_entropy
     from pytorch_distributed_training_tutorials_amd.ops.optim import FusedSGD
@@ -458,7 +462,7 @@ def run_autograd(args, rank, world, dev, comm):
 
 
 # --------------------------------------------------------------------------- reference
-def run_reference(args, rank, world, dev, comm, steps=None, warmup=None, label: str = "headline"):
+def run_reference(args, rank, world, dev, comm, dec=None, steps=None, warmup=None, label: str = "headline"):
     """Stock PyTorch-ROCm loop with the reference's structure (comparator):
     reference ddp_gpus_torchrun.py:16-88 with synthetic data of the same shape."""
     import torch.nn.functional as F
@@ -641,7 +645,8 @@ def _record(args, world, value, elapsed, extra):
         "config": {"model": "ddp_gpus_torchrun toy: Linear(20,1) + F.cross_entropy(soft targets) + SGD(lr=1e-2)"
                    if args.model == "linear" else "toy MLP Linear(20,64)-ReLU-Linear(64,10) + CE + SGD",
                    "global_batch": gb, "per_device_batch": args.batch_size, "seq_len": None,
-                   "dataset_size": args.dataset_size, "parallelism": f"dp{world}", "engine": args.engine},
+                   "dataset_size": args.dataset_size, "parallelism": f"dp{world}",
+                   "engine": getattr(args, "engine_used", args.engine)},
         "baseline_note": "vs_baseline = value / ref_samples_per_s: the stock PyTorch-ROCm reference loop (torch DDP "
                          "over RCCL, DataLoader+DistributedSampler, same model/batch/N) timed in this same process "
                          "after the headline; vs_cpu_probe divides by BASELINE.md's CPU/gloo survey probe; the "
@@ -668,31 +673,55 @@ def _comparator(args, rank, world, dev, comm):
                                               "F.cross_entropy + torch.optim.SGD, same process"}
 
 
+# engine chains: what is tried after the requested engine fails on any rank (utils/fallback.py)
+CHAINS = {"persistent": ["persistent", "fused_graph", "fused_eager", "autograd", "reference"],
+          "fused": ["fused_graph", "fused_eager", "autograd", "reference"],
+          "autograd": ["autograd", "reference"], "reference": ["reference"]}
+
+
+def _chain(args):
+    names = CHAINS[args.engine]
+    if args.dtype == "bf16":  # the bf16 engine is the persistent one; last resort: autocast(bf16) stock loop
+        names = [n for n in names if n in ("persistent", "reference")]
+    if args.share_gpu:  # RCCL needs one GPU per rank: the host-staged engines only
+        names = [n for n in names if n in ("persistent", "fused_graph", "fused_eager")]
+    return names[:1] if args.no_fallback else names
+
+
 def main(argv=None):
     args = parse(argv)
     if args.dtype == "bf16" and args.model != "mlp":
         raise SystemExit("--dtype bf16 runs the toy MLP (--model mlp); the reference Linear(20,1) job is fp32")
-    if args.dtype == "bf16" and args.engine != "persistent":
+    if args.dtype == "bf16" and args.engine not in ("persistent", "reference"):
         raise SystemExit("--dtype bf16 runs on the persistent engine (the bf16 tensor-parallel kernel)")
     cpu = args.device == "cpu" or (args.device == "auto" and not torch.cuda.is_available())
-    if cpu and args.engine != "reference":
+    if cpu and args.no_fallback and args.engine != "reference":
         raise SystemExit("bench.py needs a GPU (MI355X) for the framework engines; --device cpu runs "
-                         "--engine reference only")
+                         "--engine reference (or the engine chain down to it)")
     os.environ.setdefault("PTDT_COMM_TIMEOUT", "120")  # a hung collective aborts well inside --deadline
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     rank_env = int(os.environ.get("RANK", "0"))
     from pytorch_distributed_training_tutorials_amd.utils.deadline import Deadline
+    from pytorch_distributed_training_tutorials_amd.utils.fallback import (Decider, DesyncError, StageFailed,
+                                                                      control_group, run_chain)
+
+    done = {}  # the headline record once measured: a later phase that hangs still reports it
 
     def expire(phase, elapsed):
         why = f"deadline of {args.deadline:.0f} s expired"
         if rank_env == 0:  # own line even if another process left a partial one on the shared stdout
-            print("\n" + _error_line(args, world_env, phase, elapsed, why), flush=True)
+            if "rec" in done:
+                rec = dict(done["rec"], incomplete=f"{why} in phase {phase!r}, after the headline was measured")
+                print("\n" + json.dumps(rec), flush=True)
+            else:
+                print("\n" + _error_line(args, world_env, phase, elapsed, why), flush=True)
         print(f"[bench] rank {rank_env}: {why} in phase {phase!r}; aborting communicators and exiting",
               file=sys.stderr, flush=True)
 
     dl = Deadline(args.deadline, expire, exit_delay_s=0.0 if rank_env == 0 else 5.0)
     dl.set_phase("process group init")
     rank, world, local = _setup(args, cpu)
+    dec = Decider(rank, world, control_group(world))
     dev = torch.device("cpu") if cpu else torch.device("cuda", 0 if args.share_gpu else local)
     from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
     from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
@@ -705,16 +734,49 @@ def main(argv=None):
         comm = comm_mod.HostStagedComm(dev)
     else:
         comm = comm_mod.get_default(dev)
-        dl.register(comm.handle)
-    runner = {"persistent": run_persistent, "fused": run_fused, "autograd": run_autograd,
-              "reference": run_reference}[args.engine]
+        dl.register(getattr(comm, "handle", None))
+    names = _chain(args)
+
+    def stage(name):
+        # a fused stage reached by falling back runs the RCCL all-reduce (the xGMI path already failed)
+        ar = None if name == names[0] else "rccl"
+        fns = {"persistent": lambda d: run_persistent(args, rank, world, dev, comm, d),
+               "fused_graph": lambda d: run_fused(args, rank, world, dev, comm, d, graph=True, allreduce=ar),
+               "fused_eager": lambda d: run_fused(args, rank, world, dev, comm, d, graph=False, allreduce=ar),
+               "autograd": lambda d: run_autograd(args, rank, world, dev, comm, d),
+               "reference": lambda d: run_reference(args, rank, world, dev, comm, d)}
+        return fns[name]
+
     dl.set_phase(f"headline ({args.engine} engine: build, warmup, timed run)")
-    elapsed, extra = runner(args, rank, world, dev, comm)
+    try:
+        used, (elapsed, extra), failures = run_chain(dec, [(n, stage(n)) for n in names])
+    except (StageFailed, DesyncError) as e:
+        if rank == 0:
+            what = "every engine failed" if isinstance(e, StageFailed) else "fallback chain desynchronised"
+            print("\n" + _error_line(args, world, "headline", time.monotonic() - dl.t0, f"{what}: {e}"), flush=True)
+        destroy_process_group()
+        dl.cancel()
+        sys.exit(4)
+    args.engine_used = used
+    extra["engine_path"] = used
+    if failures:
+        extra["fallback"] = failures
     value = args.steps * args.batch_size * world / elapsed
-    if not (args.no_ref or args.share_gpu or args.engine == "reference"):
+    extra["timing"] = dict(_TIMINGS)
+    done["rec"] = _record(args, world, value, elapsed, extra)
+    if not (args.no_ref or args.share_gpu or used == "reference"):
         dl.set_phase("comparator (stock PyTorch-ROCm reference loop)")
-        extra.update(_comparator(args, rank, world, dev, comm))
-        extra["speedup_vs_torch"] = round(value / extra["ref_samples_per_s"], 3)
+        cmp, why = {}, None
+        try:
+            cmp = _comparator(args, rank, world, dev, comm)
+        except Exception as e:  # noqa: BLE001 -- the headline stands; agreed so every rank reports alike
+            why = f"{type(e).__name__}: {e}"
+        bad = dec.gather(why)
+        if bad:
+            extra["comparator_error"] = {str(r): w[:400] for r, w in bad.items()}
+        else:
+            extra.update(cmp)
+            extra["speedup_vs_torch"] = round(value / extra["ref_samples_per_s"], 3)
     dl.set_phase("report")
     extra["timing"] = dict(_TIMINGS)
     extra["gpu_warmup_ms_before_timed"] = _GPU_WARM_MS if dev.type == "cuda" else 0.0

@@ -56,8 +56,13 @@ class PipelineParallelResNet50(ModelParallelResNet50):
     solvers are not deterministic -- two single-queue runs of the SAME schedule differ by up
     to 9 % on small layer4 gradients. With deterministic algorithms
     (``torch.backends.cudnn.deterministic = True``) the stream schedule matches the
-    single-queue one to 6e-6 relative, so the stream schedule itself is race-free and is
-    allowed on one device (tests/test_dp_mp_gpu.py).
+    single-queue one to 6e-6 relative, and it is allowed on one device (tests/test_dp_mp_gpu.py).
+
+    It was NOT race-free by itself: round 5 found the fused BNs' residual-gradient side
+    channel (ops/norm.ResidualLink) crossing the stage streams outside autograd's edges
+    (23 of 25 repetitions mismatched, tools/stream_pipeline_repeat.py); the link now records
+    the stream that produced its stored value -- the sum's stream after a second delivery,
+    round 6 -- and the taker waits for it (tests/test_norm.py two-stream delivery tests).
     """
 
     def __init__(self, split_size: int = 20, *args, streams: bool = False, **kwargs):

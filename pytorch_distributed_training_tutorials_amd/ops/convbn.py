@@ -158,18 +158,21 @@ def _fused_wins(x: torch.Tensor, w: torch.Tensor, tile: int) -> bool:
     n, cin, h, wd = x.shape
     cout = w.shape[0]
     key = (n * h * wd, cin, cout, tile)
-    if key in _CHOICE:
-        return _CHOICE[key]
     if _MODE in ("1", "on"):
         return True
     from ..utils import tuning
 
+    hit = tuning.lookup("convbn", key)  # (a decision valid here: see tuning.lookup)
+    if hit is not None:
+        return hit == "fused"
     pin = tuning.pinned("convbn", key)
     if pin is not None:
-        _CHOICE[key] = pin == "fused"
-        return _CHOICE[key]
+        return pin == "fused"
     if torch.cuda.is_current_stream_capturing():
         return False
+    local = tuning.local_choice("convbn", key)
+    if local is not None:  # timed before outside any scope: agree it, no second timing
+        return tuning.agree("convbn", key, local, ("unfused", "fused"), x.device) == "fused"
     C = native()
     x2 = x.detach().permute(0, 2, 3, 1).reshape(-1, cin)
     w2 = w.detach().reshape(cout, cin)
@@ -189,8 +192,7 @@ def _fused_wins(x: torch.Tensor, w: torch.Tensor, tile: int) -> bool:
             tf, tp = min(tf, _time_us(fused, 1)), min(tp, _time_us(plain, 1))
     local = "fused" if tf < 0.97 * tp else "unfused"
     # rank 0's choice on every rank: DDP replicas must run the same BN statistics path (utils/tuning.py)
-    _CHOICE[key] = tuning.agree("convbn", key, local, ("unfused", "fused"), x.device) == "fused"
-    return _CHOICE[key]
+    return tuning.agree("convbn", key, local, ("unfused", "fused"), x.device) == "fused"
 
 
 def conv_bn_act(conv: nn.Conv2d, bn: nn.Module, x: torch.Tensor, residual: torch.Tensor | None = None,

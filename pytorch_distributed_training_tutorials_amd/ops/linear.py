@@ -98,21 +98,21 @@ def _library(relu: bool = False, key=None, native_fn=None, library_fn=None) -> b
         return False
     if key is None or native_fn is None or library_fn is None:
         return True
-    hit = _TUNED.get(key)
-    if hit is not None:
-        return hit
     from ..utils import tuning
 
+    hit = tuning.lookup("linear", key)  # (a decision valid here: see tuning.lookup)
+    if hit is not None:
+        return hit == "library"
     pin = tuning.pinned("linear", key)
     if pin is not None:
-        _TUNED[key] = pin == "library"
-        return _TUNED[key]
+        return pin == "library"
     if torch.cuda.is_current_stream_capturing():
         return True  # no timing inside a capture; the shape stays untuned
-    local = "library" if _time(library_fn) <= _time(native_fn) else "native"
+    local = tuning.local_choice("linear", key)
+    if local is None:
+        local = "library" if _time(library_fn) <= _time(native_fn) else "native"
     # every DDP rank takes rank 0's engine (replicas must stay bit-identical; utils/tuning.py)
-    _TUNED[key] = tuning.agree("linear", key, local, ("native", "library"), torch.cuda.current_device()) == "library"
-    return _TUNED[key]
+    return tuning.agree("linear", key, local, ("native", "library"), torch.cuda.current_device()) == "library"
 
 
 def plan_big(M: int, N: int, K: int) -> tuple[int, int]:

@@ -65,8 +65,11 @@ class ResidualLink:
     Streams: autograd runs each backward on its forward's stream and synchronises the
     gradients it passes along graph edges, but not this side channel. A link can span two
     streams (a pipeline's stage streams on one device, where the stage hop ``a.to(dev)`` is
-    the same tensor and keeps its link), so the delivering stream is recorded and the taker
-    waits for it when it runs elsewhere (``take``)."""
+    the same tensor and keeps its link), so the stream that produced the stored value is
+    recorded and the taker waits for it when it runs elsewhere (``take``). A second delivery
+    adds on ITS stream after waiting for the first one's, and the sum's stream becomes the
+    recorded one (the round-5 version kept the first deliverer's: a taker on that stream skipped
+    the wait for the add, one on a third stream waited on the wrong stream)."""
 
     __slots__ = ("dres", "stream")
 
@@ -82,6 +85,7 @@ class ResidualLink:
         else:
             self._sync(g.device)
             self.dres = self.dres + g
+            self.stream = torch.cuda.current_stream(g.device) if g.is_cuda else None  # the sum's producer
 
     def take(self, device):
         """The delivered gradient (None if no consumer ran), ordered after its producer's stream."""

@@ -44,6 +44,17 @@ def _flatten_broadcast(tensors, c: comm_mod.Communicator, src: int = 0):
             off += n
 
 
+def _has_grad_fn(out) -> bool:
+    """Whether any tensor in a (nested) forward output carries an autograd graph."""
+    if isinstance(out, torch.Tensor):
+        return out.grad_fn is not None
+    if isinstance(out, (list, tuple)):
+        return any(_has_grad_fn(o) for o in out)
+    if isinstance(out, dict):
+        return any(_has_grad_fn(o) for o in out.values())
+    return False
+
+
 def _same_dense_layout(a: torch.Tensor, b: torch.Tensor) -> bool:
     """Same shape and element order in memory: dense, equal strides on every dimension of size > 1
     (a [Cout, Cin, 1, 1] weight gradient is (Cin, 1, 1, 1) contiguous and (Cin, 1, Cin, Cin) in
@@ -264,10 +275,15 @@ class DistributedDataParallel(nn.Module):
         self._queued = False
         self._flush_casts()  # anything a bucket never completed (e.g. no_sync accumulation)
         self.reducer.finalize()
-        if self.world_size > 1:
+        self._close_scope()
+
+    def _close_scope(self):
+        """Disarm the SPMD scope this wrapper's grad-enabled forward armed (utils/tuning.py)."""
+        if getattr(self, "_scope_open", False):
             from ..utils import tuning
 
-            tuning.spmd_end()
+            tuning.spmd_end(self.comm)
+            self._scope_open = False
 
     def _maybe_rebuild(self):
         if not self._rebuild or self._rebuilt or self.reducer.iteration < 1:
@@ -296,10 +312,18 @@ class DistributedDataParallel(nn.Module):
         if self.world_size > 1:  # ranks run the same shapes in lock step until this step's backward ends
             from ..utils import tuning  # (utils imports this module: no top-level import)
 
+            self._close_scope()  # the previous grad-enabled forward never ran backward: its scope is stale
             tuning.spmd_begin(self.comm)
-            out = self.module(*args, **kwargs)
-            if not torch.is_grad_enabled():
-                tuning.spmd_end()
+            self._scope_open = True
+            try:
+                with tuning.ddp_forward():
+                    out = self.module(*args, **kwargs)
+            except BaseException:
+                self._close_scope()
+                raise
+            # no backward will finalise (no grad mode, or nothing in the output needs a gradient)
+            if not torch.is_grad_enabled() or not _has_grad_fn(out):
+                self._close_scope()
             return out
         return self.module(*args, **kwargs)
 
@@ -330,6 +354,7 @@ class DistributedDataParallel(nn.Module):
 
     def __del__(self):
         try:
+            self._close_scope()
             self.remove_grad_sinks()
             for h in getattr(self, "_hooks", ()):
                 h.remove()

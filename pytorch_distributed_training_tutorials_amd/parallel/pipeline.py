@@ -28,10 +28,17 @@ activations are ``[rows_i, *trailing]``, and backward gradients carry no header
 at all (a gradient has the shape and dtype of the activation it belongs to, which
 both ends already hold). A partial last batch (20 -> 8 rows) or an uneven
 micro-batch split (18 rows / 4 = 5,5,5,3; 6 rows / 4 = 2,2,2) needs no
-configuration: stage 0's chunking travels down the pipeline in the headers. A
-stage whose output changes dtype or trailing shape between micro-batches, or
-changes the row count, raises instead of desynchronising. The last stage slices
-its targets by the row counts it receives.
+configuration: stage 0's chunking travels down the pipeline in the headers. The
+last stage slices its targets by the row counts it receives.
+
+Restriction: a stage must keep the row count (every stage maps a micro-batch of
+``r`` rows to ``r`` rows) and one dtype / trailing shape for all micro-batches of a
+step -- the step header is written once, after micro-batch 0. A violation found at
+micro-batch 0 raises before anything is sent. One found later (micro-batch i > 0,
+after the header went out), or a last stage whose rows do not add up to its
+target, still completes the step's wire protocol -- zero payloads of the advertised
+shape forward, zero gradients backward -- and raises at the end of the step, so no
+peer is left blocked mid-step on this rank's messages.
 
 Overlap (GPU): sends and receives run on a dedicated P2P HIP stream. A send
 waits (stream event) for the compute stream that produced the tensor and the
@@ -184,6 +191,7 @@ class PipelineStage:
         rows_total = target.shape[0] if self.last else None
         inputs, outputs, losses = [], [], []
         out_meta = None
+        err = None  # a violation after the header went out: finish the step's protocol, then raise
         row = 0
         for i in range(n_mb):  # fill: all forwards
             if self.first:
@@ -191,7 +199,7 @@ class PipelineStage:
             else:
                 inp = self._recv((rows[i], *trail), dt, self.stage - 1)
                 inp.requires_grad_(True)
-            out = self.module(inp)
+            out = self.module(inp) if err is None else None
             inputs.append(inp)
             if self.last:
                 r = out.shape[0]
@@ -202,31 +210,44 @@ class PipelineStage:
                     loss = loss * (r / rows_total)
                 losses.append(loss)
                 outputs.append(loss)
-            else:
+                continue
+            if out is not None:
+                why = None
                 if out.dim() < 1 or out.shape[0] != rows[i]:
-                    raise RuntimeError(f"PipelineStage {self.stage}: a stage must keep the row count "
-                                       f"({rows[i]} rows in, {tuple(out.shape)} out)")
-                meta = (out.dtype, tuple(out.shape[1:]))
-                if out_meta is None:
-                    out_meta = meta
-                    self._send_header(_step_header(out, rows), self.stage + 1)
-                elif meta != out_meta:
-                    raise RuntimeError(f"PipelineStage {self.stage}: micro-batch {i} output {meta} differs from "
-                                       f"micro-batch 0's {out_meta} (one step header per step)")
+                    why = (f"PipelineStage {self.stage}: a stage must keep the row count "
+                           f"({rows[i]} rows in, {tuple(out.shape)} out)")
+                elif out_meta is not None and (out.dtype, tuple(out.shape[1:])) != out_meta:
+                    why = (f"PipelineStage {self.stage}: micro-batch {i} output {(out.dtype, tuple(out.shape[1:]))} "
+                           f"differs from micro-batch 0's {out_meta} (one step header per step)")
+                if why is not None and out_meta is None:
+                    raise RuntimeError(why)  # micro-batch 0: nothing sent yet
+                err = why
+            if out_meta is None:
+                out_meta = (out.dtype, tuple(out.shape[1:]))
+                self._send_header(_step_header(out, rows), self.stage + 1)
+            if err is not None:  # the advertised payload, zeros: the next stage's step completes
+                out = None
+                self._send(torch.zeros((rows[i], *out_meta[1]), dtype=out_meta[0], device=self.device),
+                           self.stage + 1)
+            else:
                 self._send(out, self.stage + 1)
-                outputs.append(out)
+            outputs.append(out)
         if self.last and row != rows_total:
-            raise RuntimeError(f"PipelineStage: received {row} rows for a target of {rows_total}")
+            err = f"PipelineStage: received {row} rows for a target of {rows_total}"
         for i in reversed(range(len(outputs))):  # drain: backwards in reverse
             if self.last:
-                outputs[i].backward()
+                if err is None:
+                    outputs[i].backward()
             else:  # d(output): the shape and dtype of the activation this stage sent
-                g = self._recv(outputs[i].shape, outputs[i].dtype, self.stage + 1)
-                outputs[i].backward(g)
+                g = self._recv((rows[i], *out_meta[1]), out_meta[0], self.stage + 1)
+                if outputs[i] is not None and err is None:
+                    outputs[i].backward(g)
             if not self.first:
-                gi = inputs[i].grad
+                gi = inputs[i].grad if err is None else None
                 self._send(gi if gi is not None else torch.zeros_like(inputs[i]), self.stage - 1)
         self.synchronize()
+        if err is not None:
+            raise RuntimeError(err + " -- raised after completing the step's messages (no peer left waiting)")
         if self.last:
             return torch.stack([l.detach() for l in losses]).sum()
         return None

@@ -455,16 +455,17 @@ def tuning_agree(rank, world, port, out_dir):
     outside = tuning.agree("linear", ("nt", 1, 2, 3 + rank), ("native", "library")[rank % 2], ("native", "library"))
     tuning.spmd_begin(c)
     got = []
-    for k in range(3):
-        local = ("native", "library")[(rank + k) % 2]
-        got.append(tuning.agree("linear", ("nt", 128, 1000 + k, 2048), local, ("native", "library")))
-    # ranks reaching different keys at the same point: every rank raises
-    mismatch = None
-    try:
-        tuning.agree("linear", ("nt", 64, 64 + rank, 64), "native", ("native", "library"))
-    except RuntimeError as e:
-        mismatch = str(e)
-    tuning.spmd_end()
+    with tuning.ddp_forward():  # an armed scope is in effect inside a DDP forward (or a backward)
+        for k in range(3):
+            local = ("native", "library")[(rank + k) % 2]
+            got.append(tuning.agree("linear", ("nt", 128, 1000 + k, 2048), local, ("native", "library")))
+        # ranks reaching different keys at the same point: every rank raises
+        mismatch = None
+        try:
+            tuning.agree("linear", ("nt", 64, 64 + rank, 64), "native", ("native", "library"))
+        except RuntimeError as e:
+            mismatch = str(e)
+    tuning.spmd_end(c)
     torch.save({"got": got, "choices": tuning.choices(), "outside": outside, "mismatch": mismatch},
                os.path.join(out_dir, f"r{rank}.pt"))
     destroy_process_group()
@@ -511,3 +512,167 @@ def tp_bf16_ranks_one_gpu(rank, world, port, out_dir):
                os.path.join(out_dir, f"r{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
+
+
+def fallback_chain(rank, world, port, out_dir, inject):
+    """utils/fallback.run_chain over gloo with stages shaped like bench.py's engines (their decision
+    points in order); ``inject`` is PTDT_BENCH_INJECT's syntax."""
+    _init(rank, world, port)
+    import torch.distributed as dist
+
+    from pytorch_distributed_training_tutorials_amd.utils.fallback import (Decider, DesyncError, StageFailed,
+                                                                          control_group, run_chain)
+
+    dec = Decider(rank, world, control_group(world), inject=inject)
+
+    def persistent(d):
+        d.check("device")
+        d.check("xgmi_init")
+        d.check("xgmi_poll_warmup")
+        dist.barrier()  # stands for the timed region (collective on every rank)
+        d.check("xgmi_poll_timed")
+        return "persistent-result"
+
+    def fused_graph(d):
+        d.check("device")
+        if f"early@{rank}" in inject:  # a local exception BEFORE a decision point the others reach
+            raise ValueError("local crash before graph_capture")
+        d.check("graph_capture")
+        d.allclose("graph_replay_check", torch.ones(3), torch.ones(3) * (1.0 if "replay_diff" not in inject else 1.5))
+        return "fused-graph-result"
+
+    def fused_eager(d):
+        d.check("device")
+        if f"crash@{rank}" in inject:  # an unexpected local exception (not a decision point)
+            raise ValueError("local crash")
+        return "fused-eager-result"
+
+    def reference(d):
+        return "reference-result"
+
+    stages = [("persistent", persistent), ("fused_graph", fused_graph), ("fused_eager", fused_eager),
+              ("reference", reference)]
+    try:
+        name, res, failures = run_chain(dec, stages, log=None)
+        out = {"name": name, "res": res, "failures": failures, "points": dec.points}
+    except StageFailed as e:
+        out = {"name": None, "error": str(e), "points": dec.points}
+    except DesyncError as e:
+        out = {"name": None, "desync": "different decision points" in str(e)}
+    torch.save(out, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def tuning_scopes(rank, world, port, out_dir):
+    """utils/tuning SPMD scopes under the native DDP wrapper: two wrappers in one step
+    keep their own counts, a backward agrees inside the scope, a shape first decided by rank 0
+    alone is agreed again inside a DDP forward, and a grad-enabled forward without backward does
+    not make a later rank-0-only inference broadcast alone."""
+    _init(rank, world, port)
+    import torch.nn as nn
+
+    from pytorch_distributed_training_tutorials_amd.parallel.ddp import DistributedDataParallel
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+    from pytorch_distributed_training_tutorials_amd.utils import tuning
+
+    seen = {}
+    opts = ("native", "library")
+
+    def decide(key, local):  # ops/linear.py's flow: a valid cached decision, else (re-)agree
+        hit = tuning.lookup("linear", key)
+        if hit is not None:
+            return hit
+        return tuning.agree("linear", key, tuning.local_choice("linear", key) or local, opts)
+
+    class Pick(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, tag):
+            ctx.tag = tag
+            seen[f"fwd:{tag}:{x.shape[0]}"] = decide(("fw", tag, x.shape[0]), opts[rank % 2])
+            return x * 1.0
+
+        @staticmethod
+        def backward(ctx, g):
+            seen[f"bwd:{ctx.tag}"] = decide(("bw", ctx.tag), opts[(rank + 1) % 2])
+            return g, None
+
+    class M(nn.Module):
+        def __init__(self, tag):
+            super().__init__()
+            self.lin = nn.Linear(4, 4)
+            self.tag = tag
+
+        def forward(self, x):
+            return Pick.apply(self.lin(x), self.tag)
+
+    torch.manual_seed(0)
+    a, b = DistributedDataParallel(M(1)), DistributedDataParallel(M(2))
+    c = a.comm
+    x = torch.randn(3, 4)
+    out = {}
+    # two wrappers, one step: B's scope survives A's finalisation (round 5 set depth = 1 / 0)
+    yb = b(x)
+    ya = a(x)
+    out["depth_after_fwd"] = tuning.scope_depth(c)
+    ya.sum().backward()
+    out["depth_after_a_bwd"] = tuning.scope_depth(c)
+    yb.sum().backward()
+    out["depth_after_b_bwd"] = tuning.scope_depth(c)
+    # a shape decided by rank 0 alone (outside any scope), then reached by every rank in DDP
+    if rank == 0:
+        a.module(torch.randn(5, 4))  # rank-0-only: local decision, no collective
+    a(torch.randn(5, 4)).sum().backward()
+    # grad-enabled forward with no backward, then a rank-0-only inference of a new shape
+    a(torch.randn(6, 4))
+    out["depth_stale"] = tuning.scope_depth(c)
+    if rank == 0:
+        a.module(torch.randn(7, 4))  # must not broadcast: no DDP forward / backward is running
+    a(torch.randn(8, 4)).sum().backward()  # closes the stale scope first
+    out["depth_end"] = tuning.scope_depth(c)
+    with torch.no_grad():
+        a(torch.randn(9, 4))
+    out["depth_no_grad"] = tuning.scope_depth(c)
+    out["seen"] = seen
+    torch.save(out, os.path.join(out_dir, f"r{rank}.pt"))
+    destroy_process_group()
+
+
+def pipeline_late_violation(rank, world, port, out_dir):
+    """Stage 0 changes its output width at micro-batch 2 (after the step header went out): it
+    raises at the end of the step, every other stage completes the step, and a second step
+    after the error still runs (no peer left blocked on a message)."""
+    _init(rank, world, port)
+    import torch.nn as nn
+
+    from pytorch_distributed_training_tutorials_amd.parallel import comm as comm_mod
+    from pytorch_distributed_training_tutorials_amd.parallel.env import destroy_process_group
+    from pytorch_distributed_training_tutorials_amd.parallel.pipeline import PipelineStage
+
+    class Flaky(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.lin = nn.Linear(8, 6)
+            self.calls = 0
+            self.bad_at = 2
+
+        def forward(self, x):
+            self.calls += 1
+            y = self.lin(x)
+            return y[:, :4] if self.calls - 1 == self.bad_at else y
+
+    torch.manual_seed(0)
+    mods = [Flaky()] + [nn.Linear(6, 6) for _ in range(world - 2)] + [nn.Linear(6, 3)]
+    c = comm_mod.get_default()
+    st = PipelineStage(mods[rank], c, loss_fn=nn.MSELoss(), micro_batches=4)
+    g = torch.Generator().manual_seed(1)
+    out = {"errors": [], "losses": []}
+    for step in range(2):
+        x, y = torch.randn(16, 8, generator=g), torch.randn(16, 3, generator=g)
+        try:
+            l = st.train_step(x if rank == 0 else None, y if rank == world - 1 else None)
+            out["losses"].append(None if l is None else float(l))
+        except RuntimeError as e:
+            out["errors"].append(str(e))
+    torch.save(out, os.path.join(out_dir, f"r{rank}.pt"))
+    destroy_process_group()

@@ -119,6 +119,24 @@ def test_kernel_choices_agree_across_ranks(tmp_path):
     assert all(r["mismatch"] and "different linear shape keys" in r["mismatch"] for r in res)
 
 
+def test_tuning_scopes_counted_and_gated(tmp_path):
+    """ADVICE r5 (both mediums) and VERDICT r5 #8a: two DDP wrappers in one step keep their own scope
+    counts; agreement happens inside DDP forwards and backwards only; a shape first decided by rank 0
+    alone is agreed again by every rank inside DDP (no rank skips the collective); a grad-enabled
+    forward without backward does not make a later rank-0-only inference broadcast alone (no hang)."""
+    world = 2
+    spawn(_workers.tuning_scopes, args=(world, free_port(), str(tmp_path)), nprocs=world)
+    res = _load(tmp_path, world)
+    for r in res:
+        assert (r["depth_after_fwd"], r["depth_after_a_bwd"], r["depth_after_b_bwd"]) == (2, 1, 0)
+        assert (r["depth_stale"], r["depth_end"], r["depth_no_grad"]) == (1, 0, 0)
+    shared = {k: v for k, v in res[1]["seen"].items()}
+    for k, v in shared.items():  # every decision both ranks took in DDP is rank 0's
+        assert res[0]["seen"][k] == v, k
+    assert shared["fwd:1:3"] == "native" and shared["bwd:1"] == "library" and shared["bwd:2"] == "library"
+    assert res[0]["seen"]["fwd:1:7"] == "native" and "fwd:1:7" not in res[1]["seen"]  # rank 0 alone, local
+
+
 def test_tuning_table_pins_choice(tmp_path, monkeypatch):
     import json
 

@@ -251,6 +251,36 @@ def test_residual_link_matches_autograd_add(dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("taker", ["first", "third"])
+def test_residual_link_two_deliverers_on_two_streams(taker):
+    """Two consumers deliver a residual gradient on two streams and the producer takes it on the
+    first deliverer's stream or on a third one: the taker must see the finished
+    sum every time. The producers are slow elementwise chains, so a missing or wrong wait races."""
+    from pytorch_distributed_training_tutorials_amd.ops.norm import ResidualLink
+
+    dev = torch.device("cuda", 0)
+    s1, s2, s3 = (torch.cuda.Stream(dev) for _ in range(3))
+    base = torch.randn(1 << 22, device=dev)
+    for rep in range(25):
+        link = ResidualLink()
+        torch.cuda.synchronize()
+        with torch.cuda.stream(s1):
+            a = base.clone()
+            for _ in range(8):
+                a = a * 1.0001 + 0.5
+            link.put(a)
+        with torch.cuda.stream(s2):
+            b = base.clone()
+            for _ in range(24):
+                b = b * 0.9999 - 0.25
+            link.put(b)  # waits for s1's delivery, adds on s2
+        with torch.cuda.stream(s1 if taker == "first" else s3):
+            got = link.take(dev).clone()
+        torch.cuda.synchronize()
+        assert torch.equal(got, a + b), f"repetition {rep}: the taker read an unfinished sum"
+
+
+@pytest.mark.gpu
 def test_residual_link_retain_graph_double_backward():
     """A retained graph run backward twice: every pass re-delivers the linked residual
     gradient, so the accumulated gradients equal 2x the un-linked autograd add."""

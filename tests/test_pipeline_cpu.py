@@ -55,6 +55,19 @@ def test_pipeline_matches_single_process(tmp_path, world, micro, batches):
     assert all(r["messages"] == 4 * n_mb for r in rs[1:-1])
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipeline_late_violation_drains_then_raises(tmp_path, world):
+    """a shape change found after the step header went out raises on that stage at the
+    end of the step, with every message of the step exchanged: the other stages finish the step
+    and the next step runs (in the round-5 code they blocked waiting for payloads)."""
+    spawn(_workers.pipeline_late_violation, args=(world, free_port(), str(tmp_path)), nprocs=world)
+    rs = [torch.load(os.path.join(tmp_path, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    assert len(rs[0]["errors"]) == 1 and "differs from micro-batch 0" in rs[0]["errors"][0]
+    assert "no peer left waiting" in rs[0]["errors"][0]
+    assert rs[0]["losses"] == [None]  # its second step ran
+    assert all(r["errors"] == [] and len(r["losses"]) == 2 for r in rs[1:])
+
+
 def test_inprocess_model_parallel_cpu_matches_unsplit():
     from pytorch_distributed_training_tutorials_amd.models.mp_resnet import (ModelParallelResNet50,
                                                                              PipelineParallelResNet50)
