@@ -107,12 +107,12 @@ def run_chain(decider: Decider, stages, log=print):
     of the stages given up, identical on every rank. Raises StageFailed if every stage failed."""
     failures = []
     for name, fn in stages:
-        point, local, res = None, None, None
+        point, local, res, reasons = None, None, None, None
         try:
             decider.check(f"stage:{name}")  # agreed entry (and the stage-level injection point)
             res = fn(decider)
-        except StageFailed as e:  # agreed inside the stage: every rank is here
-            point, local = e.point, str(e)
+        except StageFailed as e:  # agreed inside the stage: every rank is here, with the same reasons
+            point, local, reasons = e.point, str(e), e.reasons
         except DesyncError:
             raise
         except Exception as e:  # noqa: BLE001 -- a local failure: agreed below
@@ -121,8 +121,9 @@ def run_chain(decider: Decider, stages, log=print):
         if not bad:
             return name, res, failures
         point = point or f"stage:{name}"
-        failures.append({"stage": name, "point": point, "reasons": {str(r): w[:400] for r, w in bad.items()}})
+        reasons = reasons or bad  # the failing ranks' own reasons at the decision point
+        failures.append({"stage": name, "point": point, "reasons": {str(r): w[:400] for r, w in reasons.items()}})
         if decider.rank == 0 and log is not None:
-            log(f"[bench] {name} failed at {point!r} ({'; '.join(f'rank {r}: {w[:200]}' for r, w in bad.items())}); "
+            log(f"[bench] {name} failed at {point!r} ({'; '.join(f'rank {r}: {w[:200]}' for r, w in reasons.items())}); "
                 f"falling back", flush=True)
     raise StageFailed("every stage", {r: f["point"] for r, f in enumerate(failures)})

@@ -46,6 +46,10 @@ def test_chain_agreed_across_ranks(tmp_path, inject, path, point):
     else:
         assert out["failures"][-1]["point"] == point
         assert all(f["reasons"] for f in out["failures"])
+        toks = dict(t.split("@") for t in inject.split(",") if "@" in t)
+        for f in out["failures"]:  # an injected point names only the injected rank (the others moved on)
+            if f["point"] in toks:
+                assert set(f["reasons"]) == {toks[f["point"]]}, out["failures"]
 
 
 def test_chain_every_stage_failed(tmp_path):
