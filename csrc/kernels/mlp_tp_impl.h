@@ -61,6 +61,12 @@ namespace ptdt {
 namespace {
 
 constexpr int kTpThreadsMax = 320;  // up to 4 compute waves + the helper wave
+#ifndef PTDT_TP_BF_POLL_PEERS
+#define PTDT_TP_BF_POLL_PEERS 7
+#endif
+// bf16 engine, float4-staged instances: peers polled per round (packed words; 7 = W = 8 in one round);
+// the scalar-staging instances use 4 (their helper-wave staging arrays leave fewer registers)
+constexpr int kTpBfPollPeers = PTDT_TP_BF_POLL_PEERS;
 using f4 = __attribute__((ext_vector_type(4))) float;
 using f2 = __attribute__((ext_vector_type(2))) float;
 using bf8 = __attribute__((ext_vector_type(8))) __bf16;   // 16x16x32 bf16 operand (8 K values per lane)
@@ -156,20 +162,31 @@ __device__ __forceinline__ float sgd1(float& w, float& m, float g, bool first, f
 // others); the loop is uniform (ballot exit,
 // every lane re-polls its whole set), contributions are summed in rank order (own value
 // from the register): bit-identical replicas. Padded values (zero gradients) travel too.
-template <int NV, int G>
+// PK (the bf16 engine, whose gradients are bf16 values by autocast semantics): two values per LL
+// word -- (NV + 1) / 2 words per lane instead of NV, half the pushes, polls and poll registers, so
+// more peers' polls fit in flight at once (G). The sum is the same fp32 rank-ordered one.
+template <int NV, int G, bool PK = false>
 __device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq, float (&v)[NV], int wave, int lane) {
+  constexpr int NW = PK ? (NV + 1) / 2 : NV;  // LL words per lane
   const int parity = (int)(seq & 1u);
   const uint64_t hi = (uint64_t)seq << 32;
   const bool drop = x.drop_push != 0u && seq >= x.drop_push;
-  const int base = wave * NV * 64 + lane;
+  const int base = wave * NW * 64 + lane;
+  uint32_t pay[NW];
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    if constexpr (PK)
+      pay[k] = (__float_as_uint(v[2 * k]) >> 16) | (2 * k + 1 < NV ? __float_as_uint(v[2 * k + 1]) & 0xffff0000u : 0u);
+    else
+      pay[k] = __float_as_uint(v[k]);
+  }
   for (int p = 0; p < x.world; ++p) {
     if (p == x.rank || drop) continue;
     uint64_t PTDT_GLOBAL* const dst =
         (uint64_t PTDT_GLOBAL*)x.peers[p] + (int64_t)(parity * x.world + x.rank) * x.max_elems + base;
 #pragma unroll
-    for (int k = 0; k < NV; ++k)
-      __hip_atomic_store(dst + k * 64, hi | (uint64_t)__float_as_uint(v[k]), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
+    for (int k = 0; k < NW; ++k)
+      __hip_atomic_store(dst + k * 64, hi | (uint64_t)pay[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   float acc[NV];
 #pragma unroll
@@ -179,7 +196,7 @@ __device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq,
   const int np = x.world - 1;  // the OTHER ranks, polled in groups of G in increasing rank order
   auto peer = [&](int i) { return i < x.rank ? i : i + 1; };
   for (int i0 = 0; i0 < np; i0 += G) {
-    uint64_t w[G][NV];
+    uint64_t w[G][NW];
     auto issue = [&]() {
 #pragma unroll
       for (int g = 0; g < G; ++g) {
@@ -187,7 +204,7 @@ __device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq,
         const uint64_t PTDT_GLOBAL* src =
             (const uint64_t PTDT_GLOBAL*)x.local + (int64_t)(parity * x.world + (real ? peer(i0 + g) : 0)) * x.max_elems + base;
 #pragma unroll
-        for (int k = 0; k < NV; ++k)
+        for (int k = 0; k < NW; ++k)
           w[g][k] = real ? __hip_atomic_load(src + k * 64, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : hi;
       }
     };
@@ -197,7 +214,7 @@ __device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq,
 #pragma unroll
       for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int k = 0; k < NV; ++k) m |= (uint32_t)(w[g][k] >> 32) != seq;
+        for (int k = 0; k < NW; ++k) m |= (uint32_t)(w[g][k] >> 32) != seq;
       if (__builtin_amdgcn_ballot_w64(m) == 0) break;
       if (polls >= x.max_polls) {
         __hip_atomic_store(x.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -216,7 +233,15 @@ __device__ __forceinline__ bool tp_allreduce_lm(const XgmiArgs& x, uint32_t seq,
         own = true;
       }
 #pragma unroll
-      for (int k = 0; k < NV; ++k) acc[k] += __uint_as_float((uint32_t)w[g][k]);
+      for (int k = 0; k < NW; ++k) {
+        const uint32_t u = (uint32_t)w[g][k];
+        if constexpr (PK) {
+          acc[2 * k] += __uint_as_float(u << 16);
+          if (2 * k + 1 < NV) acc[2 * k + 1] += __uint_as_float(u & 0xffff0000u);
+        } else {
+          acc[k] += __uint_as_float(u);
+        }
+      }
     }
   }
   if (!own)
@@ -309,6 +334,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   const bool hb = a.has_bias != 0;
   const bool use_mom = a.mom != nullptr && a.momentum != 0.f;
   const float lr = a.lr, mu = a.momentum, damp = a.dampening, wd = a.weight_decay;
+  const bool plain_sgd = !use_mom && wd == 0.f;
   const int nesterov = a.nesterov;
 
   // ---- LDS carve-up
@@ -1058,7 +1084,10 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
           v[4 * MT + i] = gv2[i];
         }
         v[4 * MT + 4] = db2;  // b2[class c]: the same value in every wave (identical loss in every wave)
-        failed = !tp_allreduce_lm<NV, (LOSS == kLossCEIndex && VX) ? 3 : 2>(a.ar, seq, v, w, l);
+        // polls of G peers in flight (fp32: 3 where the registers allow it; bf16 packs two values
+        // per word, so twice the peers fit: W = 8's seven peers in ceil(7 / G) rounds)
+        constexpr int G = BF ? (VX ? kTpBfPollPeers : 4) : ((LOSS == kLossCEIndex && VX) ? 3 : 2);
+        failed = !tp_allreduce_lm<NV, G, BF>(a.ar, seq, v, w, l);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -1071,22 +1100,32 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     tick(6);  // the all-reduce alone (0 at world 1; index 6 was the list producer before the helper wave)
     // padded inputs / classes have zero gradients and zero weights: no masks needed
     const bool first = opt_step == 0;
+    if (plain_sgd) {  // (uniform) the reference's SGD(lr): one FMA per value, no momentum / decay chain
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) w1r[mt][i] = fmaf(-lr, gv1[mt][i], w1r[mt][i]);
+        w2t[i] = fmaf(-lr, gv2[i], w2t[i]);
+      }
+      if (hb) b2c = fmaf(-lr, db2, b2c);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) sgd1(w1r[mt][i], m1r[mt][i], gv1[mt][i], first, lr, mu, damp, wd, nesterov, use_mom);
+        sgd1(w2t[i], m2t[i], gv2[i], first, lr, mu, damp, wd, nesterov, use_mom);
+      }
+      if (hb) sgd1(b2c, mb2c, db2, first, lr, mu, damp, wd, nesterov, use_mom);
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        sgd1(w1r[mt][i], m1r[mt][i], gv1[mt][i], first, lr, mu, damp, wd, nesterov, use_mom);
-        lg1[mt][i] = gv1[mt][i];
-      }
-      sgd1(w2t[i], m2t[i], gv2[i], first, lr, mu, damp, wd, nesterov, use_mom);
+      for (int mt = 0; mt < MT; ++mt) lg1[mt][i] = gv1[mt][i];
       if constexpr (!BF) W2m[(4 * q + i) * LD2 + c] = w2t[i];
       lg2[i] = gv2[i];
     }
     if constexpr (BF) mirror();  // bf16 operand copies of the updated weights
-    if (hb) {
-      sgd1(b2c, mb2c, db2, first, lr, mu, damp, wd, nesterov, use_mom);
-      if (q == 0) B2m[c] = BF ? bfr(b2c) : b2c;
-    }
+    if (hb && q == 0) B2m[c] = BF ? bfr(b2c) : b2c;  // (no bias: b2c and its gradient stay 0)
     ldb2 = db2;
     ++opt_step;
     ce = ne;

@@ -57,6 +57,34 @@ def _headers():
     return sorted(list(CSRC.rglob("*.h")))
 
 
+_INC = None
+
+
+def _deps(src: Path):
+    """The csrc headers ``src`` includes, transitively (quoted includes resolved next to the including
+    file, then under csrc/): a header edit rebuilds only the units that see it."""
+    import re
+
+    global _INC
+    if _INC is None:
+        _INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+    seen, todo = set(), [src]
+    while todo:
+        f = todo.pop()
+        try:
+            text = f.read_text(errors="replace")
+        except OSError:
+            continue
+        for name in _INC.findall(text):
+            for cand in (f.parent / name, CSRC / name):
+                cand = cand.resolve()
+                if cand.exists() and cand.suffix == ".h" and cand not in seen:
+                    seen.add(cand)
+                    todo.append(cand)
+                    break
+    return sorted(seen)
+
+
 def _newer(src: Path, obj: Path, deps) -> bool:
     if not obj.exists():
         return True
@@ -81,7 +109,6 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, s
     py_inc = sysconfig.get_paths()["include"]
     BUILD.mkdir(parents=True, exist_ok=True)
     kernels, hosts = _sources()
-    hdrs = _headers()
     common = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", f"-I{CSRC}", "-Wno-unused-result"]
     host_flags = common + [
         "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
@@ -99,7 +126,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, s
         wave = src.stem.startswith("linear_wave")
         obj = (stamp_dir if (stamps and wave) else BUILD) / (src.stem + ".o")
         objs.append(obj)
-        if force or _newer(src, obj, hdrs):
+        if force or _newer(src, obj, _deps(src)):
             # single-wave engine: no SLP vectorisation -- it splits DPP adds into
             # v_mov_dpp + v_pk_add pairs (plus zero-inits), ~50 extra VALU per step
             extra = ["-fno-slp-vectorize"] if wave else []
@@ -109,7 +136,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, s
     for src in hosts:
         obj = BUILD / (src.stem + ".host.o")
         objs.append(obj)
-        if force or _newer(src, obj, hdrs):
+        if force or _newer(src, obj, _deps(src)):
             # host-only translation units: -x hip keeps hipcc's HIP headers/macros, no device code is emitted
             todo.append([hipcc, *host_flags, "-x", "hip", "-c", str(src), "-o", str(obj)])
     if todo:

@@ -189,6 +189,12 @@ for s in "$@"; do
                done
                jstep tpbf_stamps 300 python3 bench.py --model mlp --dtype bf16 --steps 20000 --warmup 2000 --no_ref --stamps
                jstep tpbf_stamps 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref --stamps ;;
+    tpshare)   # TP engine exchange rehearsal: W ranks sharing cuda:0, fp32 and bf16 (TPW: world sizes)
+               for w in ${TPW:-2 4 8}; do
+                 for dt in ${TPDT:-fp32 bf16}; do
+                   share tpshare_$dt $w --model mlp --dtype $dt --steps 2000 --warmup 200 --no_mlp_side
+                 done
+               done ;;
     tpw1ab)    # TP engine at W = 1, this tree vs the round-4 build, interleaved
                for r in 1 2; do
                  jstep tpw1_cur 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref
