@@ -14,9 +14,13 @@ epochs), then EXACTLY K timed steps bracketed by barrier + synchronize, the
 MAX elapsed over ranks, one JSON line from rank 0.
 
 Every timed step does the full work: batch gather by sampler index, forward,
-loss, backward, RCCL all-reduce of the gradient bucket across all ranks, SGD
-update; the sampler permutation of every epoch is generated on device inside
-the timed region. Engines:
+loss, backward, all-reduce of the gradient bucket across all ranks, SGD update.
+The sampler permutation is produced on device once per epoch, as the reference
+produces it once per epoch (``set_epoch``): an epoch that starts inside the timed
+steps has its list built inside the timed region (helper waves of the persistent
+engines); one that started during the warm-up steps was built then and is read
+from the launch-to-launch list cache (the driver's 20 timed steps at positions
+5-24 lie inside the first 64-step epoch). Engines:
   persistent (default) many DDP steps per launch, in-kernel xGMI all-reduce
             (single-wave engine for Linear(Din, Dout), LDS workgroup engine otherwise)
   fused     fused step kernel + in-kernel xGMI or RCCL all-reduce, epochs
@@ -33,11 +37,21 @@ like-for-like comparator is the unmodified reference scripts running on
 PyTorch-ROCm on the same node"), the survey's CPU/gloo probe ratio is kept as
 ``vs_cpu_probe``.
 
+Fallback: if the requested engine fails on ANY rank (no GPU, no peer memory for
+the in-kernel xGMI exchange, an xGMI poll timeout, a hipGraph capture error, a
+replayed graph that differs from the same steps run eagerly), every rank moves
+to the next engine of persistent -> fused (hipGraph) -> fused (eager) ->
+autograd -> stock torch together: each decision point is agreed over a gloo
+control group (utils/fallback.py). The JSON line names the measured engine
+(``engine_path``) and every failure (``fallback``: stage, point, each failing
+rank's reason); ``--no_fallback`` measures the requested engine only.
+
 Deadline: the whole run is bounded by ``--deadline`` seconds (default 420, under
 the driver's limit) and every communicator by ``PTDT_COMM_TIMEOUT`` (default
 120 s here). On expiry every rank aborts its communicators, rank 0 prints one
-JSON line with ``"error"`` and the phase the run died in, and the process exits
-non-zero (utils/deadline.py) -- no new process, no re-exec.
+JSON line -- the headline's record if it was already measured (with
+``"incomplete"``), else one with ``"error"`` and the phase the run died in -- and
+the process exits non-zero (utils/deadline.py) -- no new process, no re-exec.
 """
 from __future__ import annotations
 

@@ -215,13 +215,17 @@ __device__ __forceinline__ float ld_sc1(const float* p, bool fence = false) {
 
 // Last block of a channel tile: sum the gx row-block partials (two [gx][C] slabs) of the tile's
 // `width` channels with ALL threads. Thread (part, quad) adds rows part, part + P, ... of 4
-// consecutive channels (P = kRed / (width / 4) parts), kCombineRows rows x 2 slabs of 16-B loads in
-// flight per thread, so the whole combine is ceil(gx / (P kCombineRows)) round trips -- one for
+// consecutive channels (P = kRed / (width / 4) parts), kCombineRows rows x 2 slabs of two 8-B
+// (agent-scope atomic) loads per 4 channels in flight per thread, so the whole combine is
+// ceil(gx / (P kCombineRows)) round trips -- one for
 // every ResNet-50 shape. (Round 4's form, one channel per thread and 4 rows in flight, took up to
 // 32 dependent round trips on the wide layer-1 tiles: gx = 256 row blocks, 256 channels.) The P
 // part-sums are then added in part order through LDS (deterministic). Result in threads t < width.
 constexpr int kCombineRows = 4;
-constexpr size_t kCombineLds = (size_t)2 * kRed * 4 * sizeof(double);  // 2 slabs x P x width doubles
+// 2 slabs x P x width doubles. P x width = 4 kRed for every tile width (P = 4 kRed / width), so this
+// is the size every combine needs, not a worst case (ADVICE r5 asked to size it per launch). It does
+// not cost occupancy: a CU holds 4 of these 512-thread blocks by waves (32), 128 KiB of LDS.
+constexpr size_t kCombineLds = (size_t)2 * kRed * 4 * sizeof(double);
 __device__ __forceinline__ void ld2_sc1(const float* p, float& x, float& y, bool fence) {
   uint64_t u;
   if (fence) u = *reinterpret_cast<const uint64_t*>(p);

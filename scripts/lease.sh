@@ -189,6 +189,11 @@ for s in "$@"; do
                done
                jstep tpbf_stamps 300 python3 bench.py --model mlp --dtype bf16 --steps 20000 --warmup 2000 --no_ref --stamps
                jstep tpbf_stamps 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --no_ref --stamps ;;
+    intab)     # driver command: ROCr interrupt-signalled completion (default) vs polled (HSA_ENABLE_INTERRUPT=0)
+               for r in 1 2 3; do
+                 jstep intab_default 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no_ref --no_mlp_side
+                 jstep intab_polled 300 env HSA_ENABLE_INTERRUPT=0 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no_ref --no_mlp_side
+               done ;;
     tpshare)   # TP engine exchange rehearsal: W ranks sharing cuda:0, fp32 and bf16 (TPW: world sizes)
                for w in ${TPW:-2 4 8}; do
                  for dt in ${TPDT:-fp32 bf16}; do
