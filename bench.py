@@ -376,6 +376,8 @@ def run_persistent(args, rank, world, dev, comm, dec):
             nw = int(which.split(":")[1].split("w")[0])
             phase["logits_loss_per_wave"] = [round(x / args.steps, 1) for x in v[9:9 + nw]]
             phase["barrier_wait_per_wave"] = [round(x / args.steps, 1) for x in v[9 + nw:9 + 2 * nw]]
+            # the helper wave (staging, sampler lists, loss flush): its work per step, then its waits
+            phase["helper_work_barrier1_barrier2"] = [round(v[k] / args.steps, 1) for k in (23, 24, 25)]
     last = (args.steps - 1) % chunk
     extra = {"replicas_in_sync": in_sync, "steps_per_epoch": S, "launches_timed": math.ceil(args.steps / chunk),
              "sampler": ("torch.randperm-identical DistributedSampler order (torch_perm kernel in the timed region)"

@@ -61,6 +61,13 @@ namespace ptdt {
 namespace {
 
 constexpr int kTpThreadsMax = 320;  // up to 4 compute waves + the helper wave
+#ifndef PTDT_TP_PRODUCE_C  // sampler-list positions the helper wave produces per call (every C steps)
+#define PTDT_TP_PRODUCE_C 8
+#endif
+#ifndef PTDT_TP_TWO_AHEAD  // helper wave: batch loads issued two positions ahead (a step of latency hidden)
+#define PTDT_TP_TWO_AHEAD 1
+#endif
+constexpr bool kTpTwoAhead = PTDT_TP_TWO_AHEAD != 0;
 #ifndef PTDT_TP_BF_POLL_PEERS
 #define PTDT_TP_BF_POLL_PEERS 7
 #endif
@@ -526,7 +533,12 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   //   * adds the loss shares wave 0 left in the LDS ring for 16 past steps.
   // It meets the compute waves at their one barrier per step: no extra synchronisation.
   // Round 2 ran all of this on the compute waves (~900 of ~7500 cycles per step).
-  const int C = min(8, S);
+  const int C = min(PTDT_TP_PRODUCE_C, S);
+  // Two positions per pass (B <= 32: lane half l >> 5 takes one position, lane l & 31 its row), so
+  // no per-entry division by B; the two epochs' Feistel keys are selected per lane (four v_cndmask)
+  // and evaluated once -- round 5's form (a runtime division per entry, a per-lane choice between
+  // two key structs) compiled to branchy blocks reloading spilled SGPRs and cost ~5K cycles per call
+  // (every C steps), most of the compute waves' barrier-1 wait (profiles/r6_tp_bf16.md).
   auto produce = [&](int te, int tj) {  // positions (te, tj) .. + C - 1: they span epochs te, te + 1
     FeistelPerm fa, fb;
     if (feistel) {
@@ -534,24 +546,28 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       fb = keys_load(te + 1);
       if (l == 0 && fkeys[((te + 2) & 3) * 12 + 8] != te + 2) keys_store(te + 2);
     }
-    for (int idx = l; idx < C * B; idx += 64) {
-      const int o = idx / B, r = idx - o * B;
+    const int r = l & 31;
+    for (int o = l >> 5; o < C; o += 2) {
       int J = tj + o, E = te;
       if (J >= S) {
         J -= S;
         ++E;
       }
       const int i = J * B + r;
-      if (i >= ns) continue;
+      const bool live = r < B && i < ns;
       int v;
       if (pa.idx != nullptr) {
-        v = given_list(pa, E)[i];
+        v = live ? given_list(pa, E)[i] : 0;
       } else if (feistel) {
-        v = (int)(E == te ? fa : fb)(rank_pos(i));
+        FeistelPerm f = fa;
+        const bool second = E != te;
+#pragma unroll
+        for (int q2 = 0; q2 < 4; ++q2) f.key[q2] = second ? fb.key[q2] : fa.key[q2];
+        v = (int)f(live ? rank_pos(i) : 0u);
       } else {
-        v = (int)rank_pos(i);
+        v = live ? (int)rank_pos(i) : 0;
       }
-      list(E)[i] = v;
+      if (live) list(E)[i] = v;
     }
   };
 
@@ -653,11 +669,20 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     for (int k = 0; k < KY; ++k)
       if (k < nky) st[St::Y_OFF + (YI ? yrow[k] : yrow[k] * 16 + ycol[k])] = yv[k];
   };
-  // position of step 0 staged synchronously (helper), visible to all after the barrier
+  // position of step 0 staged synchronously (helper), visible to all after the barrier; with
+  // two-ahead staging, position 1's loads are then left in flight (the loop's step 0 writes them).
+  // Float4 staging only: the scalar form's 16 staged items per lane stay live across the step and
+  // spilled 12 VGPRs.
+  constexpr bool TA = kTpTwoAhead && VX;
   if (w == NW) {
     stage_sel(e0, j0);
     stage_issue();
     stage_write(0);
+    if constexpr (TA) {
+      const bool w0 = j0 + 1 == S;
+      stage_sel(w0 ? e0 + 1 : e0, w0 ? 0 : j0 + 1);
+      stage_issue();
+    }
   }
   __syncthreads();
   pstamp(5);  // step 0's batch staged: the loop starts
@@ -667,6 +692,14 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   if (w == NW) {
     // ================================================================ helper wave
     int ce = ce0, cj = cj0, sc = 0, pc = 0;
+    int64_t h_acc[3] = {0, 0, 0}, h_mark = ST ? (int64_t)__builtin_amdgcn_s_memtime() : 0;  // (ST) work, barrier 1, 2
+    auto h_tick = [&](int ph) {
+      if constexpr (ST) {
+        const int64_t t = (int64_t)__builtin_amdgcn_s_memtime();
+        h_acc[ph] += t - h_mark;
+        h_mark = t;
+      }
+    };
     for (int k = 0; k < n; ++k) {
       const bool wrap = cj + 1 == S;
       const int ne = wrap ? ce + 1 : ce, nj = wrap ? 0 : cj + 1;
@@ -676,17 +709,33 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         pc = C;
       }
       --pc;
-      stage_sel(ne, nj);  // position k + 1 (stale-but-valid past the launch)
-      stage_issue();
-      // shares of steps [k-17, k-1): written by wave 0 before barrier k-1
-      if (k > 1 && ((k - 1) & (kTpLossFlush - 1)) == 0) flush_losses(k - 1 - kTpLossFlush, k - 1);
-      stage_write(sn);
+      if constexpr (TA) {
+        // position k + 1 was loaded during step k - 1 (a whole step of latency hidden): write it, then
+        // put position k + 2's loads in flight across this step's barriers (its list entries were
+        // produced S + 1 >= 2 positions ahead; stale-but-valid past the launch)
+        stage_write(sn);
+        const bool wrap2 = nj + 1 == S;
+        stage_sel(wrap2 ? ne + 1 : ne, wrap2 ? 0 : nj + 1);
+        stage_issue();
+        if (k > 1 && ((k - 1) & (kTpLossFlush - 1)) == 0) flush_losses(k - 1 - kTpLossFlush, k - 1);
+      } else {
+        stage_sel(ne, nj);  // position k + 1 (stale-but-valid past the launch)
+        stage_issue();
+        // shares of steps [k-17, k-1): written by wave 0 before barrier k-1
+        if (k > 1 && ((k - 1) & (kTpLossFlush - 1)) == 0) flush_losses(k - 1 - kTpLossFlush, k - 1);
+        stage_write(sn);
+      }
+      h_tick(0);
       __syncthreads();  // barrier 1 of step k (partial logits)
+      h_tick(1);
       __syncthreads();  // barrier 2 of step k (dZ slices)
+      h_tick(2);
       ce = ne;
       cj = nj;
       sc = sn;
     }
+    if (ST && l == 0 && pa.stamps_n >= 26)  // the helper's own split: work, barrier-1 wait, barrier-2 wait
+      for (int q2 = 0; q2 < 3; ++q2) pa.stamps[23 + q2] += h_acc[q2];
     if (n > 0) {  // the remaining loss shares (every step's share written before the final barrier)
       __syncthreads();
       const int kf = n > 1 ? (((n - 2) / kTpLossFlush) * kTpLossFlush) : 0;

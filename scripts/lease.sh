@@ -194,6 +194,18 @@ for s in "$@"; do
                  jstep intab_default 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no_ref --no_mlp_side
                  jstep intab_polled 300 env HSA_ENABLE_INTERRUPT=0 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no_ref --no_mlp_side
                done ;;
+    tpvar)     # TP engine at W = 1: this tree vs tools/bin/_C_$VAR.so (build_variant.py), bf16 + fp32,
+               # interleaved, then one phase-timer run of each
+               for r in 1 2; do
+                 for dt in bf16 fp32; do
+                   jstep tpvar_base 300 python3 bench.py --model mlp --dtype $dt --steps 20000 --warmup 2000 --no_ref
+                   jstep tpvar_$VAR 300 env PTDT_EXT_PATH=$PWD/tools/bin/_C_$VAR.so python3 bench.py --model mlp --dtype $dt --steps 20000 --warmup 2000 --no_ref
+                 done
+               done
+               for dt in bf16 fp32; do
+                 jstep tpvar_base_st 300 python3 bench.py --model mlp --dtype $dt --steps 20000 --warmup 2000 --no_ref --stamps
+                 jstep tpvar_${VAR}_st 300 env PTDT_EXT_PATH=$PWD/tools/bin/_C_$VAR.so python3 bench.py --model mlp --dtype $dt --steps 20000 --warmup 2000 --no_ref --stamps
+               done ;;
     tpshare)   # TP engine exchange rehearsal: W ranks sharing cuda:0, fp32 and bf16 (TPW: world sizes)
                for w in ${TPW:-2 4 8}; do
                  for dt in ${TPDT:-fp32 bf16}; do
