@@ -84,6 +84,8 @@ def parse(argv=None):
     ap.add_argument("--lr", type=float, default=1e-2)
     ap.add_argument("--model", default="linear", choices=["linear", "mlp"],
                     help="linear = reference Linear(20,1)+soft CE; mlp = Linear(20,64)-ReLU-Linear(64,10)+CE")
+    ap.add_argument("--hidden", type=int, default=64,
+                    help="hidden width of --model mlp (64 = the north star's toy; probes only)")
     ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
                     help="bf16: the toy MLP (--model mlp) on the bf16 tensor-parallel engine with "
                          "torch.autocast(bfloat16) semantics and fp32 master weights (BASELINE config 2)")
@@ -146,7 +148,7 @@ def _build_model(args, dev):
     torch.manual_seed(args.seed)
     if args.model == "linear":
         return ddp_toy_model(20, 1).to(dev), "ce_soft"
-    return ToyMLP(20, 64, 10).to(dev), "ce_index"
+    return ToyMLP(20, args.hidden, 10).to(dev), "ce_index"
 
 
 def _dataset(args, dev, loss):
@@ -377,7 +379,8 @@ def run_persistent(args, rank, world, dev, comm, dec):
             phase["logits_loss_per_wave"] = [round(x / args.steps, 1) for x in v[9:9 + nw]]
             phase["barrier_wait_per_wave"] = [round(x / args.steps, 1) for x in v[9 + nw:9 + 2 * nw]]
             # the helper wave (staging, sampler lists, loss flush): its work per step, then its waits
-            phase["helper_work_barrier1_barrier2"] = [round(v[k] / args.steps, 1) for k in (23, 24, 25)]
+            phase["helper_per_step"] = {n: round(v[23 + k] / args.steps, 1) for k, n in enumerate(
+                ("other", "barrier1_wait", "barrier2_wait", "produce", "stage_write", "stage_sel_issue", "loss_flush"))}
     last = (args.steps - 1) % chunk
     extra = {"replicas_in_sync": in_sync, "steps_per_epoch": S, "launches_timed": math.ceil(args.steps / chunk),
              "sampler": ("torch.randperm-identical DistributedSampler order (torch_perm kernel in the timed region)"
@@ -501,7 +504,8 @@ def run_reference(args, rank, world, dev, comm, dec=None, steps=None, warmup=Non
     else:
         ds = TensorDataset(torch.randn(args.dataset_size, 20, generator=g),
                            torch.randint(0, 10, (args.dataset_size,), generator=g))
-        model = torch.nn.Sequential(torch.nn.Linear(20, 64), torch.nn.ReLU(), torch.nn.Linear(64, 10)).to(dev)
+        model = torch.nn.Sequential(torch.nn.Linear(20, args.hidden), torch.nn.ReLU(),
+                                    torch.nn.Linear(args.hidden, 10)).to(dev)
     sampler = TorchSampler(ds, num_replicas=world, rank=rank)
     loader = DataLoader(ds, batch_size=args.batch_size, pin_memory=cuda, shuffle=False, sampler=sampler)
     ddp = TorchDDP(model, device_ids=[dev.index] if cuda else None)
@@ -659,7 +663,7 @@ def _record(args, world, value, elapsed, extra):
         "dtype": args.dtype,
         "data": "synthetic (uniform [0,1) features/targets generated on device, 2048 samples), random-init weights",
         "config": {"model": "ddp_gpus_torchrun toy: Linear(20,1) + F.cross_entropy(soft targets) + SGD(lr=1e-2)"
-                   if args.model == "linear" else "toy MLP Linear(20,64)-ReLU-Linear(64,10) + CE + SGD",
+                   if args.model == "linear" else f"toy MLP Linear(20,{args.hidden})-ReLU-Linear({args.hidden},10) + CE + SGD",
                    "global_batch": gb, "per_device_batch": args.batch_size, "seq_len": None,
                    "dataset_size": args.dataset_size, "parallelism": f"dp{world}",
                    "engine": getattr(args, "engine_used", args.engine)},

@@ -61,9 +61,6 @@ namespace ptdt {
 namespace {
 
 constexpr int kTpThreadsMax = 320;  // up to 4 compute waves + the helper wave
-#ifndef PTDT_TP_PRODUCE_C  // sampler-list positions the helper wave produces per call (every C steps)
-#define PTDT_TP_PRODUCE_C 8
-#endif
 #ifndef PTDT_TP_TWO_AHEAD  // helper wave: batch loads issued two positions ahead (a step of latency hidden)
 #define PTDT_TP_TWO_AHEAD 1
 #endif
@@ -71,8 +68,8 @@ constexpr bool kTpTwoAhead = PTDT_TP_TWO_AHEAD != 0;
 #ifndef PTDT_TP_BF_POLL_PEERS
 #define PTDT_TP_BF_POLL_PEERS 7
 #endif
-// bf16 engine, float4-staged instances: peers polled per round (packed words; 7 = W = 8 in one round);
-// the scalar-staging instances use 4 (their helper-wave staging arrays leave fewer registers)
+// bf16 engine, float4-staged class-index CE instances (the toy): peers polled per round (packed words;
+// 7 = W = 8 in one round); the others use 4 (7 spilled 28-46 VGPRs there)
 constexpr int kTpBfPollPeers = PTDT_TP_BF_POLL_PEERS;
 using f4 = __attribute__((ext_vector_type(4))) float;
 using f2 = __attribute__((ext_vector_type(2))) float;
@@ -523,51 +520,34 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   }
 
   // Helper wave (w == NW): owns the sampler lists and the batch staging, so the NW compute
-  // waves run only the step's math. Per step k, between the barriers of steps k-1 and k, it
-  //   * produces list entries C = min(8, S) positions at a time, S+1 positions ahead of use
-  //     (cycle-walking Feistel of the device sampler; three LDS epoch slots keep any produced
-  //     epoch clear of the ones still read),
-  //   * reads position k+1's rows from the list, loads them (X rows, targets) and writes
-  //     them into stage slot (k+1) % 3 (rows and X^T) -- that slot was last read in step
-  //     k-2's backward (before barrier k-1) and is next read in step k+1 (after barrier k),
-  //   * adds the loss shares wave 0 left in the LDS ring for 16 past steps.
-  // It meets the compute waves at their one barrier per step: no extra synchronisation.
+  // waves run only the step's math. It meets the compute waves at their two barriers per step and
+  // splits its work between the two phases they leave it:
+  //   * before barrier 1 (the compute waves' backward + SGD + forward): stage position k+1 into slot
+  //     (k+1) % 3 (rows and X^T; float4 instances write the rows loaded during step k-1 and put
+  //     position k+2's loads in flight) -- the slot was last read in step k-2's backward (before
+  //     barrier 1 of k-1) and is next read in step k+1 (after barrier 2 of k);
+  //   * between the barriers (the compute waves' loss rows): produce ONE list position, S+2 ahead
+  //     of the step (cycle-walking Feistel of the device sampler; the Feistel keys stay in
+  //     registers within an epoch; three LDS epoch slots keep it clear of the ones still read),
+  //     and every 16 steps add the loss shares wave 0 left in the LDS ring.
+  // Round 5 produced 8 positions every 8 steps before barrier 1 (a runtime division per entry, a
+  // per-lane choice between two key structs, the keys reloaded every call): ~4.6K cycles per call,
+  // and with the staging on a SIMD shared with a compute wave the helper reached barrier 1 ~500
+  // cycles after the compute waves in every step (profiles/r6_tp_bf16.md, helper phase stamps).
   // Round 2 ran all of this on the compute waves (~900 of ~7500 cycles per step).
-  const int C = min(PTDT_TP_PRODUCE_C, S);
-  // Two positions per pass (B <= 32: lane half l >> 5 takes one position, lane l & 31 its row), so
-  // no per-entry division by B; the two epochs' Feistel keys are selected per lane (four v_cndmask)
-  // and evaluated once -- round 5's form (a runtime division per entry, a per-lane choice between
-  // two key structs) compiled to branchy blocks reloading spilled SGPRs and cost ~5K cycles per call
-  // (every C steps), most of the compute waves' barrier-1 wait (profiles/r6_tp_bf16.md).
-  auto produce = [&](int te, int tj) {  // positions (te, tj) .. + C - 1: they span epochs te, te + 1
-    FeistelPerm fa, fb;
-    if (feistel) {
-      fa = keys_load(te);
-      fb = keys_load(te + 1);
-      if (l == 0 && fkeys[((te + 2) & 3) * 12 + 8] != te + 2) keys_store(te + 2);
-    }
-    const int r = l & 31;
-    for (int o = l >> 5; o < C; o += 2) {
-      int J = tj + o, E = te;
-      if (J >= S) {
-        J -= S;
-        ++E;
-      }
-      const int i = J * B + r;
-      const bool live = r < B && i < ns;
+  FeistelPerm fcur;  // keys of epoch pe (the position produced next: (pe, pj))
+  auto keys_for = [&](int e) {  // the keys of epoch e in fcur (stored first when its slot holds another)
+    if (l == 0 && fkeys[(e & 3) * 12 + 8] != e) keys_store(e);
+    fcur = keys_load(e);
+  };
+  auto produce_one = [&](int pe, int pj) {  // lane = row of position (pe, pj); B <= 32
+    const int i = pj * B + l;
+    if (l < B && i < ns) {
       int v;
-      if (pa.idx != nullptr) {
-        v = live ? given_list(pa, E)[i] : 0;
-      } else if (feistel) {
-        FeistelPerm f = fa;
-        const bool second = E != te;
-#pragma unroll
-        for (int q2 = 0; q2 < 4; ++q2) f.key[q2] = second ? fb.key[q2] : fa.key[q2];
-        v = (int)f(live ? rank_pos(i) : 0u);
-      } else {
-        v = live ? (int)rank_pos(i) : 0;
-      }
-      if (live) list(E)[i] = v;
+      if (pa.idx != nullptr) v = given_list(pa, pe)[i];
+      else if (feistel) v = (int)fcur(rank_pos(i));
+      else v = (int)rank_pos(i);
+      list(pe)[i] = v;
     }
   };
 
@@ -691,8 +671,10 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
   const int ce0 = e0, cj0 = j0;
   if (w == NW) {
     // ================================================================ helper wave
-    int ce = ce0, cj = cj0, sc = 0, pc = 0;
-    int64_t h_acc[3] = {0, 0, 0}, h_mark = ST ? (int64_t)__builtin_amdgcn_s_memtime() : 0;  // (ST) work, barrier 1, 2
+    int ce = ce0, cj = cj0, sc = 0;
+    // (ST) [0] rest of the step's work [1] barrier-1 wait [2] barrier-2 wait [3] produce [4] stage_write
+    // [5] stage_sel + issue [6] loss flush
+    int64_t h_acc[7] = {0, 0, 0, 0, 0, 0, 0}, h_mark = ST ? (int64_t)__builtin_amdgcn_s_memtime() : 0;
     auto h_tick = [&](int ph) {
       if constexpr (ST) {
         const int64_t t = (int64_t)__builtin_amdgcn_s_memtime();
@@ -700,45 +682,60 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         h_mark = t;
       }
     };
+    // list positions produced: (e0, j0) + S + 1 here, then (e0, j0) + S + 2 + k in step k -- every
+    // position past the prologue's two epochs exactly once, each >= 1 step before it is staged
+    int pe = cj0 + 1 == S ? ce0 + 2 : ce0 + 1, pj = cj0 + 1 == S ? 0 : cj0 + 1;
+    auto advance = [&]() {
+      if (++pj == S) {
+        pj = 0;
+        ++pe;
+        if (feistel) keys_for(pe);
+      }
+    };
+    if (feistel) keys_for(pe);
+    produce_one(pe, pj);
+    advance();
     for (int k = 0; k < n; ++k) {
       const bool wrap = cj + 1 == S;
       const int ne = wrap ? ce + 1 : ce, nj = wrap ? 0 : cj + 1;
       const int sn = sc == 2 ? 0 : sc + 1;
-      if (pc == 0) {
-        produce(wrap ? ce + 2 : ce + 1, wrap ? 0 : cj + 1);
-        pc = C;
-      }
-      --pc;
+      h_tick(0);
       if constexpr (TA) {
         // position k + 1 was loaded during step k - 1 (a whole step of latency hidden): write it, then
-        // put position k + 2's loads in flight across this step's barriers (its list entries were
-        // produced S + 1 >= 2 positions ahead; stale-but-valid past the launch)
+        // put position k + 2's loads in flight across this step's barriers (stale-but-valid past the
+        // launch: its entries were produced at least one step ago)
         stage_write(sn);
+        h_tick(4);
         const bool wrap2 = nj + 1 == S;
         stage_sel(wrap2 ? ne + 1 : ne, wrap2 ? 0 : nj + 1);
         stage_issue();
-        if (k > 1 && ((k - 1) & (kTpLossFlush - 1)) == 0) flush_losses(k - 1 - kTpLossFlush, k - 1);
+        h_tick(5);
       } else {
         stage_sel(ne, nj);  // position k + 1 (stale-but-valid past the launch)
         stage_issue();
-        // shares of steps [k-17, k-1): written by wave 0 before barrier k-1
-        if (k > 1 && ((k - 1) & (kTpLossFlush - 1)) == 0) flush_losses(k - 1 - kTpLossFlush, k - 1);
+        h_tick(5);
         stage_write(sn);
+        h_tick(4);
       }
-      h_tick(0);
       __syncthreads();  // barrier 1 of step k (partial logits)
       h_tick(1);
+      produce_one(pe, pj);
+      advance();
+      h_tick(3);
+      // shares of steps [k-16, k): written by wave 0 before barrier 1 of step k - 1 or earlier
+      if (k > 0 && (k & (kTpLossFlush - 1)) == 0) flush_losses(k - kTpLossFlush, k);
+      h_tick(6);
       __syncthreads();  // barrier 2 of step k (dZ slices)
       h_tick(2);
       ce = ne;
       cj = nj;
       sc = sn;
     }
-    if (ST && l == 0 && pa.stamps_n >= 26)  // the helper's own split: work, barrier-1 wait, barrier-2 wait
-      for (int q2 = 0; q2 < 3; ++q2) pa.stamps[23 + q2] += h_acc[q2];
+    if (ST && l == 0 && pa.stamps_n >= 30)  // the helper's own split (h_acc above)
+      for (int q2 = 0; q2 < 7; ++q2) pa.stamps[23 + q2] += h_acc[q2];
     if (n > 0) {  // the remaining loss shares (every step's share written before the final barrier)
       __syncthreads();
-      const int kf = n > 1 ? (((n - 2) / kTpLossFlush) * kTpLossFlush) : 0;
+      const int kf = ((n - 1) / kTpLossFlush) * kTpLossFlush;  // the loop flushed [0, kf)
       for (int lo = kf; lo < n; lo += kTpLossFlush) flush_losses(lo, min(n, lo + kTpLossFlush));
     }
     return;
@@ -1135,7 +1132,8 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
         v[4 * MT + 4] = db2;  // b2[class c]: the same value in every wave (identical loss in every wave)
         // polls of G peers in flight (fp32: 3 where the registers allow it; bf16 packs two values
         // per word, so twice the peers fit: W = 8's seven peers in ceil(7 / G) rounds)
-        constexpr int G = BF ? (VX ? kTpBfPollPeers : 4) : ((LOSS == kLossCEIndex && VX) ? 3 : 2);
+        constexpr int G = BF ? ((VX && LOSS == kLossCEIndex) ? kTpBfPollPeers : 4)
+                             : ((LOSS == kLossCEIndex && VX) ? 3 : 2);
         failed = !tp_allreduce_lm<NV, G, BF>(a.ar, seq, v, w, l);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
