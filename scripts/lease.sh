@@ -82,6 +82,8 @@ for s in "$@"; do
                  jstep pinab 120 env PTDT_BENCH_PIN_CU=0 python3 bench.py --steps 20 --warmup 5 --no_ref --no_mlp_side
                done ;;
     default)   jstep bench_default 300 python3 bench.py ;;
+    hl20k)     # headline engine alone, long launch: per-step cost without the fixed part
+               for r in 1 2; do jstep hl20k 300 python3 bench.py --steps 20000 --warmup 2000 --no_ref --no_mlp_side; done ;;
     stamps)    jstep stamps 300 python3 bench.py --steps 20000 --warmup 2000 --stamps --no_mlp_side
                jstep stamps 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --stamps ;;
     share)     share share 2 --steps 20000 --warmup 2000 --stamps --no_mlp_side
@@ -160,6 +162,7 @@ for s in "$@"; do
                  > "$O/${T}_replay_order.txt" 2>&1; echo "replay_order exit $?"; tail -5 "$O/${T}_replay_order.txt"
                rm -rf "$O/prof_${T}_memtrace" ;;  # ~200k dispatches (MIOpen find): too big to copy back
     mlpstamps) jstep mlpstamps 300 python3 bench.py --model mlp --steps 20000 --warmup 2000 --stamps --no_ref ;;
+    profdrv)   prof drvonly 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no_ref --no_mlp_side ;;
     prof)      prof driver 300 python3 bench.py --gpus 1 --steps 20 --warmup 5
                prof reference 300 python3 bench.py --engine reference --steps 200 --warmup 20 ;;
     tppmcab)   # TP engine PMC per step: this tree vs tools/bin/_C_r4.so (round-4 build), two passes each
