@@ -469,7 +469,7 @@ std::string persistent_engine(int64_t B, int64_t Din, int64_t H, int64_t Dout, i
   a.B = (int)B; a.Din = (int)Din; a.H = (int)H; a.Dout = (int)Dout; a.loss_kind = (int)loss_kind;
   a.has_bias = has_bias ? 1 : 0;
   a.ar.world = (int)world;
-  a.ldx = 1 << 20;  // the caller zero-pads X rows to the layout's width when needed
+  a.ldx = kWaveLdxAny;  // the caller zero-pads X rows to the layout's width when needed
   a.x_padded = 1;
   PersistArgs pa{};
   pa.num_samples = (int)num_samples;

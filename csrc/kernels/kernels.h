@@ -100,6 +100,14 @@ struct PersistArgs {
 // kPersistWaveRows / kPersistWaveF restrict the wave engine to one lane-layout
 // family (row groups across DPP rows / feature groups across DPP rows).
 constexpr int kWavePrefetch = 3;  // batches in flight in the wave engine (register buffers)
+// FusedMlpArgs::ldx of an engine-choice query (persistent_engine()): any row stride, the caller pads
+// X rows to the chosen layout's width
+constexpr int kWaveLdxAny = 1 << 20;
+// LDS stride of one epoch index list in the wave engines: S batches of B entries plus up to 64
+// padding entries (layout F reads row slots rho * 16 + i < 16 R <= 64 of the last batch unclamped)
+__host__ __device__ __forceinline__ int wave_list_stride(int num_samples, int B) {
+  return (((num_samples + B - 1) / B) * B + 64 + 3) & ~3;
+}
 // kPersistMfma: the workgroup engine with the 4-wave MFMA step body for
 // Linear-ReLU-Linear (B <= 32, Din <= 32, H in 16..64 step 16, Dout <= 16);
 // kPersistAuto picks it for those shapes.

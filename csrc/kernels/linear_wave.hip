@@ -1,4 +1,5 @@
 // Host dispatch of the single-wave persistent engine (linear_wave_impl.h).
+#include <algorithm>
 #include "common.h"
 #include "kernels.h"
 
@@ -13,8 +14,8 @@ namespace {
 
 constexpr int kThreads = 256;  // wave 0 trains, waves 1-3 build index lists
 
-size_t lds_bytes(const PersistArgs& p) {  // two epoch index lists + 8 phase-timer slots
-  return (size_t)2 * al4(p.num_samples) * sizeof(int) + 8 * sizeof(unsigned long long);
+size_t lds_bytes(const FusedMlpArgs& a, const PersistArgs& p) {  // two epoch index lists + 8 phase-timer slots
+  return (size_t)2 * wave_list_stride(p.num_samples, a.B) * sizeof(int) + 8 * sizeof(unsigned long long);
 }
 constexpr size_t kStaticLds = 512;  // layout F's static pair-exchange scratch (linear_wave_impl.h)
 // loss ring of layout F: (2 epochs + prefetch depth) steps x 64 lane shares
@@ -67,7 +68,7 @@ Choice choose(const FusedMlpArgs& a, const PersistArgs& p) {
   Choice best;
   if (a.H != 0 || a.B <= 0 || a.B > 64 || a.Dout <= 0) return best;
   if (a.ar.world > kXgmiMaxRanks) return best;
-  if (lds_bytes(p) + kStaticLds > 160 * 1024) return best;
+  if (a.B <= 0 || lds_bytes(a, p) + kStaticLds > 160 * 1024) return best;
   const bool ar = a.ar.world > 1;
   static const int kLR[][2] = {{1, 1}, {2, 1}, {4, 1}, {8, 1}, {2, 2}, {4, 2}, {0, 1}, {0, 2}, {0, 4}};
   double best_cost = 1e30;
@@ -78,7 +79,6 @@ Choice choose(const FusedMlpArgs& a, const PersistArgs& p) {
     const int lanes = L == 0 ? 4 : L;            // feature chunks per row
     const int groups = L == 0 ? 16 : 64 / L;     // row slots
     if (groups * R < a.B) continue;              // rows must fit one pass
-    if (L == 0 && (int64_t)p.N * ldx >= (1ll << 32)) continue;  // layout F gathers with 32-bit offsets
     if (ar && groups < a.ar.world) continue;     // one row slot per rank
     const int need = (a.Din + lanes - 1) / lanes;
     int kp = -1;
@@ -88,6 +88,12 @@ Choice choose(const FusedMlpArgs& a, const PersistArgs& p) {
         break;
       }
     if (kp < 0) continue;
+    // layout F gathers through buffer resources: 32-bit byte offsets, 24-bit row index x row bytes
+    // (a query with kWaveLdxAny: the caller pads X rows to exactly the layout's width)
+    const int64_t row = a.ldx == kWaveLdxAny ? std::max(a.Din, lanes * kp) : ldx;
+    if (L == 0 && ((int64_t)p.N * row * 4 >= (1ll << 31) || p.N >= (1 << 24) || row * 4 >= (1 << 24) ||
+                   (int64_t)p.N * 8 >= (1ll << 31) || (int64_t)p.N * a.Dout * 4 >= (1ll << 31)))
+      continue;
     const void* fn = pick(a.loss_kind, ar, L, R, kp, a.Dout);
     if (fn == nullptr) continue;
     const double cost = model_cycles(L, R, kp, a.Dout);
@@ -120,7 +126,7 @@ hipError_t linear_wave_prepare(const FusedMlpArgs& a, const PersistArgs& p, Pers
   out->a = a;
   out->p = p;
   out->p.loss_ring = 0;
-  out->lds = lds_bytes(p);
+  out->lds = lds_bytes(a, p);
   if (c.L == 0 && out->lds + ring_bytes(a, p) + kStaticLds <= 160 * 1024) {
     out->p.loss_ring = 1;
     out->lds += ring_bytes(a, p);

@@ -929,6 +929,92 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += dpp_f<kDppRor1>(v);
   return v;
 }
+// row16_sum of N values at once. For N == 6 (KP = 5 features + the bias: the flagship Linear(20,1)
+// chunk) the 24 DPP adds are ONE asm block, stage-major, so each value's next stage is 6 instructions
+// after its previous one (no s_nop: DPP reads a VGPR 2 wait states after its VALU write) and every
+// stage is a single v_add_f32_dpp. Left to the compiler, the chains were either finished one after
+// the other with an s_nop between every two stages, or their last add sank past the step's
+// epoch-barrier branch and was no longer fused with its DPP move (v_mov + v_mov_dpp + v_add per value).
+// The sums are the same bits as row16_sum (v + ror(v), same stage order).
+template <int N>
+__device__ __forceinline__ void row16_sum_n(float* v) {
+  if constexpr (N == 6) {
+#define PTDT_R16(ROR)                                                         \
+  "v_add_f32_dpp %0, %0, %0 row_ror:" #ROR " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_add_f32_dpp %1, %1, %1 row_ror:" #ROR " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_add_f32_dpp %2, %2, %2 row_ror:" #ROR " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_add_f32_dpp %3, %3, %3 row_ror:" #ROR " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_add_f32_dpp %4, %4, %4 row_ror:" #ROR " row_mask:0xf bank_mask:0xf\n\t" \
+  "v_add_f32_dpp %5, %5, %5 row_ror:" #ROR " row_mask:0xf bank_mask:0xf\n\t"
+    asm volatile("s_nop 1\n\t" PTDT_R16(8) PTDT_R16(4) PTDT_R16(2) PTDT_R16(1)
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]));
+#undef PTDT_R16
+  } else {
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = row16_sum(v[k]);
+  }
+}
+// uniform float (the value is the same in every lane): lets a select on a uniform condition be SALU
+__device__ __forceinline__ float uniform_f(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+// a == b ? x : y for uniform operands, as s_cmp + s_cselect (the compiler turns a uniform float
+// select into v_cndmask on VGPR copies)
+__device__ __forceinline__ float select_eq_u(int a, int b, float x, float y) {
+  // readfirstlane: where the compiler cannot prove an operand uniform it would hand a VGPR to "s"
+  a = __builtin_amdgcn_readfirstlane(a);
+  b = __builtin_amdgcn_readfirstlane(b);
+  x = uniform_f(x);
+  y = uniform_f(y);
+  float r;
+  asm volatile("s_cmp_eq_u32 %1, %2\n\ts_cselect_b32 %0, %3, %4" : "=s"(r) : "s"(a), "s"(b), "s"(x), "s"(y) : "scc");
+  return r;
+}
+
+// Packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth of FMAs per issue slot).
+typedef float f2v __attribute__((ext_vector_type(2)));
+// x . w over one feature chunk: even features accumulate in .x, odd ones in .y (one packed FMA per
+// feature pair), then the halves are added -- exactly the scalar two-accumulator order
+// (acc0 = x0 w0 + x2 w2 + ..., acc1 = x1 w1 + ..., acc0 + acc1).
+template <int KP>
+__device__ __forceinline__ float chunk_dot(const float (&x)[KP], const float (&w)[KP]) {
+  f2v acc = {0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k + 1 < KP; k += 2)
+    acc = __builtin_elementwise_fma(f2v{x[k], x[k + 1]}, f2v{w[k], w[k + 1]}, acc);
+  float a0 = acc.x;
+  if constexpr ((KP & 1) != 0) a0 = fmaf(x[KP - 1], w[KP - 1], a0);
+  return a0 + acc.y;
+}
+// SGD update kinds of the step loop (one loop instantiation each; no per-element branch)
+constexpr int kSgdPlain = 0;  // no momentum, no weight decay: w -= lr * g (the reference's SGD(lr))
+constexpr int kSgdNoMom = 1;  // weight decay, no momentum
+constexpr int kSgdMom = 2;    // momentum (dampening, nesterov), weight decay
+// raw buffer resource over [p, p + bytes): 32-bit offsets, out-of-range loads return 0
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buffer_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+// KP consecutive floats at byte offset `off` (dwordx4 / dwordx2 / dword pieces)
+template <int KP>
+__device__ __forceinline__ void buffer_load_chunk(__amdgpu_buffer_rsrc_t r, uint32_t off, float (&x)[KP]) {
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  int k = 0;
+#pragma unroll
+  for (; k + 4 <= KP; k += 4) {
+    const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, off + 4 * k, 0, 0));
+    x[k] = v.x;
+    x[k + 1] = v.y;
+    x[k + 2] = v.z;
+    x[k + 3] = v.w;
+  }
+  if constexpr (KP - (KP / 4) * 4 >= 2) {
+    const f2v v = __builtin_bit_cast(f2v, __builtin_amdgcn_raw_buffer_load_b64(r, off + 4 * k, 0, 0));
+    x[k] = v.x;
+    x[k + 1] = v.y;
+    k += 2;
+  }
+  if constexpr ((KP & 1) != 0) x[KP - 1] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off + 4 * (KP - 1), 0, 0));
+}
 
 template <int R, int KP, int DOUT, int LOSS, bool AR>
 __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a, PersistArgs pa) {
@@ -959,8 +1045,11 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   if (tl_p != nullptr && threadIdx.x == 0)  // tl_mark(tl, 0) with the entry time taken above
     __hip_atomic_store(tl_p, r_now, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int estride = al4(ns_arg);
   const int S = (ns_arg + B - 1) / B;
+  // Lists are padded past num_samples with valid row indices (0): a batch's row slots rho * 16 + i
+  // read their list entries unclamped (rows past the batch are masked by `valid`), so the last
+  // batch may read up to (S - 1) * B + 16 R <= S * B + 64 entries. Same stride on the host (lds_bytes).
+  const int estride = wave_list_stride(ns_arg, B);
   int e0 = start_e, j0 = start_j;
   if (!has_start) {  // the device cursor (plain launch): a load only on this path
     e0 = cursor_p[0];
@@ -1012,32 +1101,36 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   }
   // batch loads: x rows of this lane's feature group, the targets of its loss rows
   const int rho_own = SCATTER ? (q & (R - 1)) : 0;  // the row whose loss this lane computes
-  const auto X = gptr(X_arg);
   const int ldx = ldx_arg > 0 ? ldx_arg : Din;  // feature slots past Din read X's zero padding
+  // Gathers through buffer resources with 32-bit byte offsets (the host checks N * ldx * 4 < 2^31,
+  // sel, ldx * 4 < 2^24): one v_mad_u32_u24 per row instead of a 64-bit address chain.
+  const uint32_t n_rows = (uint32_t)pa.N;
+  const __amdgpu_buffer_rsrc_t xrs = buffer_rsrc(X_arg, n_rows * (uint32_t)ldx * 4u);
+  const __amdgpu_buffer_rsrc_t yrs =
+      LOSS == kLossCEIndex ? buffer_rsrc(a.Yi, n_rows * 8u) : buffer_rsrc(a.Yf, n_rows * (uint32_t)(DOUT * 4));
+  const uint32_t ldx4 = (uint32_t)ldx * 4u, k04 = (uint32_t)k0 * 4u;
   auto load_batch = [&](Batch<R, KP, DOUT, RY>& f, const int (&sel)[R], int sel_y, int nb) {
     f.nb = nb;
 #pragma unroll
-    for (int rho = 0; rho < R; ++rho) {
-      const auto xr = X + ((uint32_t)sel[rho] * (uint32_t)ldx + (uint32_t)k0);  // 32-bit offset (host-checked)
-#pragma unroll
-      for (int k = 0; k < KP; ++k) f.x[rho][k] = xr[k];
-    }
+    for (int rho = 0; rho < R; ++rho) buffer_load_chunk<KP>(xrs, __umul24((uint32_t)sel[rho], ldx4) + k04, f.x[rho]);
 #pragma unroll
     for (int ry = 0; ry < RY; ++ry) {
-      const int s = SCATTER ? sel_y : sel[ry];
+      const uint32_t s = (uint32_t)(SCATTER ? sel_y : sel[ry]);
       if constexpr (LOSS == kLossCEIndex) {
-        f.yi[ry] = reinterpret_cast<const int*>(a.Yi)[2 * (int64_t)s];  // low dword (see mlp_tp.hip)
+        f.yi[ry] = __builtin_amdgcn_raw_buffer_load_b32(yrs, s * 8u, 0, 0);  // low dword (see mlp_tp.hip)
       } else {
 #pragma unroll
-        for (int c = 0; c < DOUT; ++c) f.y[ry][c] = gptr(a.Yf)[(int64_t)s * DOUT + c];
+        for (int c = 0; c < DOUT; ++c)
+          f.y[ry][c] = __int_as_float(__builtin_amdgcn_raw_buffer_load_b32(yrs, s * (uint32_t)(DOUT * 4) + 4u * c, 0, 0));
       }
     }
   };
   Batch<R, KP, DOUT, RY> buf[kNB];
-  const ListCache lc{pa.lcache, pa.ltag, estride};
+  const ListCache lc{pa.lcache, pa.ltag, al4(ns_arg)};  // the global cache keeps the unpadded stride
   rank_epoch_indices_or(given_list(pa, e0), list(e0), (uint32_t)pa.N, pa.W, pa.rank, pa.num_samples, pa.seed, e0, pa.shuffle,
                      (int)threadIdx.x, kThreads, lc);
-  for (int k = (int)threadIdx.x; k < pa.num_samples; k += kThreads) list(e0 + 1)[k] = 0;
+  for (int k = (int)threadIdx.x; k < estride; k += kThreads) list(e0 + 1)[k] = 0;
+  for (int k = ns_arg + (int)threadIdx.x; k < estride; k += kThreads) list(e0)[k] = 0;  // builders write [0, ns)
   pstamp(1);
   // Loss ring (pa.loss_ring): the trainer stores each lane's scaled loss share
   // per step (one ds_write), the helper waves add the 64 shares and write
@@ -1052,6 +1145,8 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     int64_t lo = pos0;
     // positions [lo, hi): 16 lanes per position (a DPP row), 4 shares per lane (one 16-B LDS read),
     // then a fixed-order 16-lane tree -- the final call runs after the last step, in the launch's tail
+    // (a progressive variant -- the helpers polling a trainer step count in LDS and reducing each
+    // position as it completed -- cost 0.017 us per step and did not shorten the tail; round 6)
     auto reduce_losses = [&](int64_t hi) {
       const int grp = ht >> 4, sub = ht & 15, ngrp = hn >> 4;
       for (int64_t P = lo + grp; P < hi; P += ngrp) {
@@ -1111,9 +1206,9 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     }
     nb_next = min(B, pa.num_samples - ij * B);
 #pragma unroll
-    for (int rho = 0; rho < R; ++rho) sel_next[rho] = list(ie)[ij * B + min(rho * 16 + i, nb_next - 1)];
+    for (int rho = 0; rho < R; ++rho) sel_next[rho] = list(ie)[ij * B + rho * 16 + i];
     if constexpr (SCATTER)  // own row's index read directly: selecting from sel_next[] by a lane value spills it
-      sel_y_next = list(ie)[ij * B + min(rho_own * 16 + i, nb_next - 1)];
+      sel_y_next = list(ie)[ij * B + rho_own * 16 + i];
     if (++ij == S) {
       ij = 0;
       ++ie;
@@ -1201,8 +1296,13 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     for (int k = 0; k < KP; ++k) Gk[c][k] = 0.f;
   }
   int rslot = 0;  // loss ring slot of the next step
-  auto train = [&](Batch<R, KP, DOUT, RY>& f, int step, auto mom_tag, auto ring_tag) {
-    constexpr bool MOM = decltype(mom_tag)::value;
+  // uniform loss scales of a full and of the short last batch (SGPRs: a per-step select is SALU)
+  const float inv_full_u = uniform_f(inv_full), inv_last_u = uniform_f(inv_last);
+  const float lr_b = hb ? lr : 0.f;  // plain SGD's bias step
+  const float gs_full = uniform_f(a.grad_scale * inv_full), gs_last = uniform_f(a.grad_scale * inv_last);
+  auto train = [&](Batch<R, KP, DOUT, RY>& f, int step, auto sgd_tag, auto ring_tag) {
+    constexpr int SGD = decltype(sgd_tag)::value;
+    constexpr bool MOM = SGD == kSgdMom;
     constexpr bool RING = decltype(ring_tag)::value;
     const int nb = f.nb;
     // ---- forward: partial logits of this feature group
@@ -1210,15 +1310,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
 #pragma unroll
     for (int rho = 0; rho < R; ++rho) {
 #pragma unroll
-      for (int c = 0; c < DOUT; ++c) {
-        float acc0 = 0.f, acc1 = 0.f;
-#pragma unroll
-        for (int k = 0; k < KP; k += 2) {
-          acc0 = fmaf(f.x[rho][k], W[c][k], acc0);
-          if (k + 1 < KP) acc1 = fmaf(f.x[rho][k + 1], W[c][k + 1], acc1);
-        }
-        zp[rho][c] = acc0 + acc1;
-      }
+      for (int c = 0; c < DOUT; ++c) zp[rho][c] = chunk_dot<KP>(f.x[rho], W[c]);
     }
     tk.tick(1);
     // ---- logits -> loss -> dL/dz (g[rho][c] in every lane)
@@ -1238,7 +1330,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
       const bool owner = R == 4 || q < 2;
       lsum = owner ? l : 0.f;
       csum = owner ? cnt : 0.f;
-      if constexpr (LOSS != kLossCEIndex) gz *= a.grad_scale * (nb == B ? inv_full : inv_last);  // 1/B once
+      if constexpr (LOSS != kLossCEIndex) gz *= select_eq_u(nb, B, gs_full, gs_last);  // 1/B once
       if constexpr (R == 2) {
         const F2 r = pl16(gz, gz);  // rows [g0, g0, g0, g0], [g1, g1, g1, g1]
         g[0][0] = r.a;
@@ -1275,7 +1367,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
       csum = wave_sum(csum);
       inv_denom = 1.f / (csum > 0.f ? csum : 1.f);
     } else {
-      inv_denom = nb == B ? inv_full : inv_last;
+      inv_denom = select_eq_u(nb, B, inv_full_u, inv_last_u);
     }
     // SCATTER already applied the scale to dL/dz before the all-gather
     const float coef = (SCATTER && LOSS != kLossCEIndex) ? 1.f : a.grad_scale * inv_denom;
@@ -1284,17 +1376,35 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     float gW[DOUT][KP], gb[DOUT];
 #pragma unroll
     for (int c = 0; c < DOUT; ++c) {
+      // sum over the lane's rows, feature pairs packed: t = g0 x0 + g1 x1 + ... (scalar order)
+      float t[KP];
 #pragma unroll
-      for (int k = 0; k < KP; ++k) {
-        float t = g[0][c] * f.x[0][k];
+      for (int k = 0; k + 1 < KP; k += 2) {
+        f2v tv = f2v{f.x[0][k], f.x[0][k + 1]} * f2v{g[0][c], g[0][c]};
 #pragma unroll
-        for (int rho = 1; rho < R; ++rho) t = fmaf(g[rho][c], f.x[rho][k], t);
-        gW[c][k] = (SCATTER && LOSS != kLossCEIndex) ? row16_sum(t) : row16_sum(t) * coef;
+        for (int rho = 1; rho < R; ++rho)
+          tv = __builtin_elementwise_fma(f2v{f.x[rho][k], f.x[rho][k + 1]}, f2v{g[rho][c], g[rho][c]}, tv);
+        t[k] = tv.x;
+        t[k + 1] = tv.y;
+      }
+      if constexpr ((KP & 1) != 0) {
+        float tl = g[0][c] * f.x[0][KP - 1];
+#pragma unroll
+        for (int rho = 1; rho < R; ++rho) tl = fmaf(g[rho][c], f.x[rho][KP - 1], tl);
+        t[KP - 1] = tl;
       }
       float tb = g[0][c];
 #pragma unroll
       for (int rho = 1; rho < R; ++rho) tb += g[rho][c];
-      gb[c] = (SCATTER && LOSS != kLossCEIndex) ? row16_sum(tb) : row16_sum(tb) * coef;
+      // the KP weight sums and the bias sum of class c: one row16_sum_n group
+      float sums[KP + 1];
+#pragma unroll
+      for (int k = 0; k < KP; ++k) sums[k] = t[k];
+      sums[KP] = tb;
+      row16_sum_n<KP + 1>(sums);
+#pragma unroll
+      for (int k = 0; k < KP; ++k) gW[c][k] = (SCATTER && LOSS != kLossCEIndex) ? sums[k] : sums[k] * coef;
+      gb[c] = (SCATTER && LOSS != kLossCEIndex) ? sums[KP] : sums[KP] * coef;
     }
     tk.tick(3);
     // ---- all-reduce over ranks: row slot r <-> rank r, summed with the same DPP tree
@@ -1320,17 +1430,26 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
       failed = !ok;
       failed = __any(failed);
 #pragma unroll
-      for (int c = 0; c < DOUT; ++c) {
+      for (int c = 0; c < DOUT; ++c) {  // the ranks' sum: the same DPP tree (row16_sum_n group per class)
+        float sums[KP + 1];
 #pragma unroll
-        for (int k = 0; k < KP; ++k) gW[c][k] = row16_sum(v[c][k]) * inv_w;
-        gb[c] = row16_sum(vb[c]) * inv_w;
+        for (int k = 0; k < KP; ++k) sums[k] = v[c][k];
+        sums[KP] = vb[c];
+        row16_sum_n<KP + 1>(sums);
+#pragma unroll
+        for (int k = 0; k < KP; ++k) gW[c][k] = sums[k] * inv_w;
+        gb[c] = sums[KP] * inv_w;
       }
     }
     tk.tick(4);
-    // ---- SGD on this lane's feature group (MOM: momentum on; the caller
-    // instantiates the whole step loop per value, so no per-step branch)
+    // ---- SGD on this lane's feature group (SGD: the update kind; the caller
+    // instantiates the whole step loop per kind, so no per-step branch)
     const bool first = opt_step == 0;
     auto upd = [&](float& w, float& m, float gr) {
+      if constexpr (SGD == kSgdPlain) {  // d = g + 0 * w == g for every finite w
+        w = fmaf(-lr, gr, w);
+        return;
+      }
       float d = fmaf(wd, w, gr);
       if constexpr (MOM) {
         const float buf = first ? d : fmaf(mu, m, (1.f - damp) * d);
@@ -1343,8 +1462,12 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     for (int c = 0; c < DOUT; ++c) {
 #pragma unroll
       for (int k = 0; k < KP; ++k) upd(W[c][k], M[c][k], gW[c][k]);
-      upd(Wb[c], Mb[c], gb[c]);
-      Wb[c] = hb ? Wb[c] : 0.f;
+      if constexpr (SGD == kSgdPlain) {
+        Wb[c] = fmaf(-lr_b, gb[c], Wb[c]);  // no bias: lr_b = 0 keeps Wb at 0 (no select)
+      } else {
+        upd(Wb[c], Mb[c], gb[c]);
+        Wb[c] = hb ? Wb[c] : 0.f;
+      }
     }
     ++opt_step;
     // the DDP bucket (a.G) keeps the last step's averaged gradients: register
@@ -1375,11 +1498,11 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   tk.tick(0);
   int done = 0;
   const int nfull = n - n % kNB;
-  auto run = [&](auto mom_tag, auto ring_tag) {
+  auto run = [&](auto sgd_tag, auto ring_tag) {
     while (done < nfull && !failed) {
 #pragma unroll
       for (int u = 0; u < kNB; ++u) {
-        train(buf[u], done + u, mom_tag, ring_tag);
+        train(buf[u], done + u, sgd_tag, ring_tag);
         fetch(buf[u]);
         tk.tick(0);
       }
@@ -1388,18 +1511,25 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
 #pragma unroll
     for (int u = 0; u < kNB - 1; ++u) {
       if (done < n && !failed) {
-        train(buf[u], done, mom_tag, ring_tag);
+        train(buf[u], done, sgd_tag, ring_tag);
         ++done;
       }
     }
   };
-  // one loop instantiation per (momentum, loss ring): no per-step branch on either
+  // one loop instantiation per (SGD kind, loss ring): no per-step branch on either. Plain SGD (the
+  // reference's SGD(lr)) has its own loop with the ring only; without the ring it takes the
+  // weight-decay loop (same values: d = g + 0 * w).
+  using Plain = std::integral_constant<int, kSgdPlain>;
+  using NoMom = std::integral_constant<int, kSgdNoMom>;
+  using Mom = std::integral_constant<int, kSgdMom>;
   if (use_mom) {
-    if (ring) run(std::true_type{}, std::true_type{});
-    else run(std::true_type{}, std::false_type{});
+    if (ring) run(Mom{}, std::true_type{});
+    else run(Mom{}, std::false_type{});
+  } else if (ring) {
+    if (wd == 0.f) run(Plain{}, std::true_type{});
+    else run(NoMom{}, std::true_type{});
   } else {
-    if (ring) run(std::false_type{}, std::true_type{});
-    else run(std::false_type{}, std::false_type{});
+    run(NoMom{}, std::false_type{});
   }
   tl_mark(pa.tl, 2);
   // final stores first, then the remaining barriers: their latency overlaps the helpers' tail
