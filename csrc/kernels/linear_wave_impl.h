@@ -113,6 +113,14 @@ struct Ticks {
   }
 };
 
+// A/B switches of the chunked exchange's poll loop (tools/build_variant.py): PTDT_LL_PIPE = 1 keeps two
+// poll rounds in flight; PTDT_LL_SLEEP = the s_sleep between single rounds (0: none)
+#ifndef PTDT_LL_PIPE
+#define PTDT_LL_PIPE 0
+#endif
+#ifndef PTDT_LL_SLEEP
+#define PTDT_LL_SLEEP 1
+#endif
 // One-shot LL exchange of one lane's gradient chunk (csrc/comm/xgmi.h protocol):
 // push the chunk to rank `peer` (when `active`), then poll rank `peer`'s chunk in
 // this rank's buffer. Chunk elements: c*Din + k0 + k (k < KP, real when
@@ -153,6 +161,54 @@ __device__ __forceinline__ bool ll_exchange(bool active, uint64_t PTDT_GLOBAL* p
 #pragma unroll
     for (int c = 0; c < DOUT; ++c)
       __hip_atomic_store(dst + nW + c, hi | __float_as_uint(gb[c]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#if PTDT_LL_PIPE
+  // two poll rounds in flight (A/B variant): a round is re-issued as soon as it was checked, so a word
+  // landing just after one round read the memory is caught by the other one
+  uint64_t wa[DOUT][KP + 1], wb[DOUT][KP + 1];
+  auto issue = [&](uint64_t (&w)[DOUT][KP + 1]) {
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k)
+        w[c][k] = __hip_atomic_load(src + c * Din + min(k0 + k, Din - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      w[c][KP] = __hip_atomic_load(src + (hb ? nW + c : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  };
+  auto arrived = [&](const uint64_t (&w)[DOUT][KP + 1]) {
+    bool all = true;
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c)
+#pragma unroll
+      for (int k = 0; k <= KP; ++k) all &= (uint32_t)(w[c][k] >> 32) == seq;
+    return all;
+  };
+  auto take = [&](const uint64_t (&w)[DOUT][KP + 1]) {
+#pragma unroll
+    for (int c = 0; c < DOUT; ++c) {
+#pragma unroll
+      for (int k = 0; k < KP; ++k) v[c][k] = k0 + k < Din ? __uint_as_float((uint32_t)w[c][k]) : 0.f;
+      vb[c] = hb ? __uint_as_float((uint32_t)w[c][KP]) : 0.f;
+    }
+  };
+  issue(wa);
+  issue(wb);
+  for (uint32_t polls = 0;; ++polls) {
+    if (arrived(wa)) {
+      take(wa);
+      return true;
+    }
+    issue(wa);
+    if (arrived(wb)) {
+      take(wb);
+      return true;
+    }
+    issue(wb);
+    if (polls >= max_polls) {  // a peer is gone: fail loudly, never hang
+      __hip_atomic_store((int PTDT_GLOBAL*)err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return false;
+    }
+  }
+#else
   for (uint32_t polls = 0;; ++polls) {
     bool all = true;
 #pragma unroll
@@ -174,8 +230,11 @@ __device__ __forceinline__ bool ll_exchange(bool active, uint64_t PTDT_GLOBAL* p
       __hip_atomic_store((int PTDT_GLOBAL*)err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return false;
     }
-    __builtin_amdgcn_s_sleep(1);
+#if PTDT_LL_SLEEP
+    __builtin_amdgcn_s_sleep(PTDT_LL_SLEEP);
+#endif
   }
+#endif
 }
 
 // Uniform LL exchange for layout F (row slot i <-> rank i, csrc/comm/xgmi.h words) -- an

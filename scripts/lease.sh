@@ -119,6 +119,15 @@ for s in "$@"; do
                  share linab_base $W --steps 2000 --warmup 200 --no_ref --no_mlp_side
                  unset PTDT_EXT_PATH
                done; done ;;
+    llab)      # single-wave chunked exchange poll loop: this tree vs tools/bin/_C_{nosleep,llpipe}.so, W = 4, 8
+               for r in 1 2; do for W in 4 8; do
+                 share llab_base $W --steps 2000 --warmup 200 --no_ref --no_mlp_side
+                 for v in nosleep llpipe; do
+                   export PTDT_EXT_PATH=$PWD/tools/bin/_C_$v.so
+                   share llab_$v $W --steps 2000 --warmup 200 --no_ref --no_mlp_side
+                   unset PTDT_EXT_PATH
+                 done
+               done; done ;;
     wsab)      # single-wave engine phase split (stamps builds): this tree vs tools/bin/_C_stamps_base.so, W = 2, 4
                for W in 2 4; do
                  export PTDT_EXT_PATH=$PWD/tools/bin/_C_stamps.so
