@@ -114,12 +114,14 @@ struct Ticks {
 };
 
 // A/B switches of the chunked exchange's poll loop (tools/build_variant.py): PTDT_LL_PIPE = 1 keeps two
-// poll rounds in flight; PTDT_LL_SLEEP = the s_sleep between single rounds (0: none)
+// poll rounds in flight; PTDT_LL_SLEEP = the s_sleep between single rounds (0: none). Shared-GPU
+// rehearsal, 2,000 steps (profiles/r6_wave_exchange_poll_ab.jsonl): no sleep 1.56-1.57 / 1.78 us per
+// step at W = 4 / 8, s_sleep 1 1.56-1.59 / 1.81-1.83, two rounds in flight 1.62 / 1.91-1.97.
 #ifndef PTDT_LL_PIPE
 #define PTDT_LL_PIPE 0
 #endif
 #ifndef PTDT_LL_SLEEP
-#define PTDT_LL_SLEEP 1
+#define PTDT_LL_SLEEP 0
 #endif
 // One-shot LL exchange of one lane's gradient chunk (csrc/comm/xgmi.h protocol):
 // push the chunk to rank `peer` (when `active`), then poll rank `peer`'s chunk in
@@ -504,7 +506,8 @@ struct Batch {
   float x[R][KP];
   float y[RY][DOUT];
   int yi[RY];
-  int nb;  // rows in this batch (last batch of an epoch may be short)
+  int nb;        // rows in this batch (last batch of an epoch may be short)
+  float cg, cl;  // layout F: dL/dz scale (grad_scale / rows) and loss scale (1 / rows) of this batch
 };
 
 // quad_perm broadcast of lane `src` of each aligned group of L (2 or 4) lanes
@@ -1013,23 +1016,6 @@ __device__ __forceinline__ void row16_sum_n(float* v) {
     for (int k = 0; k < N; ++k) v[k] = row16_sum(v[k]);
   }
 }
-// uniform float (the value is the same in every lane): lets a select on a uniform condition be SALU
-__device__ __forceinline__ float uniform_f(float v) {
-  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
-}
-// a == b ? x : y for uniform operands, as s_cmp + s_cselect (the compiler turns a uniform float
-// select into v_cndmask on VGPR copies)
-__device__ __forceinline__ float select_eq_u(int a, int b, float x, float y) {
-  // readfirstlane: where the compiler cannot prove an operand uniform it would hand a VGPR to "s"
-  a = __builtin_amdgcn_readfirstlane(a);
-  b = __builtin_amdgcn_readfirstlane(b);
-  x = uniform_f(x);
-  y = uniform_f(y);
-  float r;
-  asm volatile("s_cmp_eq_u32 %1, %2\n\ts_cselect_b32 %0, %3, %4" : "=s"(r) : "s"(a), "s"(b), "s"(x), "s"(y) : "scc");
-  return r;
-}
-
 // Packed fp32 (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth of FMAs per issue slot).
 typedef float f2v __attribute__((ext_vector_type(2)));
 // x . w over one feature chunk: even features accumulate in .x, odd ones in .y (one packed FMA per
@@ -1168,8 +1154,16 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   const __amdgpu_buffer_rsrc_t yrs =
       LOSS == kLossCEIndex ? buffer_rsrc(a.Yi, n_rows * 8u) : buffer_rsrc(a.Yf, n_rows * (uint32_t)(DOUT * 4));
   const uint32_t ldx4 = (uint32_t)ldx * 4u, k04 = (uint32_t)k0 * 4u;
+  // loss scales of a full batch and of the one short last batch (nb_last == B if none); each batch
+  // carries its pair, selected at fetch time (off the step's dependent chain)
+  const int nb_last = ns_arg - (S - 1) * B;
+  const float inv_full = 1.f / (float)((LOSS == kLossMSE) ? B * DOUT : B);
+  const float inv_last = 1.f / (float)((LOSS == kLossMSE) ? nb_last * DOUT : nb_last);
+  const float gs_full = a.grad_scale * inv_full, gs_last = a.grad_scale * inv_last;
   auto load_batch = [&](Batch<R, KP, DOUT, RY>& f, const int (&sel)[R], int sel_y, int nb) {
     f.nb = nb;
+    f.cg = nb == B ? gs_full : gs_last;
+    f.cl = nb == B ? inv_full : inv_last;
 #pragma unroll
     for (int rho = 0; rho < R; ++rho) buffer_load_chunk<KP>(xrs, __umul24((uint32_t)sel[rho], ldx4) + k04, f.x[rho]);
 #pragma unroll
@@ -1283,9 +1277,6 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
   tk.acc = reinterpret_cast<unsigned long long*>(elist + 2 * estride);
   if (tk.on && lane == 0)
     for (int k = 0; k < 8; ++k) tk.acc[k] = 0ull;
-  const int nb_last = pa.num_samples - (S - 1) * B;  // the one short batch size (== B if none)
-  const float inv_full = 1.f / (float)((LOSS == kLossMSE) ? B * DOUT : B);
-  const float inv_last = 1.f / (float)((LOSS == kLossMSE) ? nb_last * DOUT : nb_last);
   const int64_t t_begin = tk.on ? (int64_t)__builtin_amdgcn_s_memtime() : 0;
   const int64_t r_begin = tk.on ? (int64_t)__builtin_amdgcn_s_memrealtime() : 0;
 
@@ -1303,7 +1294,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
       const float ls0 = z[0] - z[0];  // log_softmax of one class: 0 (NaN if z is not finite)
       if constexpr (LOSS == kLossCESoft) {
         l = -y[0] * ls0;
-        g[0] = (ls0 + 1.f) * y[0] - y[0];
+        g[0] = fmaf(ls0, y[0], 0.f);  // exp(ls0) y - y: the same bits (+0, or NaN), one op shorter
       } else {
         const bool use = yi != a.ignore_index;
         g[0] = use ? (ls0 + 1.f) - (yi == 0 ? 1.f : 0.f) : 0.f;
@@ -1355,10 +1346,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
     for (int k = 0; k < KP; ++k) Gk[c][k] = 0.f;
   }
   int rslot = 0;  // loss ring slot of the next step
-  // uniform loss scales of a full and of the short last batch (SGPRs: a per-step select is SALU)
-  const float inv_full_u = uniform_f(inv_full), inv_last_u = uniform_f(inv_last);
   const float lr_b = hb ? lr : 0.f;  // plain SGD's bias step
-  const float gs_full = uniform_f(a.grad_scale * inv_full), gs_last = uniform_f(a.grad_scale * inv_last);
   auto train = [&](Batch<R, KP, DOUT, RY>& f, int step, auto sgd_tag, auto ring_tag) {
     constexpr int SGD = decltype(sgd_tag)::value;
     constexpr bool MOM = SGD == kSgdMom;
@@ -1389,7 +1377,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
       const bool owner = R == 4 || q < 2;
       lsum = owner ? l : 0.f;
       csum = owner ? cnt : 0.f;
-      if constexpr (LOSS != kLossCEIndex) gz *= select_eq_u(nb, B, gs_full, gs_last);  // 1/B once
+      if constexpr (LOSS != kLossCEIndex) gz *= f.cg;  // 1/B once
       if constexpr (R == 2) {
         const F2 r = pl16(gz, gz);  // rows [g0, g0, g0, g0], [g1, g1, g1, g1]
         g[0][0] = r.a;
@@ -1426,7 +1414,7 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
       csum = wave_sum(csum);
       inv_denom = 1.f / (csum > 0.f ? csum : 1.f);
     } else {
-      inv_denom = select_eq_u(nb, B, inv_full_u, inv_last_u);
+      inv_denom = f.cl;
     }
     // SCATTER already applied the scale to dL/dz before the all-gather
     const float coef = (SCATTER && LOSS != kLossCEIndex) ? 1.f : a.grad_scale * inv_denom;

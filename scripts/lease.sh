@@ -119,6 +119,10 @@ for s in "$@"; do
                  share linab_base $W --steps 2000 --warmup 200 --no_ref --no_mlp_side
                  unset PTDT_EXT_PATH
                done; done ;;
+    lwab)      # driver command with 0 / 8 / 32 zero-step launch-path warm-ups (PTDT_BENCH_LAUNCH_WARM), interleaved
+               for r in 1 2 3 4; do for k in 0 8 32; do
+                 jstep lwab_$k 120 env PTDT_BENCH_LAUNCH_WARM=$k python3 bench.py --gpus 1 --steps 20 --warmup 5 --no_ref --no_mlp_side
+               done; done ;;
     llab)      # single-wave chunked exchange poll loop: this tree vs tools/bin/_C_{nosleep,llpipe}.so, W = 4, 8
                for r in 1 2; do for W in 4 8; do
                  share llab_base $W --steps 2000 --warmup 200 --no_ref --no_mlp_side
@@ -164,6 +168,7 @@ for s in "$@"; do
                jstep tl0_stamps 300 python3 bench.py --steps 20 --warmup 5 --stamps --no_mlp_side --no_ref
                step prof_tl0 300 rocprofv3 --kernel-trace --hip-trace --stats --output-format csv -d "$O/prof_${T}_tl0" -o run -- python3 bench.py --steps 20 --warmup 5 --no_mlp_side --no_ref ;;
     tl)        jstep timeline 300 python3 tools/driver_timeline.py ;;
+    tlpin)     jstep tlpin 300 python3 tools/driver_timeline.py --variants bench,pinned,bench,pinned,nostamp ;;
     memset)    jstep memset_probe 600 python3 benchmarks/graph_memset_probe.py ;;
     memsyn)    jstep memset_syn 300 python3 benchmarks/graph_memset_probe.py --synthetic ;;
     memtrace)  step prof_memtrace 600 rocprofv3 --kernel-trace --output-format csv -d "$O/prof_${T}_memtrace" -o run -- python3 benchmarks/graph_memset_probe.py --trace_only

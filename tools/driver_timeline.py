@@ -19,6 +19,7 @@ its counter; the offset comes from the tightest round trips, +-rtt/2).
 
 Variants (one JSON line each, medians over the reps, plus the calibration line):
   bench    the bench's exact sequence (comm.barrier + sync before, launch, torch sync)
+  pinned   as bench, on a stream restricted to CU 0 (every launch lands where the previous one ran)
   spin     as bench, but the host first spins on the kernel's final stamp, then syncs
            (how long the synchronize takes once the kernel's last store is visible)
   hipsync  hipDeviceSynchronize straight from C++ instead of torch.cuda.synchronize
@@ -91,6 +92,9 @@ def main(argv=None):
     losses = torch.zeros(max(a.steps, a.warmup, 1), device=dev)
     plan = eng.persistent_plan(X, Y, args.batch_size, sampler, cursor, losses)
     hm = C.HostMapped(8)
+    # "pinned": the bench sequence on a stream restricted to CU 0 (hipExtStreamCreateWithCUMask), so every
+    # launch finds the previous one's instruction cache, L1 / TLB and XCD L2 state
+    pin = torch.cuda.ExternalStream(C.cu_masked_stream(dev.index, [0]), device=dev) if "pinned" in a.variants else None
     warm = torch.empty(64 << 20, device=dev)  # 256 MiB for the power-state ramp variants
     pos = 0
     plan.launch_at(a.warmup, pos)
@@ -139,6 +143,13 @@ def main(argv=None):
                 h0, h1, waited = plan.launch_wait_at(a.steps, pos, int(var[4:]))
                 torch.cuda.synchronize(dev)
                 h2 = C.mono_ns()
+            elif var == "pinned":
+                with torch.cuda.stream(pin):
+                    h0 = C.mono_ns()
+                    plan.launch_at(a.steps, pos)
+                    h1 = C.mono_ns()
+                    torch.cuda.synchronize(dev)
+                    h2 = C.mono_ns()
             else:
                 h0 = C.mono_ns()
                 plan.launch_at(a.steps, pos)
