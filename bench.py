@@ -609,10 +609,7 @@ def _rehearse(comm, dev, plan, n_warm: int) -> None:
         k = n_warm // reh + (1 if r < n_warm % reh else 0)
         _untimed(comm, dev, lambda k=k, p0=p0: plan.launch_at(k, p0))
         p0 += k
-    # PTDT_BENCH_LAUNCH_WARM=<k>: k more launches of ZERO steps through the same sequence (the engine's
-    # prologue and final stores only: no training step, parameters and cursor unchanged)
-    for _ in range(int(os.environ.get("PTDT_BENCH_LAUNCH_WARM", "0"))):
-        _untimed(comm, dev, lambda: plan.launch_at(0, p0))
+
 
 
 def _timed(comm, dev, fn, label: str = "headline"):

@@ -119,10 +119,6 @@ for s in "$@"; do
                  share linab_base $W --steps 2000 --warmup 200 --no_ref --no_mlp_side
                  unset PTDT_EXT_PATH
                done; done ;;
-    lwab)      # driver command with 0 / 8 / 32 zero-step launch-path warm-ups (PTDT_BENCH_LAUNCH_WARM), interleaved
-               for r in 1 2 3 4; do for k in 0 8 32; do
-                 jstep lwab_$k 120 env PTDT_BENCH_LAUNCH_WARM=$k python3 bench.py --gpus 1 --steps 20 --warmup 5 --no_ref --no_mlp_side
-               done; done ;;
     llab)      # single-wave chunked exchange poll loop: this tree vs tools/bin/_C_{nosleep,llpipe}.so, W = 4, 8
                for r in 1 2; do for W in 4 8; do
                  share llab_base $W --steps 2000 --warmup 200 --no_ref --no_mlp_side
