@@ -479,15 +479,7 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
     fp.n = (uint32_t)k[7];
     return fp;
   };
-  // lanes 0-2 of wave 0: epochs e0+1 .. e0+3 (every wave count has them: NW = 1 runs two waves); lane 3
-  // invalidates the fourth slot, whose tag is LDS left over from an earlier kernel on this CU: a stale
-  // tag equal to a later epoch made the producer skip that epoch's keys and cycle-walk another launch's
-  // permutation (sample count N' != N: the walk from an input >= 2^bits' never ends)
-  if (feistel && tid < 4) {
-    if (tid < 3) keys_store(e0 + 1 + tid);
-    else fkeys[(e0 & 3) * 12 + 8] = -0x7fffffff - 1;
-  }
-  pstamp(2);  // epoch e0+1's list up to the cursor, Feistel keys
+  pstamp(2);  // epoch e0+1's list up to the cursor (the Feistel keys follow the next barrier)
   // staged batch slots: zeros, and the constant-1 input column (b1 rides in W1's
   // column Din) in X and X^T; the per-step writes only touch columns < Din
   // (16-B zero stores, then the constant-1 entries after a barrier: the per-element index
@@ -511,9 +503,19 @@ __global__ void __launch_bounds__(kTpThreadsMax) mlp_tp_kernel(FusedMlpArgs a, P
       }
     }
   }
-  pstamp(3);  // lists, keys, staging-slot init (and the compute waves' state loads) done
+  pstamp(3);  // lists, staging-slot init (and the compute waves' state loads) done
   __syncthreads();
   pstamp(4);
+  // Feistel keys of epochs e0+1 .. e0+3 (read only by the helper wave, after barrier 1 of step 0):
+  // lanes 0-2 of wave 0 while the helper stages step 0 below, where the compute waves only wait (before
+  // the first barrier they were ~0.5 us of every launch's prologue). Lane 3 invalidates the fourth slot,
+  // whose tag is LDS left over from an earlier kernel on this CU: a stale tag equal to a later epoch made
+  // the producer skip that epoch's keys and cycle-walk another launch's permutation (sample count
+  // N' != N: the walk from an input >= 2^bits' never ends).
+  if (feistel && w == 0 && l < 4) {
+    if (l < 3) keys_store(e0 + 1 + l);
+    else fkeys[(e0 & 3) * 12 + 8] = -0x7fffffff - 1;
+  }
   if (tid == 0 && pa.idx == nullptr) {
     list_cache_publish(lc, e0);
     list_cache_publish(lc, e0 + 1);
