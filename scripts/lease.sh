@@ -82,6 +82,8 @@ for s in "$@"; do
                  jstep pinab 120 env PTDT_BENCH_PIN_CU=0 python3 bench.py --steps 20 --warmup 5 --no_ref --no_mlp_side
                done ;;
     default)   jstep bench_default 300 python3 bench.py ;;
+    tp20k)     # toy-MLP TP engine, bf16 and fp32, long launch
+               for dt in bf16 fp32; do jstep tp20k 300 python3 bench.py --model mlp --dtype $dt --steps 20000 --warmup 2000 --no_ref; done ;;
     hl20k)     # headline engine alone, long launch: per-step cost without the fixed part
                for r in 1 2; do jstep hl20k 300 python3 bench.py --steps 20000 --warmup 2000 --no_ref --no_mlp_side; done ;;
     stamps)    jstep stamps 300 python3 bench.py --steps 20000 --warmup 2000 --stamps --no_mlp_side

@@ -122,6 +122,8 @@ def test_stream_pipeline_one_gpu_matches_single_queue(dev, channels_last):
             assert a._stage_streams is not None and b._stage_streams is None  # the stream schedule ran
             torch.testing.assert_close(outs[0][0], outs[1][0], rtol=1e-5, atol=1e-6)
             worst = max(((ga - gb).abs().max() / (gb.abs().max() + 1e-30)).item() for ga, gb in zip(outs[0][1], outs[1][1]))
-            assert worst <= 1e-5, worst
+            # rounding-order differences between the two schedules measured up to 1.02e-5 (round 6, one
+            # box; <= 6e-6 on others); the unsynchronised residual link gave 1e-2 .. 9e-2
+            assert worst <= 5e-5, worst
     finally:
         torch.backends.cudnn.deterministic = det
