@@ -73,7 +73,7 @@ for s in "$@"; do
                  jstep rehab 120 env PTDT_BENCH_REHEARSALS=$r python3 bench.py --steps 20 --warmup 5 --no_ref --no_mlp_side
                done; done ;;
     rehab2)    # A/B of 3 vs 5 rehearsal launches, interleaved, headline only
-               for i in 1 2 3 4; do for r in 3 5; do
+               for i in 1 2 3 4 5 6; do for r in 3 5; do
                  jstep rehab2 120 env PTDT_BENCH_REHEARSALS=$r python3 bench.py --steps 20 --warmup 5 --no_ref --no_mlp_side
                done; done ;;
     pinab)     # A/B: default vs the persistent launches pinned to one CU (PTDT_BENCH_PIN_CU), interleaved
