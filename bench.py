@@ -318,7 +318,9 @@ def run_persistent(args, rank, world, dev, comm, dec):
         # the W warm-up steps: launches through the timed region's own sequence (_untimed) when they
         # fit, so the timed launch below is not the first of its kind in this process
         # (PTDT_BENCH_REHEARSALS: into how many such launches the W steps are split; interleaved A/B at
-        # the driver's W = 5: 1 -> 28.2-30.9 us window, 2 -> 25.0-26.1, 3 -> 24.8-26.1; default 3)
+        # the driver's W = 5: 1 -> 28.2-30.9 us window, 2 -> 25.0-26.1, 3 -> 24.8-26.1 (round 5); round 6,
+        # 6 interleaved pairs (profiles/r6_rehearsals_ab.jsonl): 3 -> 23.7-25.2, 5 -> 23.1-26.2 (median 23.7
+        # vs 24.6); default 5, i.e. every warm-up step of the driver command its own launch)
         if n_warm <= chunk:
             with pin_ctx:
                 _rehearse(comm, dev, plan, n_warm)
@@ -603,7 +605,7 @@ def _untimed(comm, dev, fn) -> None:
 def _rehearse(comm, dev, plan, n_warm: int) -> None:
     """Run exactly ``n_warm`` warm-up steps of a persistent plan (positions 0 .. n_warm-1) as
     PTDT_BENCH_REHEARSALS launches through the timed region's own sequence (_untimed)."""
-    reh = max(1, min(n_warm, int(os.environ.get("PTDT_BENCH_REHEARSALS", "3"))))
+    reh = max(1, min(n_warm, int(os.environ.get("PTDT_BENCH_REHEARSALS", "5"))))
     p0 = 0
     for r in range(reh):
         k = n_warm // reh + (1 if r < n_warm % reh else 0)
