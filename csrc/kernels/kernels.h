@@ -99,7 +99,10 @@ struct PersistArgs {
 // it supports the configuration.
 // kPersistWaveRows / kPersistWaveF restrict the wave engine to one lane-layout
 // family (row groups across DPP rows / feature groups across DPP rows).
-constexpr int kWavePrefetch = 3;  // batches in flight in the wave engine (register buffers)
+#ifndef PTDT_WAVE_PREFETCH
+#define PTDT_WAVE_PREFETCH 3
+#endif
+constexpr int kWavePrefetch = PTDT_WAVE_PREFETCH;  // batches in flight in the wave engine (register buffers)
 // FusedMlpArgs::ldx of an engine-choice query (persistent_engine()): any row stride, the caller pads
 // X rows to the chosen layout's width
 constexpr int kWaveLdxAny = 1 << 20;

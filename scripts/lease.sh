@@ -121,6 +121,15 @@ for s in "$@"; do
                  share linab_base $W --steps 2000 --warmup 200 --no_ref --no_mlp_side
                  unset PTDT_EXT_PATH
                done; done ;;
+    pfab)      # wave-engine prefetch depth: this tree (3) vs tools/bin/_C_pf2.so (2), driver command + 20k steps
+               for r in 1 2 3 4; do
+                 jstep pfab_3 120 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no_ref --no_mlp_side
+                 jstep pfab_2 120 env PTDT_EXT_PATH=$PWD/tools/bin/_C_pf2.so python3 bench.py --gpus 1 --steps 20 --warmup 5 --no_ref --no_mlp_side
+               done
+               for r in 1 2; do
+                 jstep pfab20k_3 300 python3 bench.py --steps 20000 --warmup 2000 --no_ref --no_mlp_side
+                 jstep pfab20k_2 300 env PTDT_EXT_PATH=$PWD/tools/bin/_C_pf2.so python3 bench.py --steps 20000 --warmup 2000 --no_ref --no_mlp_side
+               done ;;
     llab)      # single-wave chunked exchange poll loop: this tree vs tools/bin/_C_{nosleep,llpipe}.so, W = 4, 8
                for r in 1 2; do for W in 4 8; do
                  share llab_base $W --steps 2000 --warmup 200 --no_ref --no_mlp_side
