@@ -1252,19 +1252,28 @@ __global__ void __launch_bounds__(kThreads) linear_wave_f_kernel(FusedMlpArgs a,
 
   int ie = e0, ij = j0, barriers = 0;
   int sel_next[R], sel_y_next = 0, nb_next = 0;
+  // running LDS entry offset of position (ie, ij) and a barrier owed by the last epoch wrap: the
+  // per-step bookkeeping is an add and a compare (it was the list base, ij * B and the three-way
+  // barrier condition recomputed every step)
+  int lofs = (ie & 1) * estride + ij * B;
+  bool bar_due = false;
   auto read_index = [&]() {
-    if (ij == 0 && ie != e0 && barriers < T) {
+    if (bar_due) {  // new epoch: its list is ready, the old one free
       __syncthreads();
       ++barriers;
+      bar_due = false;
     }
-    nb_next = min(B, pa.num_samples - ij * B);
+    nb_next = ij == S - 1 ? nb_last : B;
 #pragma unroll
-    for (int rho = 0; rho < R; ++rho) sel_next[rho] = list(ie)[ij * B + rho * 16 + i];
+    for (int rho = 0; rho < R; ++rho) sel_next[rho] = elist[lofs + rho * 16 + i];
     if constexpr (SCATTER)  // own row's index read directly: selecting from sel_next[] by a lane value spills it
-      sel_y_next = list(ie)[ij * B + rho_own * 16 + i];
+      sel_y_next = elist[lofs + rho_own * 16 + i];
+    lofs += B;
     if (++ij == S) {
       ij = 0;
       ++ie;
+      lofs = (ie & 1) * estride;
+      bar_due = barriers < T;
     }
   };
   auto fetch = [&](Batch<R, KP, DOUT, RY>& f) {
